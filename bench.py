@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Headline benchmark: atom-frames/s of the frame-parallel RMSF path on MI355X.
+
+  python bench.py [--gpus N --steps K --warmup W]            (N=1)
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+      --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+One "step" = one full RMSF pass of the hot path over the rank's frame block
+(the per-frame Welford accumulator over every frame, the in-GPU Chan merge of
+the frame tiles, the cross-GPU Chan merge over RCCL, the finalise), with the
+synthetic trajectory already resident in HBM.  Workload per GPU (weak
+scaling, frame-sharded by the RMSF.py:65-69 blocks):
+  c2 (default): 100k atoms x 20k frames fp32 per GPU, no alignment
+                (BASELINE.json configs[1]); N GPUs hold 20k*N frames.
+  c4:           1M atoms x 2.5k frames per GPU (at N=8 = configs[3], 240 GB).
+At N=1 the aligned configurations are measured too and reported under
+"modes" (C3 = QCP alignment to frame 0; RMSF.py's own two-sweep "average").
+
+Rank 0 prints ONE JSON line.  ``roofline`` is measured live with HIP events
+around the dominant kernel (k_welford_flat) on its launch stream;
+``cpu_baseline`` is the oracle's numpy restatement of RMSF.py's per-rank loop
+timed on this host's cores (run before the GPU is touched).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mdanalysis-mpi_amd")]
+
+HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip table)
+FP64_PEAK_TFS = 78.6    # MI355X fp64 vector spec (not in the local guide, unverified)
+B_PER_ATOM_FRAME = 12   # algorithmic bytes per (atom, frame) per sweep
+FLOP_PER_ATOM_FRAME_SUPERPOSE = 27  # covariance 18 + |x|^2 6 + COM 3
+
+WORKLOADS = {
+    "c2": dict(n_atoms=100_000, frames_per_gpu=20_000, align=None,
+               name="C2: synthetic 100k atoms x 20k frames fp32 per GPU, no alignment, fp64 Welford"),
+    "c3": dict(n_atoms=100_000, frames_per_gpu=20_000, align="frame0",
+               name="C3: synthetic 100k atoms x 20k frames fp32 per GPU, QCP alignment to frame 0"),
+    "average": dict(n_atoms=100_000, frames_per_gpu=20_000, align="average",
+                    name="RMSF.py two-sweep: 100k atoms x 20k frames per GPU, align to frame 0, average, re-align"),
+    "c4": dict(n_atoms=1_000_000, frames_per_gpu=2_500, align=None,
+               name="C4 share: synthetic 1M atoms x 2.5k frames fp32 per GPU (N=8: 1M x 20k, 240 GB)"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
+    ap.add_argument("--n-atoms", type=int, default=None)
+    ap.add_argument("--frames-per-gpu", type=int, default=None)
+    ap.add_argument("--splits", type=int, default=None)
+    ap.add_argument("--batch-frames", type=int, default=None, help="aligned modes: frames per superpose batch")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=64, help="frames per CPU process in the baseline sample")
+    ap.add_argument("--no-modes", action="store_true", help="skip the aligned-mode measurements at N=1")
+    ap.add_argument("--mode-steps", type=int, default=3)
+    return ap.parse_args()
+
+
+def load_traffic(workload: str, n_atoms: int, n_frames: int):
+    """HBM bytes per launch of the dominant kernel from the committed PMC
+    summary (profiles/pmc_<workload>.json, written by tools/pmc_summary.py
+    from separate rocprofv3 --pmc passes), if one exists for this shape."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        if d.get("n_atoms") == n_atoms and d.get("n_frames") == n_frames:
+            return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    wl = dict(WORKLOADS[a.workload])
+    if a.n_atoms:
+        wl["n_atoms"] = a.n_atoms
+    if a.frames_per_gpu:
+        wl["frames_per_gpu"] = a.frames_per_gpu
+    n_atoms, per_gpu = wl["n_atoms"], wl["frames_per_gpu"]
+
+    # -- CPU baseline first: no process has touched the GPU yet ---------------
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import cpu_baseline
+        cpu = cpu_baseline.run(n_atoms, a.cpu_frames, align="none")
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from rmsf_amd import parallel
+    from rmsf_amd.engine import Engine
+    from rmsf_amd.pipeline import KernelTimer, run_pipeline
+    from rmsf_amd.sources import DeviceSource, FrameList
+    from rmsf_amd.synth import generate, motion_table
+
+    eng = Engine(torch.device("cuda", local))
+    n_total = per_gpu * world
+    b0, b1 = parallel.blocks(n_total, world)[rank]
+    n_local = b1 - b0
+    motion = motion_table(1, n_total) if wl["align"] else None
+    traj = generate(eng, n_atoms, b0, n_local, seed=0, motion=motion)
+    torch.cuda.synchronize()
+    src = DeviceSource(traj, offset=b0, n_traj=n_total)
+    fl = FrameList(n_total)
+
+    def run(align, timer=None):
+        return run_pipeline(eng, src, fl, align=align, block=(b0, b1), ref_owner=0, n_splits=a.splits,
+                            max_batch=a.batch_frames, timer=timer)
+
+    def timed(align, steps, warmup):
+        timer = KernelTimer()
+        for _ in range(warmup):
+            run(align)
+        torch.cuda.synchronize()
+        parallel.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            res = run(align, timer)
+        torch.cuda.synchronize()
+        parallel.barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device=eng.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt, timer, res
+
+    dt, timer, res = timed(wl["align"], a.steps, a.warmup)
+    value = n_total * n_atoms * a.steps / dt
+    acc_ms = timer.ms("accumulate")
+    kern_s = sum(acc_ms) / len(acc_ms) / 1e3
+    bytes_launch = B_PER_ATOM_FRAME * n_atoms * n_local
+    achieved = bytes_launch / kern_s / 1e9
+    traffic = load_traffic(a.workload, n_atoms, n_local)
+    out = {
+        "metric": "atom-frames/sec (RMSF) + achieved HBM GB/s fraction",
+        "value": value,
+        "unit": "atom-frames/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: counter-based generator, fp32 frames resident in HBM (generated on device)",
+        "config": {"workload": wl["name"], "n_atoms": n_atoms, "n_frames_per_gpu": per_gpu,
+                   "n_frames_total": n_total, "selection": "all atoms", "align": wl["align"],
+                   "parallelism": f"frame-sharded x{world} (RMSF.py:65-69 blocks), RCCL Chan merge"},
+        "roofline": {"bound": "hbm", "kernel": "k_accum_atoms" if wl["align"] else "k_welford_flat",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic, "algorithmic_bytes_per_launch": bytes_launch,
+                     "avg_launch_ms": kern_s * 1e3, "launches": len(acc_ms)},
+        "cpu_baseline": cpu,
+        "pipeline_hbm_gbs": B_PER_ATOM_FRAME * n_atoms * n_local * a.steps / dt / 1e9 * (1 if not wl["align"] else 1),
+    }
+    if wl["align"]:
+        sup_ms = timer.ms("superpose")
+        if sup_ms:
+            s = sum(sup_ms) / len(sup_ms) / 1e3
+            out["superpose"] = {"avg_launch_ms": s * 1e3,
+                                "gflops": FLOP_PER_ATOM_FRAME_SUPERPOSE * n_atoms * n_local / s / 1e9,
+                                "fp64_peak_tflops_spec": FP64_PEAK_TFS,
+                                "hbm_gbs": B_PER_ATOM_FRAME * n_atoms * n_local / s / 1e9}
+
+    # -- aligned modes at N=1 (reported beside the headline) ------------------
+    if world == 1 and not a.no_modes and wl["align"] is None:
+        del traj, src
+        torch.cuda.empty_cache()
+        motion = motion_table(1, n_total)
+        traj = generate(eng, n_atoms, b0, n_local, seed=0, motion=motion)
+        torch.cuda.synchronize()
+        src = DeviceSource(traj, offset=b0, n_traj=n_total)
+        modes = {}
+        for name, align in (("c3_frame0", "frame0"), ("rmsf_py_average", "average")):
+            mdt, mt, _ = timed(align, a.mode_steps, 1)
+            sweeps = 2 if align == "average" else 1
+            sup = mt.ms("superpose")
+            acc = mt.ms("accumulate")
+            af = n_total * n_atoms * a.mode_steps / mdt
+            modes[name] = {
+                "atom_frames_per_s": af,
+                "ms_per_step": mdt / a.mode_steps * 1e3,
+                "sweeps": sweeps,
+                "hbm_gbs_algorithmic": af * B_PER_ATOM_FRAME * sweeps / 1e9,
+                "superpose_avg_ms": sum(sup) / len(sup),
+                "superpose_gflops": FLOP_PER_ATOM_FRAME_SUPERPOSE * n_atoms * n_local / (sum(sup) / len(sup) / 1e3) / 1e9,
+                "accumulate_avg_ms": sum(acc) / len(acc),
+                "accumulate_hbm_gbs": B_PER_ATOM_FRAME * n_atoms * n_local / (sum(acc) / len(acc) / 1e3) / 1e9,
+            }
+        out["modes"] = modes
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,210 @@
+/*
+ * rmsf_hip.h -- C ABI of the MI355X (gfx950) frame-parallel RMSF path.
+ *
+ * This is the drop-in boundary for the hot path of i2nico/MDAnalysis-MPI
+ * `RMSF.py` (the whole reference is that one file).  The reference has no
+ * native FFI of its own: its per-frame loops call numpy, MDAnalysis
+ * `lib.qcprot` (Cython) and mpi4py.  Every entry point below replaces one of
+ * those call sites; the citation `RMSF.py:N` is /root/reference/RMSF.py line N.
+ *
+ * Conventions (all entry points):
+ *   - Plain pointers and sizes only.  `d_` = device pointer (HBM, caller
+ *     owned), `h_` = host pointer.  Coordinates are float32 `fac` layout
+ *     (frame, atom, xyz); statistics are float64.
+ *   - Every call returns an int status: 0 = ok, < 0 = error (see RMSF_E*).
+ *     rmsf_last_error() returns a thread-local message for the last failure.
+ *     No C++ exception crosses the ABI.
+ *   - Device work is enqueued asynchronously on `stream` (a hipStream_t, NULL
+ *     = the legacy default stream).  Nothing synchronises unless stated.
+ *   - `sel` (int32 atom indices into a frame) may be NULL, meaning atoms
+ *     0..n_sel-1 of each frame (the contiguous fast path).
+ *   - `frame_stride` is the distance between consecutive frames in floats
+ *     (>= 3*n_atoms of the frame; a multiple of it implements `step`).
+ */
+#ifndef RMSF_HIP_H
+#define RMSF_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RMSF_ABI_VERSION 1
+
+#define RMSF_OK 0
+#define RMSF_EINVAL (-1)   /* bad argument (shape, null pointer, size)      */
+#define RMSF_EHIP (-2)     /* HIP runtime error                             */
+#define RMSF_ENOMEM (-3)   /* allocation failed / workspace too small       */
+#define RMSF_EEMPTY (-4)   /* no frames to reduce (RMSF.py:39 would raise   */
+                           /* ZeroDivisionError)                            */
+
+/* accumulate modes for rmsf_accumulate() */
+#define RMSF_MODE_WELFORD 0 /* n/mean/M2 per coordinate   (RMSF.py:137-138) */
+#define RMSF_MODE_SUM 1     /* f64 sum of positions        (RMSF.py:103)     */
+
+/* Size of one per-frame transform record written by rmsf_superpose():
+ * R[9] (row-major, applied as x @ R, RMSF.py:100), mobile COM[3], rmsd, pad[3] */
+#define RMSF_XFORM_DOUBLES 16
+/* Size of the reference record written by rmsf_reference_setup():
+ * ref_com[3], sum_r[3] (= sum of centred ref coords), G_ref (= sum |r|^2),
+ * total mass, n_sel, pad[7]                                                   */
+#define RMSF_REFINFO_DOUBLES 16
+
+/* ---- library / device helpers (for callers without their own allocator) */
+int rmsf_abi_version(void);
+const char *rmsf_last_error(void);
+int rmsf_device_count(int *n);
+int rmsf_set_device(int dev);
+int rmsf_malloc(void **d_ptr, size_t bytes);
+int rmsf_free(void *d_ptr);
+int rmsf_memcpy_h2d(void *d_dst, const void *h_src, size_t bytes, void *stream);
+int rmsf_memcpy_d2h(void *h_dst, const void *d_src, size_t bytes, void *stream);
+int rmsf_stream_synchronize(void *stream);
+
+/* ---- frame-block decomposition: RMSF.py:63-72 ----------------------------
+ * per = n_frames // size; ranks 0..size-2 get [r*per, (r+1)*per); the last
+ * rank gets [(size-1)*per, n_frames).  Pure integer, bit-exact.            */
+int rmsf_block_range(int64_t n_frames, int size, int rank, int64_t *start,
+                     int64_t *stop);
+
+/* ---- reference structure: RMSF.py:80-87 (frame `ref_frame`, float32) and
+ * RMSF.py:113-118 (the all-reduced float64 average) -------------------------
+ * Exactly one of d_frame (float32 frame, atoms addressed via sel) or d_avg
+ * (float64 [n_sel*3], already the selection) is non-NULL.
+ * ref_com = sum(m x)/sum(m) in f64 (center_of_mass, RMSF.py:84,117);
+ * d_ref[n_sel*3] = x - ref_com (f64, RMSF.py:85,118); d_refinfo as above.  */
+int rmsf_reference_setup(const float *d_frame, const double *d_avg,
+                         int64_t n_sel, const int32_t *d_sel,
+                         const double *d_masses, double *d_ref,
+                         double *d_refinfo, void *stream);
+
+/* ---- superposition: RMSF.py:94-97,127-131 + get_rotation_matrix RMSF.py:43-51
+ * For every frame f of the block: mobile COM (mass-weighted, f64), the 3x3
+ * inner product A = sum (x-com) (x) ref and E0 against the centred reference
+ * (qcprot InnerProduct), then the QCP rotation (qcprot FastCalcRMSDAndRotation,
+ * Theobald 2005 / Liu 2010) -> d_xform[f*RMSF_XFORM_DOUBLES + ...].
+ * Two launches: a (frame, atom-chunk) covariance reduction and a per-frame
+ * QCP solve.  d_work must hold rmsf_superpose_workspace_bytes() bytes.     */
+size_t rmsf_superpose_workspace_bytes(int64_t n_sel, int64_t n_frames);
+int rmsf_superpose(const float *d_xyz, int64_t frame_stride, int64_t n_frames,
+                   int64_t n_sel, const int32_t *d_sel,
+                   const double *d_masses, const double *d_ref,
+                   const double *d_refinfo, double *d_xform, void *d_work,
+                   size_t work_bytes, void *stream);
+
+/* ---- streaming accumulator: RMSF.py:99-103 (SUM) and RMSF.py:133-138 (WELFORD)
+ * For each frame: if d_xform != NULL apply the f32-faithful transform of
+ * RMSF.py:99-101 / 133-135
+ *     p = f32(f64(p) - com_f); p = f32(f64(p) @ R_f); p = f32(f64(p) + ref_com)
+ * (ref_com from d_refinfo), then x = f64(p) feeds
+ *   WELFORD: M2 += k/(k+1) (x-mean)^2 ; mean = (k mean + x)/(k+1)
+ *   SUM:     sum += x
+ * Frames are cut into n_splits contiguous splits (frame tiles); split s
+ * holds frames [n_frames*s/n_splits, n_frames*(s+1)/n_splits) and writes
+ * d_out0[s*3*n_sel + j] (mean or sum) and, for WELFORD, d_out1 (M2).
+ * n_splits <= 0 picks one (see rmsf_accumulate_splits()).  The partials are
+ * folded by rmsf_chan_merge() / rmsf_sum_splits().                          */
+int rmsf_accumulate_splits(int64_t n_sel, int64_t n_frames, int aligned);
+int rmsf_accumulate(const float *d_xyz, int64_t frame_stride, int64_t n_frames,
+                    int64_t n_sel, const int32_t *d_sel,
+                    const double *d_xform, const double *d_refinfo, int mode,
+                    int n_splits, double *d_out0, double *d_out1,
+                    void *stream);
+
+/* split s of rmsf_accumulate() holds this many frames */
+int64_t rmsf_split_count(int64_t n_frames, int n_splits, int s);
+
+/* ---- Chan merge: second_order_moments, RMSF.py:36-41 ------------------------
+ * Folds n_parts partial (count, mean, M2) sets of n_coord coordinates, in
+ * order 0..n_parts-1, with T=n1+n2, mu=(n1 mu1+n2 mu2)/T,
+ * M=M1+M2+(n1 n2/T)(mu2-mu1)^2.  Empty partials are skipped (RMSF.py:39
+ * raises ZeroDivisionError when both are empty; Appendix B Q5).
+ * h_counts is a host array of n_parts counts.                               */
+int rmsf_chan_merge(const double *d_mean_parts, const double *d_m2_parts,
+                    const int64_t *h_counts, int n_parts, int64_t n_coord,
+                    double *d_mean, double *d_m2, void *stream);
+
+/* sum of split partial sums (sweep 1, RMSF.py:103,105) */
+int rmsf_sum_splits(const double *d_parts, int n_parts, int64_t n_coord,
+                    double *d_sum, void *stream);
+
+/* y = x / divisor  (average structure, RMSF.py:111) */
+int rmsf_divide(const double *d_x, double divisor, int64_t n, double *d_y,
+                void *stream);
+
+/* Exact k-way Chan across ranks as two all-reduce(SUM) passes (replaces the
+ * pickle comm.reduce of RMSF.py:143):
+ *   pass 1 input: d_out = w * mean_k            (w = n_k / n)
+ *   pass 2 input: d_out = M2_k + n_k (mean_k - mean)^2                      */
+int rmsf_chan_weight(const double *d_mean_k, double w, int64_t n,
+                     double *d_out, void *stream);
+int rmsf_chan_deviation(const double *d_mean_k, const double *d_m2_k,
+                        const double *d_mean, double n_k, int64_t n,
+                        double *d_out, void *stream);
+
+/* ---- finalise: RMSF.py:146  rmsf = sqrt(M2.sum(axis=1) / n) ---------------*/
+int rmsf_finalize(const double *d_m2, int64_t n_sel, int64_t n_frames,
+                  double *d_rmsf, void *stream);
+
+/* ---- qcprot.CalcRMSDRotationalMatrix (RMSF.py:48) --------------------------
+ * Batched QCP on device: A[n][9], E0[n], atom counts N[n] -> rot[n][9],
+ * rmsd[n].  Exposed for the upstream known-answer test.                      */
+int rmsf_qcp_batch(const double *d_A, const double *d_E0, const double *d_N,
+                   int64_t n, double *d_rot, double *d_rmsd, void *stream);
+
+/* Host-pointer form with the signature of
+ * MDAnalysis.lib.qcprot.CalcRMSDRotationalMatrix(ref, conf, N, rot, weights)
+ * (called at RMSF.py:48): ref/conf f64 [N][3] (already centred by the
+ * caller), rot f64[9] out, weights NULL or f64[N].  Runs on the current
+ * device, synchronous.  *rmsd_out receives the rmsd.                        */
+int rmsf_calc_rmsd_rotational_matrix(const double *h_ref, const double *h_conf,
+                                     int64_t N, double *h_rot,
+                                     const double *h_weights,
+                                     double *rmsd_out);
+
+/* ---- synthetic trajectories -------------------------------
+ * out[f*frame_stride + 3*a + c] for frames [f0, f0+nf) of n_atoms atoms:
+ *   base(a,c) ~ U[0,100), sigma(a) ~ U[0.2,2.0), g ~ triangular, unit var,
+ *   p = base + sigma*g ; optional rigid motion from d_motion[f][12]
+ *   (R[9] row-major, t[3]):  p' = ((p-50) @ R) + t ; out = f32(p').
+ * Counter-based (splitmix64 of seed/frame/atom/axis) with every float op
+ * explicitly rounded, so the CPU regenerates any slice bit-identically.     */
+int rmsf_synth_frames(float *d_out, int64_t frame_stride, int64_t n_atoms,
+                      int64_t f0, int64_t nf, uint64_t seed,
+                      const double *d_motion, void *stream);
+
+/* ---- host -> device frame stager (north star subsystem 1) ---
+ * Pinned-host, multi-buffered hipMemcpyAsync stager.  Frames arrive as host
+ * float32 arrays of n_atoms_frame atoms; the selection (h_sel, NULL = first
+ * n_sel atoms) is gathered on the host into a pinned slot by a thread pool,
+ * the slot is copied on the stager's own copy stream, and the consumer
+ * stream is made to wait on the copy event.  A slot is reused only after
+ * the consumer released it (an event recorded on the consumer stream).     */
+typedef struct rmsf_stager rmsf_stager;
+int rmsf_stager_create(int64_t n_atoms_frame, int64_t n_sel,
+                       const int32_t *h_sel, int64_t batch_frames,
+                       int n_slots, int n_threads, rmsf_stager **out);
+int rmsf_stager_destroy(rmsf_stager *st);
+/* Stage n_frames (<= batch_frames) host frames (stride h_frame_stride
+ * floats) into the next slot.  Returns the slot index and its device
+ * pointer (compact [n_frames][n_sel][3] layout, frame_stride = 3*n_sel).
+ * `consumer_stream` waits on the copy before any later work it runs.       */
+int rmsf_stager_stage(rmsf_stager *st, const float *h_frames,
+                      int64_t h_frame_stride, int64_t n_frames,
+                      void *consumer_stream, int *slot, float **d_batch);
+/* Stage frames given as an array of n_frames host pointers (one per frame,
+ * each n_atoms_frame*3 floats) -- the per-Timestep MDAnalysis path.        */
+int rmsf_stager_stage_ptrs(rmsf_stager *st, const float *const *h_frame_ptrs,
+                           int64_t n_frames, void *consumer_stream, int *slot,
+                           float **d_batch);
+/* Mark the slot free once the work queued so far on consumer_stream ends. */
+int rmsf_stager_release(rmsf_stager *st, int slot, void *consumer_stream);
+/* Wait until every copy issued by the stager has completed. */
+int rmsf_stager_synchronize(rmsf_stager *st);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RMSF_HIP_H */

@@ -1,0 +1,1036 @@
+// rmsf_kernels.hip -- hand-written HIP kernels for gfx950 (MI355X, CDNA4) and
+// the extern "C" launchers declared in include/rmsf_hip.h.
+//
+// Hot path of /root/reference/RMSF.py (cited as RMSF.py:N):
+//   * k_welford_flat     RMSF.py:137-138, no alignment, contiguous selection.
+//                        HBM-bound stream: 12 B per atom-frame, one float4 per
+//                        lane per frame, fp64 mean/M2 in registers across a
+//                        frame tile (split).
+//   * k_accum_atoms      RMSF.py:99-103 (SUM) and RMSF.py:133-138 (WELFORD)
+//                        with the f32-faithful superposition transform; one
+//                        atom (12 B, global_load_dwordx3) per lane per frame.
+//   * k_frame_stats      per-(frame, atom chunk) reduction of the mobile COM
+//                        and the qcprot inner product (RMSF.py:94-97,127-131).
+//   * k_qcp_frames       per-frame QCP (qcprot FastCalcRMSDAndRotation, the
+//                        published Theobald/Liu algorithm), one wave per frame.
+//   * k_reference        RMSF.py:80-87 / 113-118 reference centring.
+//   * k_chan_merge       second_order_moments, RMSF.py:36-41.
+//   * k_finalize         RMSF.py:146.
+//   * k_synth            counter-based synthetic trajectory generator.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rmsf_hip.h"
+
+#define RMSF_EXPORT __attribute__((visibility("default")))
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(const char *what, hipError_t e) {
+  return fail(RMSF_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                  \
+  do {                                                 \
+    hipError_t e_ = (expr);                            \
+    if (e_ != hipSuccess) return hip_fail(#expr, e_);  \
+  } while (0)
+
+int after_launch(const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(what, e);
+  return RMSF_OK;
+}
+
+inline hipStream_t S(void *stream) { return reinterpret_cast<hipStream_t>(stream); }
+
+constexpr int kBlock = 256;
+constexpr int kXform = RMSF_XFORM_DOUBLES;
+constexpr int kRefInfo = RMSF_REFINFO_DOUBLES;
+constexpr int kStats = 16;       // doubles per (frame, chunk) partial
+constexpr int kStatsAPT = 8;     // atoms per thread in k_frame_stats
+constexpr int kChunkAtoms = kBlock * kStatsAPT;
+
+// ---------------------------------------------------------------------------
+// Welford coefficients a_k = k/(k+1), b_k = 1/(k+1) (RMSF.py:137-138), folded
+// at compile time (IEEE division, identical to numpy's) into a constant table
+// read with scalar loads.  A split never exceeds kCoefN frames.
+constexpr int kCoefN = 4096;
+struct WCoef {
+  double a, b;
+};
+struct WCoefTable {
+  WCoef v[kCoefN];
+};
+constexpr WCoefTable make_coef_table() {
+  WCoefTable t{};
+  for (int k = 0; k < kCoefN; ++k) {
+    t.v[k].a = double(k) / double(k + 1);
+    t.v[k].b = 1.0 / double(k + 1);
+  }
+  return t;
+}
+__constant__ WCoefTable g_coef = make_coef_table();
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void welford(double &m, double &q, double x, const WCoef c) {
+  // M2 += k/(k+1) (x-mean)^2 ; mean = (k mean + x)/(k+1) == mean + (x-mean)/(k+1)
+  const double d = x - m;
+  q = fma(c.a * d, d, q);
+  m = fma(c.b, d, m);
+}
+
+__device__ __forceinline__ int64_t split_begin(int64_t n_frames, int n_splits, int s) {
+  return (n_frames * s) / n_splits;
+}
+
+// ---------------------------------------------------------------------------
+// k_welford_flat: contiguous selection, no alignment (config C2).
+// grid = (ceil(n4/256), n_splits); lane owns 4 consecutive coordinates.
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_welford_flat(
+    const float *__restrict__ xyz, int64_t stride4, int64_t n4, int64_t n_frames,
+    int n_splits, double *__restrict__ out_mean, double *__restrict__ out_m2,
+    int64_t n_coord) {
+  const int64_t i4 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i4 >= n4) return;
+  const int s = blockIdx.y;
+  const int64_t fb = split_begin(n_frames, n_splits, s);
+  const int nf = (int)(split_begin(n_frames, n_splits, s + 1) - fb);
+  const f32x4 *p = reinterpret_cast<const f32x4 *>(xyz) + fb * stride4 + i4;
+
+  double m0 = 0, m1 = 0, m2 = 0, m3 = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+  int k = 0;
+  for (; k + U <= nf; k += U) {
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + (int64_t)(k + u) * stride4);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const WCoef c = g_coef.v[k + u];
+      welford(m0, q0, (double)v[u].x, c);
+      welford(m1, q1, (double)v[u].y, c);
+      welford(m2, q2, (double)v[u].z, c);
+      welford(m3, q3, (double)v[u].w, c);
+    }
+  }
+  for (; k < nf; ++k) {
+    const f32x4 v = __builtin_nontemporal_load(p + (int64_t)k * stride4);
+    const WCoef c = g_coef.v[k];
+    welford(m0, q0, (double)v.x, c);
+    welford(m1, q1, (double)v.y, c);
+    welford(m2, q2, (double)v.z, c);
+    welford(m3, q3, (double)v.w, c);
+  }
+  f64x2 *om = reinterpret_cast<f64x2 *>(out_mean + (int64_t)s * n_coord + 4 * i4);
+  f64x2 *oq = reinterpret_cast<f64x2 *>(out_m2 + (int64_t)s * n_coord + 4 * i4);
+  om[0] = f64x2{m0, m1};
+  om[1] = f64x2{m2, m3};
+  oq[0] = f64x2{q0, q1};
+  oq[1] = f64x2{q2, q3};
+}
+
+// ---------------------------------------------------------------------------
+// f32-faithful superposition transform of RMSF.py:99-101 / 133-135.
+//   p = f32(f64(p) - com); p = f32(f64(p) @ R); p = f32(f64(p) + ref_com)
+__device__ __forceinline__ void apply_xform(float &x, float &y, float &z, const double *__restrict__ t,
+                                            double rc0, double rc1, double rc2) {
+  const float p0 = (float)((double)x - t[9]);
+  const float p1 = (float)((double)y - t[10]);
+  const float p2 = (float)((double)z - t[11]);
+  const double d0 = p0, d1 = p1, d2 = p2;
+  // out_b = sum_a p_a R[a][b]   (np.dot(positions, R), R row-major)
+  const float r0 = (float)(d0 * t[0] + d1 * t[3] + d2 * t[6]);
+  const float r1 = (float)(d0 * t[1] + d1 * t[4] + d2 * t[7]);
+  const float r2 = (float)(d0 * t[2] + d1 * t[5] + d2 * t[8]);
+  x = (float)((double)r0 + rc0);
+  y = (float)((double)r1 + rc1);
+  z = (float)((double)r2 + rc2);
+}
+
+// k_accum_atoms: one selected atom per lane, frames of split blockIdx.y.
+// MODE 0 = WELFORD (out0 = mean, out1 = M2), 1 = SUM (out0 = sum).
+template <int MODE, bool ALIGN, bool GATHER, int U>
+__global__ __launch_bounds__(kBlock) void k_accum_atoms(
+    const float *__restrict__ xyz, int64_t fstride, int64_t n_sel, const int32_t *__restrict__ sel,
+    int64_t n_frames, int n_splits, const double *__restrict__ xform, const double *__restrict__ refinfo,
+    double *__restrict__ out0, double *__restrict__ out1) {
+  const int64_t a = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (a >= n_sel) return;
+  const int s = blockIdx.y;
+  const int64_t fb = split_begin(n_frames, n_splits, s);
+  const int nf = (int)(split_begin(n_frames, n_splits, s + 1) - fb);
+  const int64_t off = GATHER ? 3 * (int64_t)sel[a] : 3 * a;
+  const float *p = xyz + fb * fstride + off;
+  const double *xf = ALIGN ? xform + fb * kXform : nullptr;
+  const double rc0 = ALIGN ? refinfo[0] : 0.0, rc1 = ALIGN ? refinfo[1] : 0.0, rc2 = ALIGN ? refinfo[2] : 0.0;
+
+  double m0 = 0, m1 = 0, m2 = 0, q0 = 0, q1 = 0, q2 = 0;
+  auto consume = [&](float x, float y, float z, int k) {
+    if (ALIGN) apply_xform(x, y, z, xf + (int64_t)k * kXform, rc0, rc1, rc2);
+    if (MODE == RMSF_MODE_WELFORD) {
+      const WCoef c = g_coef.v[k];
+      welford(m0, q0, (double)x, c);
+      welford(m1, q1, (double)y, c);
+      welford(m2, q2, (double)z, c);
+    } else {
+      m0 += (double)x;
+      m1 += (double)y;
+      m2 += (double)z;
+    }
+  };
+  int k = 0;
+  for (; k + U <= nf; k += U) {
+    float vx[U], vy[U], vz[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float *q = p + (int64_t)(k + u) * fstride;
+      vx[u] = __builtin_nontemporal_load(q);
+      vy[u] = __builtin_nontemporal_load(q + 1);
+      vz[u] = __builtin_nontemporal_load(q + 2);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) consume(vx[u], vy[u], vz[u], k + u);
+  }
+  for (; k < nf; ++k) {
+    const float *q = p + (int64_t)k * fstride;
+    consume(q[0], q[1], q[2], k);
+  }
+  const int64_t o = (int64_t)s * 3 * n_sel + 3 * a;
+  out0[o + 0] = m0;
+  out0[o + 1] = m1;
+  out0[o + 2] = m2;
+  if (MODE == RMSF_MODE_WELFORD) {
+    out1[o + 0] = q0;
+    out1[o + 1] = q1;
+    out1[o + 2] = q2;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Wave / block reductions (64-wide waves).
+template <int N>
+__device__ __forceinline__ void wave_sum(double (&v)[N]) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[j] += __shfl_xor(v[j], off, 64);
+  }
+}
+
+// k_frame_stats: grid = (n_frames, n_chunks).  Sums, relative to a pivot p
+// (the frame's first selected atom, for conditioning), over the chunk's atoms:
+//   [0..2]  sum x'            [3..5]  sum m x'   (only with masses)
+//   [6..14] sum x'_a r_b      [15]    sum |x'|^2
+template <bool GATHER, bool MASSES>
+__global__ __launch_bounds__(kBlock) void k_frame_stats(
+    const float *__restrict__ xyz, int64_t fstride, int64_t n_sel, const int32_t *__restrict__ sel,
+    const double *__restrict__ masses, const double *__restrict__ ref, int n_chunks,
+    double *__restrict__ part) {
+  const int64_t f = blockIdx.x;
+  const int ch = blockIdx.y;
+  const float *fr = xyz + f * fstride;
+  const int64_t o0 = GATHER ? 3 * (int64_t)sel[0] : 0;
+  const double px = fr[o0], py = fr[o0 + 1], pz = fr[o0 + 2];
+
+  double acc[kStats];
+#pragma unroll
+  for (int j = 0; j < kStats; ++j) acc[j] = 0.0;
+  const int64_t beg = (int64_t)ch * kChunkAtoms;
+  const int64_t end = min(n_sel, beg + kChunkAtoms);
+  for (int64_t a = beg + threadIdx.x; a < end; a += kBlock) {
+    const int64_t off = GATHER ? 3 * (int64_t)sel[a] : 3 * a;
+    const double x = (double)fr[off] - px;
+    const double y = (double)fr[off + 1] - py;
+    const double z = (double)fr[off + 2] - pz;
+    const double r0 = ref[3 * a], r1 = ref[3 * a + 1], r2 = ref[3 * a + 2];
+    acc[0] += x;
+    acc[1] += y;
+    acc[2] += z;
+    if (MASSES) {
+      const double m = masses[a];
+      acc[3] = fma(m, x, acc[3]);
+      acc[4] = fma(m, y, acc[4]);
+      acc[5] = fma(m, z, acc[5]);
+    }
+    acc[6] = fma(x, r0, acc[6]);
+    acc[7] = fma(x, r1, acc[7]);
+    acc[8] = fma(x, r2, acc[8]);
+    acc[9] = fma(y, r0, acc[9]);
+    acc[10] = fma(y, r1, acc[10]);
+    acc[11] = fma(y, r2, acc[11]);
+    acc[12] = fma(z, r0, acc[12]);
+    acc[13] = fma(z, r1, acc[13]);
+    acc[14] = fma(z, r2, acc[14]);
+    acc[15] = fma(x, x, fma(y, y, fma(z, z, acc[15])));
+  }
+  wave_sum(acc);
+  __shared__ double red[kBlock / 64][kStats];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < kStats; ++j) red[w][j] = acc[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < kStats) {
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < kBlock / 64; ++i) t += red[i][threadIdx.x];
+    part[((int64_t)f * n_chunks + ch) * kStats + threadIdx.x] = t;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// QCP: the published quaternion-characteristic-polynomial algorithm
+// (D. Theobald, Acta Cryst A 61:478, 2005; P. Liu et al., J Comput Chem
+// 31:1561, 2010), as used by MDAnalysis.lib.qcprot (RMSF.py:48).  A is the
+// row-major inner product sum_i mob_i[a] ref_i[b]; rot is applied as x @ rot.
+// SURVEY.md Appendix A.2-A.3 gives the exact sequence followed here.
+__host__ __device__ inline void qcp_solve(const double *A, double E0, double len, double *rot,
+                                          double *rmsd) {
+  const double Sxx = A[0], Sxy = A[1], Sxz = A[2];
+  const double Syx = A[3], Syy = A[4], Syz = A[5];
+  const double Szx = A[6], Szy = A[7], Szz = A[8];
+
+  const double Sxx2 = Sxx * Sxx, Syy2 = Syy * Syy, Szz2 = Szz * Szz;
+  const double Sxy2 = Sxy * Sxy, Syz2 = Syz * Syz, Sxz2 = Sxz * Sxz;
+  const double Syx2 = Syx * Syx, Szy2 = Szy * Szy, Szx2 = Szx * Szx;
+
+  const double SyzSzymSyySzz2 = 2.0 * (Syz * Szy - Syy * Szz);
+  const double Sxx2Syy2Szz2Syz2Szy2 = Syy2 + Szz2 - Sxx2 + Syz2 + Szy2;
+
+  const double C2 = -2.0 * (Sxx2 + Syy2 + Szz2 + Sxy2 + Syx2 + Sxz2 + Szx2 + Syz2 + Szy2);
+  const double C1 = 8.0 * (Sxx * Syz * Szy + Syy * Szx * Sxz + Szz * Sxy * Syx - Sxx * Syy * Szz -
+                           Syz * Szx * Sxy - Szy * Syx * Sxz);
+
+  const double SxzpSzx = Sxz + Szx, SyzpSzy = Syz + Szy, SxypSyx = Sxy + Syx;
+  const double SyzmSzy = Syz - Szy, SxzmSzx = Sxz - Szx, SxymSyx = Sxy - Syx;
+  const double SxxpSyy = Sxx + Syy, SxxmSyy = Sxx - Syy;
+  const double Sxy2Sxz2Syx2Szx2 = Sxy2 + Sxz2 - Syx2 - Szx2;
+
+  const double C0 =
+      Sxy2Sxz2Syx2Szx2 * Sxy2Sxz2Syx2Szx2 +
+      (Sxx2Syy2Szz2Syz2Szy2 + SyzSzymSyySzz2) * (Sxx2Syy2Szz2Syz2Szy2 - SyzSzymSyySzz2) +
+      (-(SxzpSzx) * (SyzmSzy) + (SxymSyx) * (SxxmSyy - Szz)) *
+          (-(SxzmSzx) * (SyzpSzy) + (SxymSyx) * (SxxmSyy + Szz)) +
+      (-(SxzpSzx) * (SyzpSzy) - (SxypSyx) * (SxxpSyy - Szz)) *
+          (-(SxzmSzx) * (SyzmSzy) - (SxypSyx) * (SxxpSyy + Szz)) +
+      (+(SxypSyx) * (SyzpSzy) + (SxzpSzx) * (SxxmSyy + Szz)) *
+          (-(SxymSyx) * (SyzmSzy) + (SxzpSzx) * (SxxpSyy + Szz)) +
+      (+(SxypSyx) * (SyzmSzy) + (SxzmSzx) * (SxxmSyy - Szz)) *
+          (-(SxymSyx) * (SyzpSzy) + (SxzmSzx) * (SxxpSyy - Szz));
+
+  // Newton-Raphson on the quartic, from lambda = E0 (upper bound).
+  double l = E0;
+  for (int i = 0; i < 50; ++i) {
+    const double old = l;
+    const double x2 = l * l;
+    const double b = (x2 + C2) * l;
+    const double a = b + C1;
+    const double delta = (a * l + C0) / (2.0 * x2 * l + b + a);
+    l -= delta;
+    if (fabs(l - old) < fabs(1e-11 * l)) break;
+  }
+  *rmsd = sqrt(fabs(2.0 * (E0 - l) / len));
+
+  const double a11 = SxxpSyy + Szz - l, a12 = SyzmSzy, a13 = -SxzmSzx, a14 = SxymSyx;
+  const double a21 = SyzmSzy, a22 = SxxmSyy - Szz - l, a23 = SxypSyx, a24 = SxzpSzx;
+  const double a31 = a13, a32 = a23, a33 = Syy - Sxx - Szz - l, a34 = SyzpSzy;
+  const double a41 = a14, a42 = a24, a43 = a34, a44 = Szz - SxxpSyy - l;
+  const double a3344_4334 = a33 * a44 - a43 * a34, a3244_4234 = a32 * a44 - a42 * a34;
+  const double a3243_4233 = a32 * a43 - a42 * a33, a3143_4133 = a31 * a43 - a41 * a33;
+  const double a3144_4134 = a31 * a44 - a41 * a34, a3142_4132 = a31 * a42 - a41 * a32;
+  double q1 = a22 * a3344_4334 - a23 * a3244_4234 + a24 * a3243_4233;
+  double q2 = -a21 * a3344_4334 + a23 * a3144_4134 - a24 * a3143_4133;
+  double q3 = a21 * a3244_4234 - a22 * a3144_4134 + a24 * a3142_4132;
+  double q4 = -a21 * a3243_4233 + a22 * a3143_4133 - a23 * a3142_4132;
+  double qsqr = q1 * q1 + q2 * q2 + q3 * q3 + q4 * q4;
+
+  const double evecprec = 1e-6;
+  if (qsqr < evecprec) {
+    q1 = a12 * a3344_4334 - a13 * a3244_4234 + a14 * a3243_4233;
+    q2 = -a11 * a3344_4334 + a13 * a3144_4134 - a14 * a3143_4133;
+    q3 = a11 * a3244_4234 - a12 * a3144_4134 + a14 * a3142_4132;
+    q4 = -a11 * a3243_4233 + a12 * a3143_4133 - a13 * a3142_4132;
+    qsqr = q1 * q1 + q2 * q2 + q3 * q3 + q4 * q4;
+    if (qsqr < evecprec) {
+      const double a1324_1423 = a13 * a24 - a14 * a23, a1224_1422 = a12 * a24 - a14 * a22;
+      const double a1223_1322 = a12 * a23 - a13 * a22, a1124_1421 = a11 * a24 - a14 * a21;
+      const double a1123_1321 = a11 * a23 - a13 * a21, a1122_1221 = a11 * a22 - a12 * a21;
+      q1 = a42 * a1324_1423 - a43 * a1224_1422 + a44 * a1223_1322;
+      q2 = -a41 * a1324_1423 + a43 * a1124_1421 - a44 * a1123_1321;
+      q3 = a41 * a1224_1422 - a42 * a1124_1421 + a44 * a1122_1221;
+      q4 = -a41 * a1223_1322 + a42 * a1123_1321 - a43 * a1122_1221;
+      qsqr = q1 * q1 + q2 * q2 + q3 * q3 + q4 * q4;
+      if (qsqr < evecprec) {
+        q1 = a32 * a1324_1423 - a33 * a1224_1422 + a34 * a1223_1322;
+        q2 = -a31 * a1324_1423 + a33 * a1124_1421 - a34 * a1123_1321;
+        q3 = a31 * a1224_1422 - a32 * a1124_1421 + a34 * a1122_1221;
+        q4 = -a31 * a1223_1322 + a32 * a1123_1321 - a33 * a1122_1221;
+        qsqr = q1 * q1 + q2 * q2 + q3 * q3 + q4 * q4;
+        if (qsqr < evecprec) {
+          rot[0] = rot[4] = rot[8] = 1.0;
+          rot[1] = rot[2] = rot[3] = rot[5] = rot[6] = rot[7] = 0.0;
+          return;
+        }
+      }
+    }
+  }
+  const double normq = sqrt(qsqr);
+  q1 /= normq;
+  q2 /= normq;
+  q3 /= normq;
+  q4 /= normq;
+  const double a2 = q1 * q1, x2 = q2 * q2, y2 = q3 * q3, z2 = q4 * q4;
+  const double xy = q2 * q3, az = q1 * q4, zx = q4 * q2, ay = q1 * q3, yz = q3 * q4, ax = q1 * q2;
+  rot[0] = a2 + x2 - y2 - z2;
+  rot[1] = 2 * (xy + az);
+  rot[2] = 2 * (zx - ay);
+  rot[3] = 2 * (xy - az);
+  rot[4] = a2 - x2 + y2 - z2;
+  rot[5] = 2 * (yz + ax);
+  rot[6] = 2 * (zx + ay);
+  rot[7] = 2 * (yz - ax);
+  rot[8] = a2 - x2 - y2 + z2;
+}
+
+// k_qcp_frames: one wave per frame.  Folds the chunk partials in a fixed
+// order (deterministic), forms COM / A / E0 and solves QCP on lane 0.
+template <bool GATHER, bool MASSES>
+__global__ __launch_bounds__(kBlock) void k_qcp_frames(
+    const double *__restrict__ part, int n_chunks, int64_t n_frames, const float *__restrict__ xyz,
+    int64_t fstride, const int32_t *__restrict__ sel, const double *__restrict__ refinfo,
+    double *__restrict__ xform) {
+  const int64_t f = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (f >= n_frames) return;
+  double s[kStats];
+#pragma unroll
+  for (int j = 0; j < kStats; ++j) s[j] = 0.0;
+  for (int c = lane; c < n_chunks; c += 64) {
+    const double *pp = part + ((int64_t)f * n_chunks + c) * kStats;
+#pragma unroll
+    for (int j = 0; j < kStats; ++j) s[j] += pp[j];
+  }
+  wave_sum(s);
+  if (lane != 0) return;
+
+  const double nsel = refinfo[7 + 1];  // n_sel
+  const double mtot = refinfo[7];      // total mass (n_sel without masses)
+  const int64_t o0 = GATHER ? 3 * (int64_t)sel[0] : 0;
+  const float *fr = xyz + f * fstride;
+  const double px = fr[o0], py = fr[o0 + 1], pz = fr[o0 + 2];
+  // COM relative to the pivot
+  const double cx = (MASSES ? s[3] : s[0]) / mtot;
+  const double cy = (MASSES ? s[4] : s[1]) / mtot;
+  const double cz = (MASSES ? s[5] : s[2]) / mtot;
+  // sum of centred reference coordinates (0 for unit masses up to rounding)
+  const double sr0 = refinfo[3], sr1 = refinfo[4], sr2 = refinfo[5];
+  double A[9];
+  A[0] = s[6] - cx * sr0;
+  A[1] = s[7] - cx * sr1;
+  A[2] = s[8] - cx * sr2;
+  A[3] = s[9] - cy * sr0;
+  A[4] = s[10] - cy * sr1;
+  A[5] = s[11] - cy * sr2;
+  A[6] = s[12] - cz * sr0;
+  A[7] = s[13] - cz * sr1;
+  A[8] = s[14] - cz * sr2;
+  const double gmob = s[15] - 2.0 * (cx * s[0] + cy * s[1] + cz * s[2]) + nsel * (cx * cx + cy * cy + cz * cz);
+  const double E0 = 0.5 * (gmob + refinfo[6]);
+  double *t = xform + f * kXform;
+  double rot[9], rmsd;
+  qcp_solve(A, E0, nsel, rot, &rmsd);
+#pragma unroll
+  for (int j = 0; j < 9; ++j) t[j] = rot[j];
+  t[9] = px + cx;
+  t[10] = py + cy;
+  t[11] = pz + cz;
+  t[12] = rmsd;
+  t[13] = t[14] = t[15] = 0.0;
+}
+
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void block_sum_1024(double (&v)[N], double (*red)[N]) {
+  wave_sum(v);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) red[w][j] = v[j];
+  }
+  __syncthreads();
+  const int nw = blockDim.x >> 6;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    double t = 0.0;
+    for (int i = 0; i < nw; ++i) t += red[i][j];
+    v[j] = t;
+  }
+}
+
+// k_reference: one 1024-thread block.  RMSF.py:84-85 / 117-118.
+template <bool FROM_F32, bool GATHER, bool MASSES>
+__global__ __launch_bounds__(1024) void k_reference(const float *__restrict__ frame,
+                                                    const double *__restrict__ avg, int64_t n_sel,
+                                                    const int32_t *__restrict__ sel,
+                                                    const double *__restrict__ masses,
+                                                    double *__restrict__ ref, double *__restrict__ info) {
+  __shared__ double red4[16][4];
+  auto coord = [&](int64_t a, int c) -> double {
+    if (FROM_F32) return (double)frame[(GATHER ? 3 * (int64_t)sel[a] : 3 * a) + c];
+    return avg[3 * a + c];
+  };
+  double v[4] = {0, 0, 0, 0};  // sum m x, sum m y, sum m z, sum m
+  for (int64_t a = threadIdx.x; a < n_sel; a += blockDim.x) {
+    const double m = MASSES ? masses[a] : 1.0;
+    v[0] = fma(coord(a, 0), m, v[0]);
+    v[1] = fma(coord(a, 1), m, v[1]);
+    v[2] = fma(coord(a, 2), m, v[2]);
+    v[3] += m;
+  }
+  block_sum_1024(v, red4);
+  const double c0 = v[0] / v[3], c1 = v[1] / v[3], c2 = v[2] / v[3];
+  double w[4] = {0, 0, 0, 0};  // sum r (3), sum |r|^2
+  for (int64_t a = threadIdx.x; a < n_sel; a += blockDim.x) {
+    const double r0 = coord(a, 0) - c0, r1 = coord(a, 1) - c1, r2 = coord(a, 2) - c2;
+    ref[3 * a] = r0;
+    ref[3 * a + 1] = r1;
+    ref[3 * a + 2] = r2;
+    w[0] += r0;
+    w[1] += r1;
+    w[2] += r2;
+    w[3] = fma(r0, r0, fma(r1, r1, fma(r2, r2, w[3])));
+  }
+  block_sum_1024(w, red4);
+  if (threadIdx.x == 0) {
+    info[0] = c0;
+    info[1] = c1;
+    info[2] = c2;
+    info[3] = w[0];
+    info[4] = w[1];
+    info[5] = w[2];
+    info[6] = w[3];
+    info[7] = v[3];
+    info[8] = (double)n_sel;
+    for (int j = 9; j < kRefInfo; ++j) info[j] = 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+constexpr int kMergeGroup = 128;
+struct MergeCounts {
+  double n[kMergeGroup];
+};
+
+// Fold (acc) + parts[0..np) in order: second_order_moments, RMSF.py:36-41.
+__global__ __launch_bounds__(kBlock) void k_chan_merge(const double *__restrict__ acc_mean,
+                                                       const double *__restrict__ acc_m2, double acc_n,
+                                                       const double *__restrict__ mp,
+                                                       const double *__restrict__ qp, MergeCounts cnt,
+                                                       int np, int64_t n, double *mo, double *qo) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  double n1 = acc_n, mu = 0.0, M = 0.0;
+  if (acc_n > 0) {
+    mu = acc_mean[j];
+    M = acc_m2[j];
+  }
+  for (int s = 0; s < np; ++s) {
+    const double n2 = cnt.n[s];
+    if (n2 <= 0) continue;  // empty partial (Appendix B Q5)
+    const double mu2 = mp[(int64_t)s * n + j], M2 = qp[(int64_t)s * n + j];
+    if (n1 <= 0) {
+      n1 = n2;
+      mu = mu2;
+      M = M2;
+      continue;
+    }
+    const double T = n1 + n2;
+    const double d = mu2 - mu;
+    const double mun = (n1 * mu + n2 * mu2) / T;
+    M = M + M2 + (n1 * n2 / T) * (d * d);
+    mu = mun;
+    n1 = T;
+  }
+  mo[j] = mu;
+  qo[j] = M;
+}
+
+__global__ __launch_bounds__(kBlock) void k_sum_splits(const double *__restrict__ parts, int np, int64_t n,
+                                                       double *__restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  double t = 0.0;
+  for (int s = 0; s < np; ++s) t += parts[(int64_t)s * n + j];
+  out[j] = t;
+}
+
+__global__ __launch_bounds__(kBlock) void k_divide(const double *__restrict__ x, double d, int64_t n,
+                                                   double *__restrict__ y) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j < n) y[j] = x[j] / d;
+}
+
+__global__ __launch_bounds__(kBlock) void k_chan_weight(const double *__restrict__ m, double w, int64_t n,
+                                                        double *__restrict__ y) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j < n) y[j] = w * m[j];
+}
+
+__global__ __launch_bounds__(kBlock) void k_chan_deviation(const double *__restrict__ mk,
+                                                           const double *__restrict__ qk,
+                                                           const double *__restrict__ mean, double nk,
+                                                           int64_t n, double *__restrict__ y) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const double d = mk[j] - mean[j];
+  y[j] = qk[j] + nk * (d * d);
+}
+
+__global__ __launch_bounds__(kBlock) void k_finalize(const double *__restrict__ m2, int64_t n_sel, double nf,
+                                                     double *__restrict__ out) {
+  const int64_t a = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (a >= n_sel) return;
+  out[a] = sqrt((m2[3 * a] + m2[3 * a + 1] + m2[3 * a + 2]) / nf);
+}
+
+__global__ __launch_bounds__(kBlock) void k_qcp_batch(const double *__restrict__ A, const double *__restrict__ E0,
+                                                      const double *__restrict__ N, int64_t n,
+                                                      double *__restrict__ rot, double *__restrict__ rmsd) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  double r[9], d;
+  qcp_solve(A + 9 * i, E0[i], N[i], r, &d);
+  for (int j = 0; j < 9; ++j) rot[9 * i + j] = r[j];
+  rmsd[i] = d;
+}
+
+// qcprot InnerProduct (weights optional), single block: A (9) and E0.
+__global__ __launch_bounds__(1024) void k_inner_product(const double *__restrict__ ref,
+                                                        const double *__restrict__ conf,
+                                                        const double *__restrict__ w, int64_t N,
+                                                        double *__restrict__ out) {
+  __shared__ double red[16][11];
+  double v[11];
+  for (int j = 0; j < 11; ++j) v[j] = 0.0;
+  for (int64_t i = threadIdx.x; i < N; i += blockDim.x) {
+    const double wi = w ? w[i] : 1.0;
+    const double x1 = wi * conf[3 * i], y1 = wi * conf[3 * i + 1], z1 = wi * conf[3 * i + 2];
+    const double x2 = ref[3 * i], y2 = ref[3 * i + 1], z2 = ref[3 * i + 2];
+    v[9] += x1 * conf[3 * i] + y1 * conf[3 * i + 1] + z1 * conf[3 * i + 2];
+    v[10] += wi * (x2 * x2 + y2 * y2 + z2 * z2);
+    v[0] += x1 * x2;
+    v[1] += x1 * y2;
+    v[2] += x1 * z2;
+    v[3] += y1 * x2;
+    v[4] += y1 * y2;
+    v[5] += y1 * z2;
+    v[6] += z1 * x2;
+    v[7] += z1 * y2;
+    v[8] += z1 * z2;
+  }
+  block_sum_1024(v, red);
+  if (threadIdx.x == 0) {
+    for (int j = 0; j < 9; ++j) out[j] = v[j];
+    out[9] = 0.5 * (v[9] + v[10]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic generator.  Every f64 op is a single IEEE-rounded op (no FMA
+// contraction), so oracle/synth.py reproduces the frames bit-for-bit.
+__host__ __device__ inline uint64_t sm64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__host__ __device__ inline uint64_t skey(uint64_t seed, uint64_t stream, uint64_t i, uint64_t j) {
+  return sm64(sm64(sm64(seed ^ (stream * 0xD1B54A32D192ED03ull)) + i) + j);
+}
+
+__global__ __launch_bounds__(kBlock) void k_synth(float *__restrict__ out, int64_t fstride, int64_t n_atoms,
+                                                  int64_t f0, int64_t nf, uint64_t seed,
+                                                  const double *__restrict__ motion) {
+#pragma clang fp contract(off)
+  const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= nf * n_atoms) return;
+  const int64_t fl = t / n_atoms, a = t - fl * n_atoms;
+  const int64_t f = f0 + fl;
+  const double two24 = 5.9604644775390625e-08;   // 2^-24
+  const double two53 = 1.1102230246251565e-16;   // 2^-53
+  const double sqrt6 = 2.449489742783178;
+  const double sigma = 0.2 + (double)(skey(seed, 2, (uint64_t)a, 0) >> 11) * two53 * 1.8;
+  double p[3];
+  for (int c = 0; c < 3; ++c) {
+    const double base = (double)(skey(seed, 1, (uint64_t)a, (uint64_t)c) >> 11) * two53 * 100.0;
+    const uint64_t h = skey(seed, 3, (uint64_t)f, (uint64_t)(3 * a + c));
+    const uint64_t u = (h >> 40) + ((h >> 16) & 0xFFFFFFull);
+    const double g = ((double)u * two24 - 1.0) * sqrt6;
+    const double s = sigma * g;
+    p[c] = base + s;
+  }
+  float *o = out + fl * fstride + 3 * a;
+  if (motion) {
+    const double *M = motion + 12 * f;
+    const double d0 = p[0] - 50.0, d1 = p[1] - 50.0, d2 = p[2] - 50.0;
+    for (int b = 0; b < 3; ++b) {
+      const double e0 = d0 * M[b];
+      const double e1 = d1 * M[3 + b];
+      const double e2 = d2 * M[6 + b];
+      const double y = ((e0 + e1) + e2) + M[9 + b];
+      o[b] = (float)y;
+    }
+  } else {
+    o[0] = (float)p[0];
+    o[1] = (float)p[1];
+    o[2] = (float)p[2];
+  }
+}
+
+inline unsigned grid1(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+int64_t n_chunks_for(int64_t n_sel) { return (n_sel + kChunkAtoms - 1) / kChunkAtoms; }
+
+}  // namespace
+
+// ===========================================================================
+// extern "C" ABI
+// ===========================================================================
+extern "C" {
+
+RMSF_EXPORT int rmsf_abi_version(void) { return RMSF_ABI_VERSION; }
+
+// error hook used by stager.cpp (not part of the public header)
+RMSF_EXPORT int rmsf_internal_set_error(int code, const char *msg) { return fail(code, msg ? msg : ""); }
+
+RMSF_EXPORT const char *rmsf_last_error(void) { return g_err.c_str(); }
+
+RMSF_EXPORT int rmsf_device_count(int *n) {
+  if (!n) return fail(RMSF_EINVAL, "rmsf_device_count: null");
+  HIP_TRY(hipGetDeviceCount(n));
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_set_device(int dev) {
+  HIP_TRY(hipSetDevice(dev));
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_malloc(void **p, size_t bytes) {
+  if (!p) return fail(RMSF_EINVAL, "rmsf_malloc: null");
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) return fail(RMSF_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_free(void *p) {
+  HIP_TRY(hipFree(p));
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_memcpy_h2d(void *d, const void *h, size_t bytes, void *stream) {
+  HIP_TRY(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, S(stream)));
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_memcpy_d2h(void *h, const void *d, size_t bytes, void *stream) {
+  HIP_TRY(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, S(stream)));
+  HIP_TRY(hipStreamSynchronize(S(stream)));
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_stream_synchronize(void *stream) {
+  HIP_TRY(hipStreamSynchronize(S(stream)));
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_block_range(int64_t n_frames, int size, int rank, int64_t *start, int64_t *stop) {
+  if (n_frames < 0 || size < 1 || rank < 0 || rank >= size || !start || !stop)
+    return fail(RMSF_EINVAL, "rmsf_block_range: bad arguments");
+  const int64_t per = n_frames / size;  // RMSF.py:64 (floor division)
+  if (rank < size - 1) {                // RMSF.py:65
+    *start = rank * per;
+    *stop = (rank + 1) * per;
+  } else {                              // RMSF.py:66
+    *start = (int64_t)(size - 1) * per;
+    *stop = n_frames;
+  }
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_reference_setup(const float *d_frame, const double *d_avg, int64_t n_sel,
+                                     const int32_t *d_sel, const double *d_masses, double *d_ref,
+                                     double *d_refinfo, void *stream) {
+  if ((d_frame == nullptr) == (d_avg == nullptr))
+    return fail(RMSF_EINVAL, "rmsf_reference_setup: exactly one of d_frame / d_avg");
+  if (n_sel < 1 || !d_ref || !d_refinfo) return fail(RMSF_EINVAL, "rmsf_reference_setup: bad arguments");
+  const bool g = d_sel != nullptr, m = d_masses != nullptr;
+  hipStream_t s = S(stream);
+#define REF_LAUNCH(F, G, M) \
+  hipLaunchKernelGGL((k_reference<F, G, M>), dim3(1), dim3(1024), 0, s, d_frame, d_avg, n_sel, d_sel, d_masses, d_ref, d_refinfo)
+  if (d_frame) {
+    if (g && m) REF_LAUNCH(true, true, true);
+    else if (g) REF_LAUNCH(true, true, false);
+    else if (m) REF_LAUNCH(true, false, true);
+    else REF_LAUNCH(true, false, false);
+  } else {
+    if (m) REF_LAUNCH(false, false, true);
+    else REF_LAUNCH(false, false, false);
+  }
+#undef REF_LAUNCH
+  return after_launch("k_reference");
+}
+
+RMSF_EXPORT size_t rmsf_superpose_workspace_bytes(int64_t n_sel, int64_t n_frames) {
+  if (n_sel < 1 || n_frames < 0) return 0;
+  return (size_t)n_frames * (size_t)n_chunks_for(n_sel) * kStats * sizeof(double);
+}
+
+RMSF_EXPORT int rmsf_superpose(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
+                               const int32_t *d_sel, const double *d_masses, const double *d_ref,
+                               const double *d_refinfo, double *d_xform, void *d_work, size_t work_bytes,
+                               void *stream) {
+  if (n_frames == 0) return RMSF_OK;
+  if (!d_xyz || !d_ref || !d_refinfo || !d_xform || !d_work || n_sel < 1 || n_frames < 0 ||
+      fstride < (d_sel ? 3 : 3 * n_sel))
+    return fail(RMSF_EINVAL, "rmsf_superpose: bad arguments");
+  const int64_t nch = n_chunks_for(n_sel);
+  if (nch > 65535) return fail(RMSF_EINVAL, "rmsf_superpose: selection too large");
+  if (work_bytes < rmsf_superpose_workspace_bytes(n_sel, n_frames))
+    return fail(RMSF_ENOMEM, "rmsf_superpose: workspace too small");
+  hipStream_t s = S(stream);
+  double *part = static_cast<double *>(d_work);
+  const bool g = d_sel != nullptr, m = d_masses != nullptr;
+  // frames go to grid.x (up to 2^31-1), chunks to grid.y.
+  for (int64_t f0 = 0; f0 < n_frames; f0 += 0x7fffffff) {
+    const int64_t nf = std::min<int64_t>(n_frames - f0, 0x7fffffff);
+    dim3 grid((unsigned)nf, (unsigned)nch);
+    const float *x = d_xyz + f0 * fstride;
+    double *pp = part + f0 * nch * kStats;
+#define ST_LAUNCH(G, M) \
+  hipLaunchKernelGGL((k_frame_stats<G, M>), grid, dim3(kBlock), 0, s, x, fstride, n_sel, d_sel, d_masses, d_ref, (int)nch, pp)
+    if (g && m) ST_LAUNCH(true, true);
+    else if (g) ST_LAUNCH(true, false);
+    else if (m) ST_LAUNCH(false, true);
+    else ST_LAUNCH(false, false);
+#undef ST_LAUNCH
+  }
+  int rc = after_launch("k_frame_stats");
+  if (rc) return rc;
+  const unsigned gq = (unsigned)((n_frames + 3) / 4);
+#define QCP_LAUNCH(G, M) \
+  hipLaunchKernelGGL((k_qcp_frames<G, M>), dim3(gq), dim3(kBlock), 0, s, part, (int)nch, n_frames, d_xyz, fstride, d_sel, d_refinfo, d_xform)
+  if (g && m) QCP_LAUNCH(true, true);
+  else if (g) QCP_LAUNCH(true, false);
+  else if (m) QCP_LAUNCH(false, true);
+  else QCP_LAUNCH(false, false);
+#undef QCP_LAUNCH
+  return after_launch("k_qcp_frames");
+}
+
+RMSF_EXPORT int64_t rmsf_split_count(int64_t n_frames, int n_splits, int s) {
+  if (n_splits < 1 || s < 0 || s >= n_splits) return -1;
+  return (n_frames * (s + 1)) / n_splits - (n_frames * s) / n_splits;
+}
+
+RMSF_EXPORT int rmsf_accumulate_splits(int64_t n_sel, int64_t n_frames, int aligned) {
+  (void)aligned;
+  if (n_frames <= 0) return 1;
+  // Enough (lane-groups x splits) to fill 256 CUs several times over, with
+  // splits of <= kCoefN frames; the partial I/O (16 B per coordinate per
+  // split) stays ~1-2% of the frame stream.
+  const int64_t lanes = (3 * n_sel + 3) / 4;
+  const int64_t blocks_x = std::max<int64_t>(1, (lanes + kBlock - 1) / kBlock);
+  int64_t want = (16384 + blocks_x - 1) / blocks_x;  // ~16k workgroups in flight overall
+  want = std::max<int64_t>(want, (n_frames + kCoefN - 1) / kCoefN);
+  want = std::min<int64_t>(want, std::max<int64_t>(1, n_frames / 32));
+  want = std::max<int64_t>(want, (n_frames + kCoefN - 1) / kCoefN);
+  want = std::min<int64_t>(want, 65535);
+  return (int)std::max<int64_t>(1, want);
+}
+
+RMSF_EXPORT int rmsf_accumulate(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
+                                const int32_t *d_sel, const double *d_xform, const double *d_refinfo, int mode,
+                                int n_splits, double *d_out0, double *d_out1, void *stream) {
+  if (mode != RMSF_MODE_WELFORD && mode != RMSF_MODE_SUM) return fail(RMSF_EINVAL, "rmsf_accumulate: bad mode");
+  if (!d_xyz || !d_out0 || (mode == RMSF_MODE_WELFORD && !d_out1) || n_sel < 1 || n_frames < 1 ||
+      fstride < (d_sel ? 3 : 3 * n_sel))
+    return fail(RMSF_EINVAL, "rmsf_accumulate: bad arguments");
+  if (d_xform && !d_refinfo) return fail(RMSF_EINVAL, "rmsf_accumulate: aligned mode needs d_refinfo");
+  if (n_splits <= 0) n_splits = rmsf_accumulate_splits(n_sel, n_frames, d_xform != nullptr);
+  if (n_splits > 65535) return fail(RMSF_EINVAL, "rmsf_accumulate: n_splits > 65535");
+  if ((n_frames + n_splits - 1) / n_splits > kCoefN)
+    return fail(RMSF_EINVAL, "rmsf_accumulate: a split exceeds 4096 frames; raise n_splits");
+  hipStream_t s = S(stream);
+  const int64_t n_coord = 3 * n_sel;
+  const bool flat_ok = !d_xform && !d_sel && mode == RMSF_MODE_WELFORD && (n_coord % 4 == 0) &&
+                       (fstride % 4 == 0) && (reinterpret_cast<uintptr_t>(d_xyz) % 16 == 0) &&
+                       (reinterpret_cast<uintptr_t>(d_out0) % 16 == 0) &&
+                       (reinterpret_cast<uintptr_t>(d_out1) % 16 == 0);
+  if (flat_ok) {
+    const int64_t n4 = n_coord / 4;
+    dim3 grid(grid1(n4), (unsigned)n_splits);
+    hipLaunchKernelGGL((k_welford_flat<4>), grid, dim3(kBlock), 0, s, d_xyz, fstride / 4, n4, n_frames, n_splits,
+                       d_out0, d_out1, n_coord);
+    return after_launch("k_welford_flat");
+  }
+  dim3 grid(grid1(n_sel), (unsigned)n_splits);
+  const bool g = d_sel != nullptr, al = d_xform != nullptr;
+#define AC_LAUNCH(M, A, G) \
+  hipLaunchKernelGGL((k_accum_atoms<M, A, G, 4>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_sel, d_sel, n_frames, n_splits, d_xform, d_refinfo, d_out0, d_out1)
+  if (mode == RMSF_MODE_WELFORD) {
+    if (al && g) AC_LAUNCH(0, true, true);
+    else if (al) AC_LAUNCH(0, true, false);
+    else if (g) AC_LAUNCH(0, false, true);
+    else AC_LAUNCH(0, false, false);
+  } else {
+    if (al && g) AC_LAUNCH(1, true, true);
+    else if (al) AC_LAUNCH(1, true, false);
+    else if (g) AC_LAUNCH(1, false, true);
+    else AC_LAUNCH(1, false, false);
+  }
+#undef AC_LAUNCH
+  return after_launch("k_accum_atoms");
+}
+
+RMSF_EXPORT int rmsf_chan_merge(const double *d_mean_parts, const double *d_m2_parts, const int64_t *h_counts,
+                                int n_parts, int64_t n_coord, double *d_mean, double *d_m2, void *stream) {
+  if (!d_mean_parts || !d_m2_parts || !h_counts || n_parts < 1 || n_coord < 1 || !d_mean || !d_m2)
+    return fail(RMSF_EINVAL, "rmsf_chan_merge: bad arguments");
+  int64_t total = 0;
+  for (int i = 0; i < n_parts; ++i) {
+    if (h_counts[i] < 0) return fail(RMSF_EINVAL, "rmsf_chan_merge: negative count");
+    total += h_counts[i];
+  }
+  if (total == 0) return fail(RMSF_EEMPTY, "rmsf_chan_merge: every partial is empty (no frames)");
+  hipStream_t s = S(stream);
+  double acc_n = 0.0;
+  for (int g0 = 0; g0 < n_parts; g0 += kMergeGroup) {
+    const int np = std::min(kMergeGroup, n_parts - g0);
+    MergeCounts c{};
+    for (int i = 0; i < np; ++i) c.n[i] = (double)h_counts[g0 + i];
+    hipLaunchKernelGGL(k_chan_merge, dim3(grid1(n_coord)), dim3(kBlock), 0, s, d_mean, d_m2, acc_n,
+                       d_mean_parts + (int64_t)g0 * n_coord, d_m2_parts + (int64_t)g0 * n_coord, c, np, n_coord,
+                       d_mean, d_m2);
+    int rc = after_launch("k_chan_merge");
+    if (rc) return rc;
+    for (int i = 0; i < np; ++i) acc_n += (double)h_counts[g0 + i];
+  }
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_sum_splits(const double *d_parts, int n_parts, int64_t n, double *d_sum, void *stream) {
+  if (!d_parts || !d_sum || n_parts < 1 || n < 1) return fail(RMSF_EINVAL, "rmsf_sum_splits: bad arguments");
+  hipLaunchKernelGGL(k_sum_splits, dim3(grid1(n)), dim3(kBlock), 0, S(stream), d_parts, n_parts, n, d_sum);
+  return after_launch("k_sum_splits");
+}
+
+RMSF_EXPORT int rmsf_divide(const double *d_x, double divisor, int64_t n, double *d_y, void *stream) {
+  if (!d_x || !d_y || n < 1) return fail(RMSF_EINVAL, "rmsf_divide: bad arguments");
+  if (divisor == 0.0) return fail(RMSF_EEMPTY, "rmsf_divide: divisor is zero (no frames)");
+  hipLaunchKernelGGL(k_divide, dim3(grid1(n)), dim3(kBlock), 0, S(stream), d_x, divisor, n, d_y);
+  return after_launch("k_divide");
+}
+
+RMSF_EXPORT int rmsf_chan_weight(const double *d_mean_k, double w, int64_t n, double *d_out, void *stream) {
+  if (!d_mean_k || !d_out || n < 1) return fail(RMSF_EINVAL, "rmsf_chan_weight: bad arguments");
+  hipLaunchKernelGGL(k_chan_weight, dim3(grid1(n)), dim3(kBlock), 0, S(stream), d_mean_k, w, n, d_out);
+  return after_launch("k_chan_weight");
+}
+
+RMSF_EXPORT int rmsf_chan_deviation(const double *d_mean_k, const double *d_m2_k, const double *d_mean, double n_k,
+                                    int64_t n, double *d_out, void *stream) {
+  if (!d_mean_k || !d_m2_k || !d_mean || !d_out || n < 1)
+    return fail(RMSF_EINVAL, "rmsf_chan_deviation: bad arguments");
+  hipLaunchKernelGGL(k_chan_deviation, dim3(grid1(n)), dim3(kBlock), 0, S(stream), d_mean_k, d_m2_k, d_mean, n_k, n,
+                     d_out);
+  return after_launch("k_chan_deviation");
+}
+
+RMSF_EXPORT int rmsf_finalize(const double *d_m2, int64_t n_sel, int64_t n_frames, double *d_rmsf, void *stream) {
+  if (!d_m2 || !d_rmsf || n_sel < 1) return fail(RMSF_EINVAL, "rmsf_finalize: bad arguments");
+  if (n_frames < 1) return fail(RMSF_EEMPTY, "rmsf_finalize: no frames");
+  hipLaunchKernelGGL(k_finalize, dim3(grid1(n_sel)), dim3(kBlock), 0, S(stream), d_m2, n_sel, (double)n_frames,
+                     d_rmsf);
+  return after_launch("k_finalize");
+}
+
+RMSF_EXPORT int rmsf_qcp_batch(const double *d_A, const double *d_E0, const double *d_N, int64_t n, double *d_rot,
+                               double *d_rmsd, void *stream) {
+  if (!d_A || !d_E0 || !d_N || !d_rot || !d_rmsd || n < 0) return fail(RMSF_EINVAL, "rmsf_qcp_batch: bad arguments");
+  if (n == 0) return RMSF_OK;
+  hipLaunchKernelGGL(k_qcp_batch, dim3(grid1(n)), dim3(kBlock), 0, S(stream), d_A, d_E0, d_N, n, d_rot, d_rmsd);
+  return after_launch("k_qcp_batch");
+}
+
+RMSF_EXPORT int rmsf_calc_rmsd_rotational_matrix(const double *h_ref, const double *h_conf, int64_t N, double *h_rot,
+                                                 const double *h_weights, double *rmsd_out) {
+  if (!h_ref || !h_conf || !h_rot || N < 1) return fail(RMSF_EINVAL, "CalcRMSDRotationalMatrix: bad arguments");
+  const size_t cb = (size_t)N * 3 * sizeof(double);
+  double *d = nullptr;
+  const size_t total = 2 * cb + (size_t)N * sizeof(double) + 32 * sizeof(double);
+  HIP_TRY(hipMalloc(&d, total));
+  double *dref = d, *dconf = d + 3 * N, *dw = d + 6 * N, *dio = d + 7 * N;
+  int rc = RMSF_OK;
+  do {
+    hipError_t e;
+    if ((e = hipMemcpy(dref, h_ref, cb, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail("memcpy", e); break; }
+    if ((e = hipMemcpy(dconf, h_conf, cb, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail("memcpy", e); break; }
+    if (h_weights && (e = hipMemcpy(dw, h_weights, N * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess) {
+      rc = hip_fail("memcpy", e);
+      break;
+    }
+    hipLaunchKernelGGL(k_inner_product, dim3(1), dim3(1024), 0, 0, dref, dconf, h_weights ? dw : nullptr, N, dio);
+    if ((rc = after_launch("k_inner_product"))) break;
+    const double nd = (double)N;
+    if ((e = hipMemcpy(dio + 10, &nd, sizeof nd, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail("memcpy", e); break; }
+    hipLaunchKernelGGL(k_qcp_batch, dim3(1), dim3(kBlock), 0, 0, dio, dio + 9, dio + 10, (int64_t)1, dio + 11, dio + 20);
+    if ((rc = after_launch("k_qcp_batch"))) break;
+    double h[10];
+    if ((e = hipMemcpy(h, dio + 11, sizeof h, hipMemcpyDeviceToHost)) != hipSuccess) { rc = hip_fail("memcpy", e); break; }
+    for (int j = 0; j < 9; ++j) h_rot[j] = h[j];
+    if (rmsd_out) *rmsd_out = h[9];
+  } while (0);
+  (void)hipFree(d);
+  return rc;
+}
+
+RMSF_EXPORT int rmsf_synth_frames(float *d_out, int64_t fstride, int64_t n_atoms, int64_t f0, int64_t nf,
+                                  uint64_t seed, const double *d_motion, void *stream) {
+  if (!d_out || n_atoms < 1 || nf < 0 || f0 < 0 || fstride < 3 * n_atoms)
+    return fail(RMSF_EINVAL, "rmsf_synth_frames: bad arguments");
+  if (nf == 0) return RMSF_OK;
+  const int64_t total = nf * n_atoms;
+  const int64_t per_launch = (int64_t)kBlock * 0x7fffffffLL / 2;
+  for (int64_t done = 0; done < nf;) {
+    // keep each launch's element count (frames * atoms) under the grid limit
+    int64_t fchunk = std::max<int64_t>(1, per_launch / n_atoms);
+    fchunk = std::min(fchunk, nf - done);
+    hipLaunchKernelGGL(k_synth, dim3(grid1(fchunk * n_atoms)), dim3(kBlock), 0, S(stream), d_out + done * fstride,
+                       fstride, n_atoms, f0 + done, fchunk, seed, d_motion);
+    int rc = after_launch("k_synth");
+    if (rc) return rc;
+    done += fchunk;
+  }
+  (void)total;
+  return RMSF_OK;
+}
+
+}  // extern "C"

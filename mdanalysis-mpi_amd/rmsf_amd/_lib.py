@@ -1,0 +1,129 @@
+"""ctypes binding of ``librmsf_hip.so`` (the C ABI declared in include/rmsf_hip.h).
+
+This module is the only place that touches the shared library.  It fails
+loudly: there is no CPU fallback anywhere in the product path -- if the HIP
+library is missing or no HIP device is visible, callers get an exception.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_size_t, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "librmsf_hip.so"))
+
+RMSF_OK = 0
+RMSF_EINVAL = -1
+RMSF_EHIP = -2
+RMSF_ENOMEM = -3
+RMSF_EEMPTY = -4
+RMSF_MODE_WELFORD = 0
+RMSF_MODE_SUM = 1
+RMSF_XFORM_DOUBLES = 16
+RMSF_REFINFO_DOUBLES = 16
+ABI_VERSION = 1
+
+
+class RmsfError(RuntimeError):
+    """A non-zero status returned through the C ABI."""
+
+    def __init__(self, code: int, func: str, msg: str):
+        super().__init__(f"{func} failed with status {code}: {msg}")
+        self.code = code
+
+
+class RmsfEmptyError(RmsfError, ZeroDivisionError):
+    """No frames to reduce.  Subclasses ZeroDivisionError because RMSF.py:39
+    raises exactly that when two empty partials are merged."""
+
+
+# name -> (restype, argtypes); every symbol include/rmsf_hip.h declares.
+P = c_void_p
+SIGNATURES = {
+    "rmsf_abi_version": (c_int, []),
+    "rmsf_last_error": (c_char_p, []),
+    "rmsf_device_count": (c_int, [POINTER(c_int)]),
+    "rmsf_set_device": (c_int, [c_int]),
+    "rmsf_malloc": (c_int, [POINTER(c_void_p), c_size_t]),
+    "rmsf_free": (c_int, [P]),
+    "rmsf_memcpy_h2d": (c_int, [P, P, c_size_t, P]),
+    "rmsf_memcpy_d2h": (c_int, [P, P, c_size_t, P]),
+    "rmsf_stream_synchronize": (c_int, [P]),
+    "rmsf_block_range": (c_int, [c_int64, c_int, c_int, POINTER(c_int64), POINTER(c_int64)]),
+    "rmsf_reference_setup": (c_int, [P, P, c_int64, P, P, P, P, P]),
+    "rmsf_superpose_workspace_bytes": (c_size_t, [c_int64, c_int64]),
+    "rmsf_superpose": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, P, P, P, c_size_t, P]),
+    "rmsf_accumulate_splits": (c_int, [c_int64, c_int64, c_int]),
+    "rmsf_accumulate": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, c_int, c_int, P, P, P]),
+    "rmsf_split_count": (c_int64, [c_int64, c_int, c_int]),
+    "rmsf_chan_merge": (c_int, [P, P, P, c_int, c_int64, P, P, P]),
+    "rmsf_sum_splits": (c_int, [P, c_int, c_int64, P, P]),
+    "rmsf_divide": (c_int, [P, c_double, c_int64, P, P]),
+    "rmsf_chan_weight": (c_int, [P, c_double, c_int64, P, P]),
+    "rmsf_chan_deviation": (c_int, [P, P, P, c_double, c_int64, P, P]),
+    "rmsf_finalize": (c_int, [P, c_int64, c_int64, P, P]),
+    "rmsf_qcp_batch": (c_int, [P, P, P, c_int64, P, P, P]),
+    "rmsf_calc_rmsd_rotational_matrix": (c_int, [P, P, c_int64, P, P, POINTER(c_double)]),
+    "rmsf_synth_frames": (c_int, [P, c_int64, c_int64, c_int64, c_int64, c_uint64, P, P]),
+    "rmsf_stager_create": (c_int, [c_int64, c_int64, P, c_int64, c_int, c_int, POINTER(c_void_p)]),
+    "rmsf_stager_destroy": (c_int, [P]),
+    "rmsf_stager_stage": (c_int, [P, P, c_int64, c_int64, P, POINTER(c_int), POINTER(c_void_p)]),
+    "rmsf_stager_stage_ptrs": (c_int, [P, P, c_int64, P, POINTER(c_int), POINTER(c_void_p)]),
+    "rmsf_stager_release": (c_int, [P, c_int, P]),
+    "rmsf_stager_synchronize": (c_int, [P]),
+}
+
+_lib = None
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load the library (once) and declare every signature.
+
+    Raises ImportError with a build hint if the .so is missing -- the product
+    never falls back to a CPU path.
+    """
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError(
+            f"librmsf_hip.so not found at {p}; build it with "
+            "`make -C mdanalysis-mpi_amd/csrc` or `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError = a declared symbol is missing
+        fn.restype = res
+        fn.argtypes = args
+    v = lib.rmsf_abi_version()
+    if v != ABI_VERSION:
+        raise ImportError(f"librmsf_hip.so ABI {v} != expected {ABI_VERSION}")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc: int, func: str) -> None:
+    if rc != RMSF_OK:
+        msg = (_lib or load()).rmsf_last_error()
+        msg = msg.decode(errors="replace") if msg else ""
+        cls = RmsfEmptyError if rc == RMSF_EEMPTY else RmsfError
+        raise cls(rc, func, msg)
+
+
+def call(name: str, *args) -> int:
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    check(rc, name)
+    return rc
+
+
+def i64p(values) -> ctypes.Array:
+    arr = (c_int64 * len(values))(*[int(v) for v in values])
+    return arr
+
+
+def int32_array(values) -> ctypes.Array:
+    return (c_int32 * len(values))(*[int(v) for v in values])

@@ -1,0 +1,133 @@
+"""Device engine: thin typed wrappers around the C ABI on torch-allocated HBM.
+
+torch is plumbing here (the caching allocator for HBM buffers, the current
+HIP stream, torch.distributed for RCCL); every byte of arithmetic on the hot
+path runs in the hand-written HIP kernels of csrc/rmsf_kernels.hip.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import RMSF_MODE_SUM, RMSF_MODE_WELFORD, RMSF_REFINFO_DOUBLES, RMSF_XFORM_DOUBLES, call
+
+F64 = torch.float64
+F32 = torch.float32
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+class Engine:
+    """Launches the RMSF kernels on one device, on torch's current stream."""
+
+    def __init__(self, device: torch.device | int | str | None = None):
+        self.lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise RuntimeError("rmsf_amd needs a HIP device (MI355X); none is visible -- no CPU fallback exists")
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError(f"rmsf_amd runs on HIP devices only, got {self.device}")
+        call("rmsf_set_device", self.device.index if self.device.index is not None else 0)
+
+    # -- helpers -----------------------------------------------------------
+    @property
+    def stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def empty(self, *shape, dtype=F64) -> torch.Tensor:
+        return torch.empty(*shape, dtype=dtype, device=self.device)
+
+    def zeros(self, *shape, dtype=F64) -> torch.Tensor:
+        return torch.zeros(*shape, dtype=dtype, device=self.device)
+
+    def sel_tensor(self, sel) -> torch.Tensor | None:
+        if sel is None:
+            return None
+        s = torch.as_tensor(np.ascontiguousarray(sel, dtype=np.int32)).to(self.device)
+        return s
+
+    # -- kernels -----------------------------------------------------------
+    def reference_setup(self, n_sel: int, *, frame_ptr: int | None = None, avg: torch.Tensor | None = None,
+                        sel: torch.Tensor | None = None, masses: torch.Tensor | None = None):
+        """RMSF.py:80-87 (frame) / 113-118 (average): centred f64 reference + info."""
+        ref = self.empty(n_sel, 3)
+        info = self.empty(RMSF_REFINFO_DOUBLES)
+        call("rmsf_reference_setup", frame_ptr, _ptr(avg), n_sel, _ptr(sel if frame_ptr else None), _ptr(masses),
+             ref.data_ptr(), info.data_ptr(), self.stream)
+        return ref, info
+
+    def workspace_bytes(self, n_sel: int, n_frames: int) -> int:
+        return int(self.lib.rmsf_superpose_workspace_bytes(n_sel, n_frames))
+
+    def superpose(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, sel, masses, ref, refinfo,
+                  xform: torch.Tensor, work: torch.Tensor) -> None:
+        """RMSF.py:94-97,127-131 + get_rotation_matrix (RMSF.py:43-51): per-frame COM + QCP."""
+        call("rmsf_superpose", xyz_ptr, fstride, n_frames, n_sel, _ptr(sel), _ptr(masses), ref.data_ptr(),
+             refinfo.data_ptr(), xform.data_ptr(), work.data_ptr(), work.numel() * work.element_size(), self.stream)
+
+    def splits(self, n_sel: int, n_frames: int, aligned: bool) -> int:
+        return int(self.lib.rmsf_accumulate_splits(n_sel, n_frames, int(aligned)))
+
+    def split_counts(self, n_frames: int, n_splits: int) -> list[int]:
+        return [int(self.lib.rmsf_split_count(n_frames, n_splits, s)) for s in range(n_splits)]
+
+    def accumulate(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, sel, xform, refinfo, mode: int,
+                   n_splits: int, out0: torch.Tensor, out1: torch.Tensor | None) -> None:
+        """RMSF.py:99-103 (SUM) / 133-138 (WELFORD) over split frame tiles."""
+        call("rmsf_accumulate", xyz_ptr, fstride, n_frames, n_sel, _ptr(sel), _ptr(xform), _ptr(refinfo), mode,
+             n_splits, out0.data_ptr(), _ptr(out1), self.stream)
+
+    def chan_merge(self, mean_parts: torch.Tensor, m2_parts: torch.Tensor, counts, n_coord: int,
+                   mean_out: torch.Tensor, m2_out: torch.Tensor) -> None:
+        """second_order_moments (RMSF.py:36-41) folded over the partials in order."""
+        c = _lib.i64p(counts)
+        call("rmsf_chan_merge", mean_parts.data_ptr(), m2_parts.data_ptr(), ctypes.cast(c, ctypes.c_void_p),
+             len(counts), n_coord, mean_out.data_ptr(), m2_out.data_ptr(), self.stream)
+
+    def sum_splits(self, parts: torch.Tensor, n_parts: int, n: int, out: torch.Tensor) -> None:
+        call("rmsf_sum_splits", parts.data_ptr(), n_parts, n, out.data_ptr(), self.stream)
+
+    def divide(self, x: torch.Tensor, divisor: float, out: torch.Tensor) -> None:
+        call("rmsf_divide", x.data_ptr(), float(divisor), x.numel(), out.data_ptr(), self.stream)
+
+    def chan_weight(self, mean_k: torch.Tensor, w: float, out: torch.Tensor) -> None:
+        call("rmsf_chan_weight", mean_k.data_ptr(), float(w), mean_k.numel(), out.data_ptr(), self.stream)
+
+    def chan_deviation(self, mean_k, m2_k, mean, n_k: float, out) -> None:
+        call("rmsf_chan_deviation", mean_k.data_ptr(), m2_k.data_ptr(), mean.data_ptr(), float(n_k), mean_k.numel(),
+             out.data_ptr(), self.stream)
+
+    def finalize(self, m2: torch.Tensor, n_sel: int, n_frames: int, out: torch.Tensor) -> None:
+        """RMSF.py:146: sqrt(M2.sum(axis=1)/n)."""
+        call("rmsf_finalize", m2.data_ptr(), n_sel, n_frames, out.data_ptr(), self.stream)
+
+    def qcp_batch(self, A: torch.Tensor, E0: torch.Tensor, N: torch.Tensor):
+        n = A.shape[0]
+        rot = self.empty(n, 9)
+        rmsd = self.empty(n)
+        call("rmsf_qcp_batch", A.data_ptr(), E0.data_ptr(), N.data_ptr(), n, rot.data_ptr(), rmsd.data_ptr(),
+             self.stream)
+        return rot, rmsd
+
+    def synth_frames(self, out: torch.Tensor, n_atoms: int, f0: int, nf: int, seed: int,
+                     motion: torch.Tensor | None = None, fstride: int | None = None) -> None:
+        fstride = 3 * n_atoms if fstride is None else fstride
+        call("rmsf_synth_frames", out.data_ptr(), fstride, n_atoms, f0, nf, ctypes.c_uint64(seed).value,
+             _ptr(motion), self.stream)
+
+
+def block_range(n_frames: int, size: int, rank: int) -> tuple[int, int]:
+    """RMSF.py:63-72 through the C ABI (bit-exact integer arithmetic)."""
+    a, b = ctypes.c_int64(), ctypes.c_int64()
+    call("rmsf_block_range", n_frames, size, rank, ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+__all__ = ["Engine", "block_range", "RMSF_MODE_SUM", "RMSF_MODE_WELFORD", "RMSF_XFORM_DOUBLES"]

@@ -1,0 +1,224 @@
+"""The frame-parallel RMSF pipeline of RMSF.py, on HIP kernels.
+
+Per rank (one process per GPU):
+  align=None      Welford over the block                    (rms.RMSF.run)
+  align="frame0"  superpose every frame on frame ``ref_frame``, then Welford
+  align="average" RMSF.py exactly: sweep 1 superposes on frame ``ref_frame``
+                  and sums (RMSF.py:89-105); all-reduce + divide gives the
+                  average structure (RMSF.py:107-111); sweep 2 superposes on
+                  the centred average and runs Welford (RMSF.py:113-140).
+then the exact cross-rank Chan merge (RMSF.py:141-143) and the finalise
+(RMSF.py:145-146).  Every launch is asynchronous on the current stream; the
+only host synchronisation is the final copy of the result.
+"""
+from __future__ import annotations
+
+import contextlib
+from collections import defaultdict
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import parallel
+from ._lib import RMSF_MODE_SUM, RMSF_MODE_WELFORD, RMSF_XFORM_DOUBLES, RmsfEmptyError
+from .engine import Engine
+from .sources import Batch, FrameList
+
+ALIGN_MODES = (None, "frame0", "average")
+
+
+class KernelTimer:
+    """HIP-event spans recorded on the launching (current) stream around the
+    ABI calls of the pipeline -- used by bench.py for the per-kernel roofline."""
+
+    def __init__(self):
+        self.spans = defaultdict(list)
+
+    @contextlib.contextmanager
+    def span(self, name: str):
+        s = torch.cuda.current_stream()
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        yield
+        b.record(s)
+        self.spans[name].append((a, b))
+
+    def clear(self) -> None:
+        self.spans.clear()
+
+    def ms(self, name: str) -> list[float]:
+        torch.cuda.synchronize()
+        return [a.elapsed_time(b) for a, b in self.spans.get(name, [])]
+
+
+_NULL = contextlib.nullcontext()
+
+
+def _span(timer, name):
+    return timer.span(name) if timer is not None else _NULL
+
+
+class Accumulator:
+    """Running Welford (or f64 sum) over streamed batches, on device.
+
+    Layout: ``parts0/parts1`` are [1 + S_max, 3*n_sel] f64; slot 0 holds the
+    running result, slots 1..S the current batch's split partials, folded into
+    slot 0 by the Chan-merge kernel (or the split-sum kernel)."""
+
+    def __init__(self, eng: Engine, n_sel: int, mode: int, max_batch: int, aligned: bool,
+                 n_splits: int | None = None, timer: KernelTimer | None = None):
+        self.eng, self.n_sel, self.mode, self.aligned = eng, n_sel, mode, aligned
+        self.timer = timer
+        self.n_coord = 3 * n_sel
+        self.fixed_splits = n_splits
+        self.s_max = n_splits or eng.splits(n_sel, max_batch, aligned)
+        # only slot 0 (the running result) must start at zero: split slots are
+        # fully written by the accumulate kernel before they are read
+        self.parts0 = eng.empty(1 + self.s_max, self.n_coord)
+        self.parts0[0].zero_()
+        self.parts1 = None
+        if mode == RMSF_MODE_WELFORD:
+            self.parts1 = eng.empty(1 + self.s_max, self.n_coord)
+            self.parts1[0].zero_()
+        self.n = 0
+
+    def add(self, b: Batch, xform: torch.Tensor | None = None, refinfo: torch.Tensor | None = None) -> None:
+        eng = self.eng
+        s = self.fixed_splits or min(self.s_max, eng.splits(self.n_sel, b.n_frames, self.aligned))
+        with _span(self.timer, "accumulate"):
+            eng.accumulate(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, xform, refinfo, self.mode, s,
+                           self.parts0[1:], None if self.parts1 is None else self.parts1[1:])
+        if self.mode == RMSF_MODE_WELFORD:
+            counts = [self.n] + eng.split_counts(b.n_frames, s)
+            eng.chan_merge(self.parts0, self.parts1, counts, self.n_coord, self.parts0[0], self.parts1[0])
+        else:
+            eng.sum_splits(self.parts0, 1 + s, self.n_coord, self.parts0[0])
+        self.n += b.n_frames
+
+    @property
+    def result0(self) -> torch.Tensor:
+        return self.parts0[0]
+
+    @property
+    def result1(self) -> torch.Tensor:
+        return self.parts1[0]
+
+
+class Superposer:
+    """Per-frame COM + inner product + QCP for one batch (rmsf_superpose)."""
+
+    def __init__(self, eng: Engine, n_sel: int, max_batch: int, masses: torch.Tensor | None,
+                 timer: KernelTimer | None = None):
+        self.eng, self.n_sel, self.masses, self.timer = eng, n_sel, masses, timer
+        self.xform = eng.empty(max_batch, RMSF_XFORM_DOUBLES)
+        nbytes = eng.workspace_bytes(n_sel, max_batch)
+        self.work = eng.empty(max(1, (nbytes + 7) // 8))
+
+    def run(self, b: Batch, ref: torch.Tensor, refinfo: torch.Tensor) -> torch.Tensor:
+        xf = self.xform[: b.n_frames]
+        with _span(self.timer, "superpose"):
+            self.eng.superpose(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, self.masses, ref, refinfo, xf,
+                               self.work)
+        return xf
+
+
+@dataclass
+class PipelineResult:
+    rmsf: torch.Tensor            # f64 [n_sel]
+    mean: torch.Tensor            # f64 [n_sel, 3]
+    m2: torch.Tensor              # f64 [n_sel, 3]  (sum of squares, RMSF.py:120)
+    n_frames: int                 # frames over all ranks
+    n_local: int                  # frames of this rank's block
+    block: tuple[int, int]
+    average: torch.Tensor | None = None   # f64 [n_sel, 3] (align="average")
+    rmsd: torch.Tensor | None = None      # f64 [n_local] last-sweep QCP rmsd
+    extras: dict = field(default_factory=dict)
+
+
+def reference_from_frame(eng: Engine, source, frame: int, n_sel: int, masses, owner: int | None = None):
+    """RMSF.py:80-87: centred f64 reference of frame ``frame``.  In a sharded
+    run the rank holding the frame computes it and broadcasts (RMSF.py has
+    every rank re-read frame 0 from disk; the device equivalent is one
+    broadcast of 3*n_sel + 16 doubles)."""
+    rank, size = parallel.world()
+    if size > 1 and owner is not None:
+        ref = eng.empty(n_sel, 3)
+        info = eng.empty(16)
+        if rank == owner:
+            b = source.reference(frame, eng.stream)
+            r, i = eng.reference_setup(n_sel, frame_ptr=b.ptr, sel=b.sel, masses=masses)
+            b.done()
+            ref.copy_(r)
+            info.copy_(i)
+        parallel.broadcast_(ref, owner)
+        parallel.broadcast_(info, owner)
+        return ref, info
+    b = source.reference(frame, eng.stream)
+    r, i = eng.reference_setup(n_sel, frame_ptr=b.ptr, sel=b.sel, masses=masses)
+    b.done()
+    return r, i
+
+
+def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=None, ref_frame: int = 0,
+                 max_batch: int | None = None, n_splits: int | None = None, collect_rmsd: bool = False,
+                 ref_owner: int | None = None, block: tuple[int, int] | None = None,
+                 timer: KernelTimer | None = None) -> PipelineResult:
+    if align not in ALIGN_MODES:
+        raise ValueError(f"align must be one of {ALIGN_MODES}, got {align!r}")
+    rank, size = parallel.world()
+    n_total = len(frames)
+    if n_total == 0:
+        raise RmsfEmptyError(-4, "RMSF.run", "no frames selected")
+    b0, b1 = block if block is not None else parallel.blocks(n_total, size)[rank]
+    n_local = b1 - b0
+    n_sel = source.n_sel
+    if max_batch is None:
+        max_batch = max(1, n_local)
+    max_batch = max(1, min(max_batch, max(1, n_local)))
+    m_dev = None
+    if masses is not None:
+        m_dev = torch.as_tensor(np.ascontiguousarray(masses, dtype=np.float64)).to(eng.device)
+        if m_dev.numel() != n_sel:
+            raise ValueError("masses must have one entry per selected atom")
+    aligned = align is not None
+    sup = Superposer(eng, n_sel, max_batch, m_dev, timer) if aligned else None
+    rmsd = eng.empty(n_local) if (aligned and collect_rmsd) else None
+    average = None
+
+    def sweep(acc: Accumulator, ref=None, info=None):
+        done = 0
+        for b in source.batches(frames, b0, b1, max_batch, eng.stream):
+            xf = None
+            if aligned:
+                xf = sup.run(b, ref, info)
+                if rmsd is not None:
+                    rmsd[done:done + b.n_frames].copy_(xf[:, 12])
+            acc.add(b, xf, info)
+            done += b.n_frames
+            b.done()
+
+    if align == "average":
+        ref0, info0 = reference_from_frame(eng, source, ref_frame, n_sel, m_dev, ref_owner)
+        acc1 = Accumulator(eng, n_sel, RMSF_MODE_SUM, max_batch, True, n_splits, timer)
+        if n_local:
+            sweep(acc1, ref0, info0)
+        total = parallel.allreduce_sum_(acc1.result0)       # RMSF.py:110
+        average = eng.empty(3 * n_sel)
+        eng.divide(total, float(n_total), average)          # RMSF.py:111
+        ref, info = eng.reference_setup(n_sel, avg=average, masses=m_dev)  # RMSF.py:113-118
+    elif align == "frame0":
+        ref, info = reference_from_frame(eng, source, ref_frame, n_sel, m_dev, ref_owner)
+    else:
+        ref = info = None
+
+    acc = Accumulator(eng, n_sel, RMSF_MODE_WELFORD, max_batch, aligned, n_splits, timer)
+    if n_local:
+        sweep(acc, ref, info)
+    mean, m2 = parallel.global_chan(eng, acc.result0, acc.result1, acc.n, n_total)  # RMSF.py:141-143
+    rmsf = eng.empty(n_sel)
+    eng.finalize(m2, n_sel, n_total, rmsf)                   # RMSF.py:146
+    return PipelineResult(rmsf=rmsf, mean=mean.view(n_sel, 3), m2=m2.view(n_sel, 3), n_frames=n_total,
+                          n_local=n_local, block=(b0, b1),
+                          average=None if average is None else average.view(n_sel, 3), rmsd=rmsd)

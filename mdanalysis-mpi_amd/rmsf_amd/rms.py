@@ -1,0 +1,124 @@
+"""``RMSF`` -- drop-in for ``MDAnalysis.analysis.rms.RMSF`` on MI355X.
+
+The reference (RMSF.py:1-18) states its workflow as::
+
+    average = align.AverageStructure(u, u, select='protein and name CA', ref_frame=0).run()
+    aligner = align.AlignTraj(u, average.results.universe, select='protein and name CA', in_memory=True).run()
+    R = rms.RMSF(c_alphas).run()            # -> R.results.rmsf
+
+and implements it with mpi4py frame blocks.  ``RMSF(ag, align="average")``
+computes exactly that (the two sweeps of RMSF.py:89-140), ``align=None`` is
+plain ``rms.RMSF`` on an already-aligned trajectory, and ``align="frame0"``
+superposes every frame on ``ref_frame`` first (config C3).  Under
+``torch.distributed`` (one process per GPU) the frames are split into the
+contiguous blocks of RMSF.py:65-69 and merged with RCCL.
+
+Inputs: an MDAnalysis AtomGroup, a host ``numpy`` float32 array
+[n_frames, n_atoms, 3], or an HBM-resident torch tensor of that shape.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import parallel
+from .engine import Engine
+from .pipeline import run_pipeline
+from .sources import AtomGroupSource, DeviceSource, FrameList, HostSource
+
+
+class Results(dict):
+    """Attribute-access dict, like ``MDAnalysis.analysis.base.Results``."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+class RMSF:
+    """Per-atom root-mean-square fluctuation, ``results.rmsf`` (f64 [n_sel]).
+
+    Parameters
+    ----------
+    atomgroup : MDAnalysis AtomGroup | np.ndarray | torch.Tensor
+        The selection to analyse, or a float32 trajectory [F, n_atoms, 3].
+    select : array of int, optional
+        Atom indices (array inputs only); default all atoms.
+    align : None | "frame0" | "average"
+        Superposition before the statistics (see module docstring).
+    masses : array, optional
+        Per-selected-atom masses for the centre of mass (RMSF.py:84,94 use
+        ``center_of_mass``); default uniform.  For an AtomGroup the group's
+        masses are used.
+    ref_frame : int
+        Trajectory frame of the first reference (RMSF.py:63).
+    """
+
+    def __init__(self, atomgroup, *, select=None, align=None, masses=None, ref_frame: int = 0,
+                 device=None, batch_frames: int | None = None, n_splits: int | None = None,
+                 collect_rmsd: bool = False, verbose: bool = False, **kwargs):
+        self._input = atomgroup
+        self.select = select
+        self.align = align
+        self.masses = masses
+        self.ref_frame = ref_frame
+        self.device = device
+        self.batch_frames = batch_frames
+        self.n_splits = n_splits
+        self.collect_rmsd = collect_rmsd
+        self.verbose = verbose
+        self.results = Results()
+        self._source = None
+
+    # MDAnalysis AnalysisBase compatible signature
+    def run(self, start=None, stop=None, step=None, frames=None, verbose=None, **kwargs):
+        if frames is not None:
+            raise NotImplementedError("explicit frame lists are not supported; use start/stop/step")
+        eng = Engine(self.device)
+        src, masses = self._make_source(eng)
+        fl = FrameList(src.n_traj, start, stop, step)
+        rank, size = parallel.world()
+        if verbose if verbose is not None else self.verbose:
+            b0, b1 = parallel.blocks(len(fl), size)[rank]
+            print("Process:%3d --> Frames: %10d -- %10d" % (rank, b0, b1))  # RMSF.py:74
+        res = run_pipeline(eng, src, fl, align=self.align, masses=masses, ref_frame=self.ref_frame,
+                           max_batch=self.batch_frames, n_splits=self.n_splits, collect_rmsd=self.collect_rmsd)
+        torch.cuda.current_stream(eng.device).synchronize()
+        r = self.results
+        r.rmsf = res.rmsf.cpu().numpy()
+        r.mean = res.mean.cpu().numpy()
+        r.sumsquares = res.m2.cpu().numpy()
+        r.n_frames = res.n_frames
+        r.n_local = res.n_local
+        r.block = res.block
+        if res.average is not None:
+            r.average = res.average.cpu().numpy()
+        if res.rmsd is not None:
+            r.rmsd = res.rmsd.cpu().numpy()
+        self.n_frames = res.n_frames
+        return self
+
+    @property
+    def rmsf(self):
+        return self.results.rmsf
+
+    def _make_source(self, eng: Engine):
+        x = self._input
+        if isinstance(x, torch.Tensor):
+            if x.device.type != "cuda":
+                x = x.detach().cpu().numpy()
+            else:
+                return DeviceSource(x, self.select), self.masses
+        if isinstance(x, np.ndarray):
+            return HostSource(x, self.select, batch_frames=self.batch_frames), self.masses
+        if hasattr(x, "universe") and hasattr(x, "positions"):
+            masses = self.masses
+            if masses is None and self.align is not None:
+                masses = np.asarray(x.masses, dtype=np.float64)
+            return AtomGroupSource(x, batch_frames=self.batch_frames), masses
+        raise TypeError(f"unsupported input {type(x)!r}: AtomGroup, numpy array or HIP torch tensor expected")

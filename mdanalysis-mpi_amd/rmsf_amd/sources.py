@@ -1,0 +1,229 @@
+"""Frame sources: where device frame blocks come from.
+
+RMSF.py reads frames with ``universe.trajectory[frame]`` (RMSF.py:92,124) and
+re-decodes them on every sweep.  Here a source yields *device* batches of
+frames (pointer, frame stride, count, selection) for a range of positions in
+the frame list:
+
+  * ``DeviceSource``  a float32 trajectory already resident in HBM (torch
+    tensor [F, n_atoms, 3]); zero-copy, the selection is gathered in-kernel.
+  * ``HostSource``    a host numpy float32 array, streamed through the pinned
+    double-buffered ``Stager`` (C++ in csrc/stager.cpp).
+  * ``AtomGroupSource`` an MDAnalysis AtomGroup (when MDAnalysis is present):
+    ``ag.positions`` per Timestep, batched through the same stager.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Callable, Iterator
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call
+
+
+@dataclass
+class Batch:
+    ptr: int                      # device pointer of the first frame of the batch
+    fstride: int                  # floats between consecutive frames
+    n_frames: int
+    sel: torch.Tensor | None      # int32 device selection (None = atoms 0..n_sel-1)
+    release: Callable[[], None] | None = None
+
+    def done(self) -> None:
+        if self.release is not None:
+            self.release()
+            self.release = None
+
+
+class Stager:
+    """ctypes handle on the C++ pinned multi-buffer stager (rmsf_stager_*)."""
+
+    def __init__(self, n_atoms_frame: int, n_sel: int, sel, batch_frames: int, n_slots: int = 3,
+                 n_threads: int = 4):
+        self._h = ctypes.c_void_p()
+        self._sel = None if sel is None else np.ascontiguousarray(sel, dtype=np.int32)
+        sp = None if self._sel is None else self._sel.ctypes.data
+        call("rmsf_stager_create", n_atoms_frame, n_sel, sp, batch_frames, n_slots, n_threads,
+             ctypes.byref(self._h))
+        self.batch_frames = batch_frames
+        self.n_sel = n_sel
+
+    def stage(self, host: np.ndarray, first: int, step: int, n: int, stream: int) -> tuple[int, int]:
+        """Stage frames host[first], host[first+step], ... (n of them)."""
+        slot, dptr = ctypes.c_int(), ctypes.c_void_p()
+        frame_floats = host.shape[1] * 3
+        base = host.ctypes.data + first * frame_floats * 4
+        call("rmsf_stager_stage", self._h, base, frame_floats * step, n, stream, ctypes.byref(slot),
+             ctypes.byref(dptr))
+        return slot.value, dptr.value
+
+    def stage_compact(self, buf: np.ndarray, n: int, stream: int) -> tuple[int, int]:
+        slot, dptr = ctypes.c_int(), ctypes.c_void_p()
+        call("rmsf_stager_stage", self._h, buf.ctypes.data, buf.shape[1] * 3, n, stream, ctypes.byref(slot),
+             ctypes.byref(dptr))
+        return slot.value, dptr.value
+
+    def release(self, slot: int, stream: int) -> None:
+        call("rmsf_stager_release", self._h, slot, stream)
+
+    def synchronize(self) -> None:
+        call("rmsf_stager_synchronize", self._h)
+
+    def close(self) -> None:
+        if self._h:
+            call("rmsf_stager_destroy", self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class FrameList:
+    """The frame positions ``range(start, stop, step)`` of RMSF.run()."""
+
+    def __init__(self, n_traj: int, start=None, stop=None, step=None):
+        self.r = range(n_traj)[slice(start, stop, step)]
+
+    def __len__(self) -> int:
+        return len(self.r)
+
+    @property
+    def start(self) -> int:
+        return self.r.start
+
+    @property
+    def step(self) -> int:
+        return self.r.step
+
+
+class DeviceSource:
+    """HBM-resident float32 trajectory [F_local, n_atoms, 3] holding global frames
+    [offset, offset + F_local) of a trajectory with ``n_traj`` frames."""
+
+    def __init__(self, traj: torch.Tensor, sel=None, offset: int = 0, n_traj: int | None = None):
+        if traj.dtype != torch.float32 or traj.device.type != "cuda":
+            raise TypeError("DeviceSource needs a float32 tensor on a HIP device")
+        if traj.dim() != 3 or traj.shape[2] != 3:
+            raise ValueError("trajectory must be [n_frames, n_atoms, 3]")
+        if traj.stride(2) != 1 or traj.stride(1) != 3:
+            raise ValueError("trajectory frames must be contiguous [n_atoms, 3] rows")
+        self.traj = traj
+        self.n_atoms = traj.shape[1]
+        self.fstride = traj.stride(0)
+        self.offset = offset
+        self.n_traj = traj.shape[0] + offset if n_traj is None else n_traj
+        self.sel_host = None if sel is None else np.ascontiguousarray(sel, dtype=np.int64)
+        if self.sel_host is not None:
+            if self.sel_host.size and (self.sel_host.min() < 0 or self.sel_host.max() >= self.n_atoms):
+                raise IndexError("selection index out of range")
+        self.n_sel = self.n_atoms if sel is None else len(self.sel_host)
+        self.sel_dev = None
+        if self.sel_host is not None and not np.array_equal(self.sel_host, np.arange(self.n_sel)):
+            self.sel_dev = torch.as_tensor(self.sel_host.astype(np.int32)).to(traj.device)
+
+    def holds(self, frame: int) -> bool:
+        return self.offset <= frame < self.offset + self.traj.shape[0]
+
+    def _ptr(self, frame: int) -> int:
+        if not self.holds(frame):
+            raise IndexError(f"frame {frame} is not resident in this shard")
+        return self.traj.data_ptr() + (frame - self.offset) * self.fstride * 4
+
+    def reference(self, frame: int, stream: int) -> Batch:
+        return Batch(self._ptr(frame), self.fstride, 1, self.sel_dev)
+
+    def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
+        for i in range(b0, b1, max_frames):
+            n = min(max_frames, b1 - i)
+            yield Batch(self._ptr(frames.r[i]), self.fstride * frames.step, n, self.sel_dev)
+
+
+class HostSource:
+    """Host float32 array [F, n_atoms, 3] streamed through the pinned stager."""
+
+    def __init__(self, traj: np.ndarray, sel=None, batch_frames: int | None = None, n_slots: int = 3,
+                 n_threads: int = 4):
+        traj = np.ascontiguousarray(traj, dtype=np.float32)
+        if traj.ndim != 3 or traj.shape[2] != 3:
+            raise ValueError("trajectory must be [n_frames, n_atoms, 3]")
+        self.traj = traj
+        self.n_traj, self.n_atoms = traj.shape[0], traj.shape[1]
+        sel_arr = None if sel is None else np.ascontiguousarray(sel, dtype=np.int64)
+        if sel_arr is not None and sel_arr.size and (sel_arr.min() < 0 or sel_arr.max() >= self.n_atoms):
+            raise IndexError("selection index out of range")
+        self.n_sel = self.n_atoms if sel_arr is None else len(sel_arr)
+        if batch_frames is None:  # ~64 MB per slot
+            batch_frames = max(1, min(4096, (64 << 20) // max(1, 12 * self.n_sel)))
+        self.batch_frames = batch_frames
+        self.stager = Stager(self.n_atoms, self.n_sel, sel_arr, batch_frames, n_slots, n_threads)
+
+    def holds(self, frame: int) -> bool:
+        return 0 <= frame < self.n_traj
+
+    def reference(self, frame: int, stream: int) -> Batch:
+        slot, ptr = self.stager.stage(self.traj, frame, 1, 1, stream)
+        return Batch(ptr, 3 * self.n_sel, 1, None, lambda: self.stager.release(slot, stream))
+
+    def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
+        bf = min(max_frames, self.batch_frames)
+        for i in range(b0, b1, bf):
+            n = min(bf, b1 - i)
+            slot, ptr = self.stager.stage(self.traj, frames.r[i], frames.step, n, stream)
+            yield Batch(ptr, 3 * self.n_sel, n, None, lambda s=slot: self.stager.release(s, stream))
+
+
+class AtomGroupSource:
+    """MDAnalysis AtomGroup: per-Timestep ``ag.positions`` (the selection rows,
+    RMSF.py:95,128) packed into a host batch and staged to the device."""
+
+    def __init__(self, atomgroup, batch_frames: int | None = None, n_slots: int = 3):
+        self.ag = atomgroup
+        self.traj = atomgroup.universe.trajectory
+        self.n_traj = len(self.traj)
+        self.n_sel = len(atomgroup)
+        if batch_frames is None:
+            batch_frames = max(1, min(1024, (32 << 20) // max(1, 12 * self.n_sel)))
+        self.batch_frames = batch_frames
+        self.stager = Stager(self.n_sel, self.n_sel, None, batch_frames, n_slots, 1)
+        self._bufs = [np.empty((batch_frames, self.n_sel, 3), np.float32) for _ in range(n_slots)]
+        self._next = 0
+
+    def holds(self, frame: int) -> bool:
+        return 0 <= frame < self.n_traj
+
+    def _buf(self) -> np.ndarray:
+        b = self._bufs[self._next]
+        self._next = (self._next + 1) % len(self._bufs)
+        return b
+
+    def reference(self, frame: int, stream: int) -> Batch:
+        cur = self.traj.ts.frame
+        try:
+            self.traj[frame]
+            buf = self._buf()
+            buf[0] = self.ag.positions
+        finally:
+            self.traj[cur]
+        slot, ptr = self.stager.stage_compact(buf, 1, stream)
+        return Batch(ptr, 3 * self.n_sel, 1, None, lambda: self.stager.release(slot, stream))
+
+    def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
+        bf = min(max_frames, self.batch_frames)
+        for i in range(b0, b1, bf):
+            n = min(bf, b1 - i)
+            buf = self._buf()
+            for j in range(n):
+                self.traj[frames.r[i + j]]
+                buf[j] = self.ag.positions
+            slot, ptr = self.stager.stage_compact(buf, n, stream)
+            yield Batch(ptr, 3 * self.n_sel, n, None, lambda s=slot: self.stager.release(s, stream))
+
+
+__all__ = ["Batch", "Stager", "FrameList", "DeviceSource", "HostSource", "AtomGroupSource", "_lib"]

@@ -1,0 +1,201 @@
+"""GPU tier, kernel level: every HIP kernel against the oracle through the C ABI.
+
+Tolerances: integer/index work and the synthetic generator are bit-exact;
+floating point follows the north star's 1e-6 A absolute bound on RMSF and
+tighter bounds on intermediate f64 quantities (stated per assertion)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import rmsf_oracle as O
+from oracle import synth as SY
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from rmsf_amd.engine import Engine
+    return Engine()
+
+
+def _sync():
+    torch.cuda.synchronize()
+
+
+def test_synth_bit_exact(eng):
+    from rmsf_amd.synth import generate, motion_table
+    d = np.load(os.path.join(GOLDEN, "synth_slice.npz"))
+    g = generate(eng, 100, 0, 4, seed=5)
+    gm = generate(eng, 100, 0, 4, seed=5, motion=d["motion"])
+    _sync()
+    np.testing.assert_array_equal(g.cpu().numpy(), d["frames"])
+    np.testing.assert_array_equal(gm.cpu().numpy(), d["frames_motion"])
+    # a large, odd-shaped slice deep into a big trajectory
+    mt = motion_table(1, 5000)
+    big = generate(eng, 1001, 4990, 10, seed=123, motion=mt)
+    _sync()
+    np.testing.assert_array_equal(big.cpu().numpy()[3:7, 200:400], SY.frames(123, 1001, 4993, 4, mt, np.arange(200, 400)))
+
+
+def test_qcp_known_answer_device(eng):
+    from rmsf_amd import CalcRMSDRotationalMatrix
+    d = np.load(os.path.join(GOLDEN, "qcp_kat.npz"))
+    ref = d["ref"] - d["ref"].mean(0)
+    mob = d["mob"] - d["mob"].mean(0)
+    rot = np.zeros(9)
+    rmsd = CalcRMSDRotationalMatrix(ref, mob, 7, rot, None)
+    assert rmsd == pytest.approx(0.7191064509622, abs=1e-12)
+    np.testing.assert_allclose(rot.reshape(3, 3), d["rot"], atol=1e-7)
+    with pytest.raises(ValueError):
+        CalcRMSDRotationalMatrix(ref.astype(np.float32), mob, 7, rot, None)
+    w = np.random.default_rng(0).uniform(0.5, 2, 7)
+    rot_w = np.zeros(9)
+    r_w = CalcRMSDRotationalMatrix(ref, mob, 7, rot_w, w)
+    rot_o = np.zeros(9)
+    r_o = O.CalcRMSDRotationalMatrix(ref, mob, 7, rot_o, w)
+    assert r_w == pytest.approx(r_o, abs=1e-12)
+    np.testing.assert_allclose(rot_w, rot_o, atol=1e-12)
+
+
+def test_qcp_batch_vs_oracle(eng):
+    rng = np.random.default_rng(5)
+    As, E0s, Ns, exp = [], [], [], []
+    for i in range(300):
+        n = int(rng.integers(3, 200))
+        ref = rng.normal(size=(n, 3)) * 10
+        mob = ref @ O.kabsch(rng.normal(size=(3, 3)), rng.normal(size=(3, 3))) + rng.normal(size=(n, 3))
+        ref -= ref.mean(0)
+        mob -= mob.mean(0)
+        A, E0 = O.inner_product(ref, mob)
+        As.append(A)
+        E0s.append(E0)
+        Ns.append(n)
+        exp.append(O.fast_calc_rmsd_and_rotation(A, E0, float(n)))
+    dev = lambda a: torch.tensor(np.asarray(a, dtype=np.float64), device=eng.device)
+    rot, rmsd = eng.qcp_batch(dev(As), dev(E0s), dev(Ns))
+    _sync()
+    np.testing.assert_allclose(rot.cpu().numpy(), np.array([e[0] for e in exp]), atol=1e-13)
+    np.testing.assert_allclose(rmsd.cpu().numpy(), np.array([e[1] for e in exp]), atol=1e-11)
+
+
+@pytest.mark.parametrize("masses", [False, True])
+@pytest.mark.parametrize("gather", [False, True])
+def test_reference_setup(eng, masses, gather):
+    rng = np.random.default_rng(2)
+    frame = SY.frames(3, 500, 7, 1)[0]
+    sel = np.sort(rng.choice(500, 120, replace=False)) if gather else np.arange(500)
+    m = rng.uniform(1, 16, len(sel)) if masses else None
+    fdev = torch.tensor(frame, device=eng.device)
+    sdev = torch.tensor(sel.astype(np.int32), device=eng.device) if gather else None
+    mdev = torch.tensor(m, device=eng.device) if masses else None
+    ref, info = eng.reference_setup(len(sel), frame_ptr=fdev.data_ptr(), sel=sdev, masses=mdev)
+    _sync()
+    com, rc = O.centred_reference(frame[sel], m)
+    np.testing.assert_allclose(info.cpu().numpy()[:3], com, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(ref.cpu().numpy(), rc, rtol=0, atol=1e-12)
+    # from a float64 average
+    avg = torch.tensor(rc + 3.0, device=eng.device).reshape(-1)
+    ref2, info2 = eng.reference_setup(len(sel), avg=avg, masses=mdev)
+    _sync()
+    com2, rc2 = O.centred_reference(rc + 3.0, m)
+    np.testing.assert_allclose(ref2.cpu().numpy(), rc2, atol=1e-12)
+
+
+@pytest.mark.parametrize("gather", [False, True])
+def test_superpose_vs_oracle(eng, gather):
+    from rmsf_amd.synth import generate, motion_table
+    n_atoms, nf = 5000 if not gather else 9000, 37
+    mt = motion_table(4, nf)
+    traj = generate(eng, n_atoms, 0, nf, seed=9, motion=mt)
+    sel = np.sort(np.random.default_rng(1).choice(n_atoms, 4500, replace=False)) if gather else np.arange(n_atoms)
+    sdev = torch.tensor(sel.astype(np.int32), device=eng.device) if gather else None
+    ref, info = eng.reference_setup(len(sel), frame_ptr=traj.data_ptr(), sel=sdev)
+    xf = eng.empty(nf, 16)
+    work = eng.empty(eng.workspace_bytes(len(sel), nf) // 8 + 1)
+    eng.superpose(traj.data_ptr(), 3 * n_atoms, nf, len(sel), sdev, None, ref, info, xf, work)
+    _sync()
+    xf = xf.cpu().numpy()
+    host = traj.cpu().numpy()
+    ref_com, ref_c = O.centred_reference(host[0][sel])
+    for f in range(nf):
+        p = host[f][sel]
+        com = O.center_of_mass(p)
+        R = O.get_rotation_matrix(ref_c, p.astype(np.float64) - com, len(sel))
+        np.testing.assert_allclose(xf[f, 9:12], com, atol=1e-9)
+        np.testing.assert_allclose(xf[f, :9].reshape(3, 3), R, atol=1e-10)
+
+
+@pytest.mark.parametrize("n_sel,nf,splits", [(4096, 1000, None), (4096, 1000, 7), (1001, 333, None),
+                                              (3, 5, 1), (100_000, 64, None)])
+def test_welford_noalign(eng, n_sel, nf, splits):
+    from rmsf_amd.synth import generate
+    from rmsf_amd._lib import RMSF_MODE_WELFORD
+    traj = generate(eng, n_sel, 0, nf, seed=21)
+    s = splits or eng.splits(n_sel, nf, False)
+    mp = eng.empty(s, 3 * n_sel)
+    qp = eng.empty(s, 3 * n_sel)
+    eng.accumulate(traj.data_ptr(), 3 * n_sel, nf, n_sel, None, None, None, RMSF_MODE_WELFORD, s, mp, qp)
+    mean, m2 = eng.empty(3 * n_sel), eng.empty(3 * n_sel)
+    eng.chan_merge(mp, qp, eng.split_counts(nf, s), 3 * n_sel, mean, m2)
+    rmsf = eng.empty(n_sel)
+    eng.finalize(m2, n_sel, nf, rmsf)
+    _sync()
+    host = traj.cpu().numpy()
+    x = host.astype(np.float64)
+    np.testing.assert_allclose(mean.cpu().numpy().reshape(-1, 3), x.mean(0), rtol=0, atol=1e-10)
+    np.testing.assert_allclose(rmsf.cpu().numpy(), O.rmsf_two_pass(host), rtol=0, atol=1e-9)
+    if n_sel == 4096 and nf == 1000:
+        d = np.load(os.path.join(GOLDEN, "noalign_4096.npz"))
+        np.testing.assert_allclose(rmsf.cpu().numpy(), d["rmsf_P1"], rtol=0, atol=1e-9)
+
+
+def test_chan_merge_kernel_many_groups(eng):
+    """>128 partials exercise the grouped launches; counts with empties."""
+    rng = np.random.default_rng(0)
+    counts = [int(c) for c in rng.integers(0, 5, 300)]
+    counts[0] = 0
+    n = 33
+    data = [rng.normal(size=(c, n)) for c in counts]
+    mp = np.stack([d.mean(0) if len(d) else np.zeros(n) for d in data])
+    qp = np.stack([((d - d.mean(0)) ** 2).sum(0) if len(d) else np.zeros(n) for d in data])
+    mean, m2 = eng.empty(n), eng.empty(n)
+    eng.chan_merge(torch.tensor(mp, device=eng.device), torch.tensor(qp, device=eng.device), counts, n, mean, m2)
+    _sync()
+    allx = np.concatenate([d for d in data if len(d)])
+    np.testing.assert_allclose(mean.cpu().numpy(), allx.mean(0), atol=1e-12)
+    np.testing.assert_allclose(m2.cpu().numpy(), ((allx - allx.mean(0)) ** 2).sum(0), rtol=1e-11)
+    from rmsf_amd import RmsfEmptyError
+    with pytest.raises(ZeroDivisionError):
+        eng.chan_merge(torch.tensor(mp, device=eng.device), torch.tensor(qp, device=eng.device), [0] * 300, n,
+                       mean, m2)
+    assert issubclass(RmsfEmptyError, ZeroDivisionError)
+
+
+def test_second_order_moments_api(eng):
+    from rmsf_amd import second_order_moments
+    rng = np.random.default_rng(1)
+    a, b = rng.normal(size=(7, 10, 3)), rng.normal(size=(4, 10, 3)) + 1
+    S1 = [7, a.mean(0), ((a - a.mean(0)) ** 2).sum(0)]
+    S2 = [4, b.mean(0), ((b - b.mean(0)) ** 2).sum(0)]
+    T, mu, M = second_order_moments(S1, S2)
+    Te, mue, Me = O.second_order_moments(S1, S2)
+    assert T == Te
+    np.testing.assert_allclose(mu, mue, atol=1e-14)
+    np.testing.assert_allclose(M, Me, rtol=1e-13)
+    with pytest.raises(ZeroDivisionError):
+        second_order_moments([0, np.zeros((10, 3)), np.zeros((10, 3))], [0, np.zeros((10, 3)), np.zeros((10, 3))])
+
+
+def test_error_paths(eng):
+    from rmsf_amd import RmsfError
+    from rmsf_amd._lib import RMSF_MODE_WELFORD
+    x = eng.empty(10, 3, dtype=torch.float32)
+    out = eng.empty(30)
+    with pytest.raises(RmsfError, match="bad arguments"):
+        eng.accumulate(x.data_ptr(), 3, 10, 0, None, None, None, RMSF_MODE_WELFORD, 1, out, out)
+    with pytest.raises(RmsfError, match="4096"):
+        eng.accumulate(x.data_ptr(), 30, 10000, 10, None, None, None, RMSF_MODE_WELFORD, 1, out, out)

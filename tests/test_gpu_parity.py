@@ -1,0 +1,139 @@
+"""GPU tier, end to end: ``RMSF(...).run().results.rmsf`` on the HIP path vs the
+oracle restatement of RMSF.py, within the north star's 1e-6 A (absolute).
+
+Covers the three modes (None / frame0 / average = RMSF.py), device-resident
+and host-streamed (pinned stager) inputs, gathered selections, masses, frame
+slicing, split/batch invariance, edge cases, and -- at the full 100k-atom
+size -- slice checks regenerated on the CPU."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import rmsf_oracle as O
+from oracle import synth as SY
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-6  # Angstrom, absolute (north star)
+
+
+@pytest.fixture(scope="module")
+def c1():
+    d = np.load(os.path.join(GOLDEN, "c1_synth.npz"))
+    traj = SY.frames(int(d["seed"]), int(d["n_atoms"]), 0, int(d["n_frames"]), d["motion"])
+    return d, traj
+
+
+@pytest.mark.parametrize("align,tag", [(None, "none"), ("frame0", "frame0"), ("average", "average")])
+@pytest.mark.parametrize("where", ["device", "host"])
+def test_c1_modes_vs_golden(c1, align, tag, where):
+    from rmsf_amd import RMSF
+    d, traj = c1
+    x = torch.tensor(traj, device="cuda") if where == "device" else traj
+    r = RMSF(x, select=d["sel"], align=align).run()
+    np.testing.assert_allclose(r.results.rmsf, d[f"rmsf_{tag}_P1"], rtol=0, atol=TOL)
+    np.testing.assert_allclose(r.results.mean, d[f"mean_{tag}"], rtol=0, atol=1e-6)
+    assert r.results.n_frames == 98
+    if align == "average":
+        np.testing.assert_allclose(r.results.average, d["average"], rtol=0, atol=1e-9)
+
+
+def test_c1_masses_and_slices(c1):
+    from rmsf_amd import RMSF
+    d, traj = c1
+    x = torch.tensor(traj, device="cuda")
+    r = RMSF(x, select=d["sel"], align="average", masses=d["masses"]).run()
+    np.testing.assert_allclose(r.results.rmsf, d["rmsf_average_masses_P2"], atol=TOL)
+    r = RMSF(x, select=d["sel"], align="average").run(start=3, stop=90, step=2)
+    np.testing.assert_allclose(r.results.rmsf, d["rmsf_average_slice"], atol=TOL)
+    r = RMSF(traj, select=d["sel"], align="average", batch_frames=7).run(start=3, stop=90, step=2)
+    np.testing.assert_allclose(r.results.rmsf, d["rmsf_average_slice"], atol=TOL)
+
+
+@pytest.mark.parametrize("batch,splits", [(1, 1), (5, 2), (13, None), (98, 3)])
+def test_batch_and_split_invariance(c1, batch, splits):
+    """Frame tiles inside a GPU (splits) and streamed batches are merged by the
+    same Chan kernel as ranks are; any cut gives the same answer."""
+    from rmsf_amd import RMSF
+    d, traj = c1
+    x = torch.tensor(traj, device="cuda")
+    r = RMSF(x, select=d["sel"], align="average", batch_frames=batch, n_splits=splits).run()
+    np.testing.assert_allclose(r.results.rmsf, d["rmsf_average_P1"], atol=TOL)
+
+
+def test_edges():
+    from rmsf_amd import RMSF, RmsfEmptyError
+    d = np.load(os.path.join(GOLDEN, "edges.npz"))
+    t3 = SY.frames(int(d["seed"]), int(d["n_atoms"]), 0, 3, d["motion"])
+    one = RMSF(torch.tensor(t3[:1], device="cuda"), align="average").run()
+    np.testing.assert_array_equal(one.results.rmsf, 0.0)  # RMSF of one frame is exactly 0
+    ident = RMSF(np.repeat(t3[:1], 10, axis=0), align="average").run()
+    assert ident.results.rmsf.max() < 1e-6
+    r = RMSF(torch.tensor(t3, device="cuda"), align="average").run()
+    np.testing.assert_allclose(r.results.rmsf, d["p1_of_3"], atol=TOL)
+    with pytest.raises(ZeroDivisionError):
+        RMSF(torch.tensor(t3, device="cuda")).run(start=2, stop=2)
+    assert issubclass(RmsfEmptyError, ZeroDivisionError)
+
+
+def test_rigid_motion_removed():
+    """Analytic: rigid copies of one structure -> RMSF at the f32 floor."""
+    from rmsf_amd import RMSF
+    from rmsf_amd.synth import motion_table
+    one = SY.frames(40, 3000, 0, 1)[0].astype(np.float64) - 50.0
+    mt = motion_table(41, 64)
+    traj = np.stack([(one @ mt[f, :9].reshape(3, 3) + mt[f, 9:]).astype(np.float32) for f in range(64)])
+    r = RMSF(torch.tensor(traj, device="cuda"), align="frame0").run()
+    assert r.results.rmsf.max() < 2e-5
+    exp = O.rmsf_script(traj, None, align="frame0")["rmsf"]
+    np.testing.assert_allclose(r.results.rmsf, exp, atol=TOL)
+
+
+def test_rmsd_byproduct(c1):
+    from rmsf_amd import RMSF
+    d, traj = c1
+    r = RMSF(torch.tensor(traj, device="cuda"), select=d["sel"], align="frame0", collect_rmsd=True).run()
+    sel = d["sel"]
+    ref_com, ref_c = O.centred_reference(traj[0][sel])
+    exp = []
+    for f in range(len(traj)):
+        p = traj[f][sel]
+        A, E0 = O.inner_product(ref_c, p.astype(np.float64) - O.center_of_mass(p))
+        exp.append(O.fast_calc_rmsd_and_rotation(A, E0, float(len(sel)))[1])
+    np.testing.assert_allclose(r.results.rmsd, exp, atol=1e-7)
+
+
+def test_full_size_noalign_slices():
+    """C2 shape (100k atoms) at 2k frames: full-width result, CPU-verified on
+    sampled atoms regenerated bit-exactly from the counter-based generator."""
+    from rmsf_amd import RMSF
+    from rmsf_amd.engine import Engine
+    from rmsf_amd.synth import generate
+    eng = Engine()
+    n_atoms, nf = 100_000, 2000
+    traj = generate(eng, n_atoms, 0, nf, seed=0)
+    r = RMSF(traj).run()
+    atoms = np.random.default_rng(0).choice(n_atoms, 64, replace=False)
+    host = SY.frames(0, n_atoms, 0, nf, atoms=atoms)
+    np.testing.assert_allclose(r.results.rmsf[atoms], O.rmsf_two_pass(host), atol=1e-9)
+    # size-independent property: close to the analytic sqrt(3) sigma
+    np.testing.assert_allclose(r.results.rmsf, SY.expected_rmsf(0, np.arange(n_atoms)), rtol=0.12)
+    del traj
+
+
+def test_full_size_aligned_slices():
+    """C3 shape (100k atoms, QCP to frame 0) at 256 frames; the per-atom
+    result of sampled atoms is rebuilt on the CPU from the GPU's own frames."""
+    from rmsf_amd import RMSF
+    from rmsf_amd.engine import Engine
+    from rmsf_amd.synth import generate, motion_table
+    eng = Engine()
+    n_atoms, nf = 100_000, 256
+    mt = motion_table(1, nf)
+    traj = generate(eng, n_atoms, 0, nf, seed=0, motion=mt)
+    r = RMSF(traj, align="frame0").run()
+    host = traj.cpu().numpy()
+    exp = O.rmsf_script(host, None, align="frame0")["rmsf"]
+    np.testing.assert_allclose(r.results.rmsf, exp, atol=TOL)
