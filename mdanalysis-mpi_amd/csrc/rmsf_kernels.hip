@@ -60,8 +60,7 @@ constexpr int kBlock = 256;
 constexpr int kXform = RMSF_XFORM_DOUBLES;
 constexpr int kRefInfo = RMSF_REFINFO_DOUBLES;
 constexpr int kStats = 16;       // doubles per (frame, chunk) partial
-constexpr int kStatsAPT = 8;     // atoms per thread in k_frame_stats
-constexpr int kChunkAtoms = kBlock * kStatsAPT;
+constexpr int64_t kStatsBlocks = 16384;  // aim for >= this many (frame-group, chunk) blocks
 
 // ---------------------------------------------------------------------------
 // Welford coefficients a_k = k/(k+1), b_k = 1/(k+1) (RMSF.py:137-138), folded
@@ -232,65 +231,166 @@ __device__ __forceinline__ void wave_sum(double (&v)[N]) {
   }
 }
 
-// k_frame_stats: grid = (n_frames, n_chunks).  Sums, relative to a pivot p
-// (the frame's first selected atom, for conditioning), over the chunk's atoms:
+// k_frame_stats -- "lanes over frames".  grid = (ceil(n_frames/64), n_chunks).
+// Block (g, c): frames [64g, 64g+64) (lane = frame), atoms [c*chunk, ...).
+// Tiles of 64 frames x kTA atoms are staged HBM -> registers -> LDS (the next
+// tile's loads are in flight while the current one is consumed); wave w
+// consumes atoms [w*kTA/4, (w+1)*kTA/4) of every tile for its 64 frames.  The
+// atom index is wave-uniform, so the f64 reference (and masses) arrive by
+// scalar loads and no per-atom cross-lane reduction exists: each lane owns
+// its frame's sums.  Sums are relative to a per-frame pivot p (the frame's
+// first selected atom, for conditioning):
 //   [0..2]  sum x'            [3..5]  sum m x'   (only with masses)
 //   [6..14] sum x'_a r_b      [15]    sum |x'|^2
-template <bool GATHER, bool MASSES>
+// VEC4: contiguous selection, 16-B aligned frames -> float4 staging loads;
+// otherwise (gathered selection / odd strides) element-wise staging loads.
+constexpr int kTF = 64;                    // frames per block (one per lane)
+constexpr int kTA = 32;                    // atoms per tile
+constexpr int kPitch = 3 * kTA + 4;        // LDS row pitch (dwords): 16-B rows, conflict-free b128 column reads
+constexpr int kRow4 = 3 * kTA / 4;         // float4 per tile row
+constexpr int kNPre = kTF * kRow4 / kBlock;  // float4 per thread per tile (VEC4)
+constexpr int kNEl = kTF * kTA / kBlock;     // atoms per thread per tile (element path)
+constexpr int kAPW = kTA / 4;              // atoms per wave per tile
+static_assert(kTF * kRow4 % kBlock == 0 && kTF * kTA % kBlock == 0, "tile shape");
+static_assert((kBlock / 64 - 1) * kStats * 64 * 2 <= kTF * kPitch, "wave fold (doubles) fits in the tile buffer (floats)");
+
+template <bool GATHER, bool MASSES, bool VEC4>
 __global__ __launch_bounds__(kBlock) void k_frame_stats(
-    const float *__restrict__ xyz, int64_t fstride, int64_t n_sel, const int32_t *__restrict__ sel,
-    const double *__restrict__ masses, const double *__restrict__ ref, int n_chunks,
-    double *__restrict__ part) {
-  const int64_t f = blockIdx.x;
+    const float *__restrict__ xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
+    const int32_t *__restrict__ sel, const double *__restrict__ masses, const double *__restrict__ ref,
+    int64_t chunk, int n_chunks, double *__restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float tile[kTF * kPitch];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t f0 = (int64_t)blockIdx.x * kTF;
   const int ch = blockIdx.y;
-  const float *fr = xyz + f * fstride;
+  const int64_t a_beg = (int64_t)ch * chunk, a_end = min(n_sel, a_beg + chunk);
+  const int64_t f = f0 + lane;
+  const int64_t last = n_frames - 1;
+  const float *myfr = xyz + min(f, last) * fstride;
   const int64_t o0 = GATHER ? 3 * (int64_t)sel[0] : 0;
-  const double px = fr[o0], py = fr[o0 + 1], pz = fr[o0 + 2];
+  const double px = myfr[o0], py = myfr[o0 + 1], pz = myfr[o0 + 2];
 
   double acc[kStats];
 #pragma unroll
   for (int j = 0; j < kStats; ++j) acc[j] = 0.0;
-  const int64_t beg = (int64_t)ch * kChunkAtoms;
-  const int64_t end = min(n_sel, beg + kChunkAtoms);
-  for (int64_t a = beg + threadIdx.x; a < end; a += kBlock) {
-    const int64_t off = GATHER ? 3 * (int64_t)sel[a] : 3 * a;
-    const double x = (double)fr[off] - px;
-    const double y = (double)fr[off + 1] - py;
-    const double z = (double)fr[off + 2] - pz;
-    const double r0 = ref[3 * a], r1 = ref[3 * a + 1], r2 = ref[3 * a + 2];
-    acc[0] += x;
-    acc[1] += y;
-    acc[2] += z;
-    if (MASSES) {
-      const double m = masses[a];
-      acc[3] = fma(m, x, acc[3]);
-      acc[4] = fma(m, y, acc[4]);
-      acc[5] = fma(m, z, acc[5]);
-    }
-    acc[6] = fma(x, r0, acc[6]);
-    acc[7] = fma(x, r1, acc[7]);
-    acc[8] = fma(x, r2, acc[8]);
-    acc[9] = fma(y, r0, acc[9]);
-    acc[10] = fma(y, r1, acc[10]);
-    acc[11] = fma(y, r2, acc[11]);
-    acc[12] = fma(z, r0, acc[12]);
-    acc[13] = fma(z, r1, acc[13]);
-    acc[14] = fma(z, r2, acc[14]);
-    acc[15] = fma(x, x, fma(y, y, fma(z, z, acc[15])));
-  }
-  wave_sum(acc);
-  __shared__ double red[kBlock / 64][kStats];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (lane == 0) {
+
+  f32x4 pre[VEC4 ? kNPre : 1];
+  float pel[VEC4 ? 1 : 3 * kNEl];
+  const int64_t lim = 3 * n_sel;  // floats of the selection inside a frame row (VEC4)
+  auto gload = [&](int64_t t0) {
+    if (VEC4) {
 #pragma unroll
-    for (int j = 0; j < kStats; ++j) red[w][j] = acc[j];
+      for (int k = 0; k < kNPre; ++k) {
+        const int idx = threadIdx.x + k * kBlock;
+        const int row = idx / kRow4, col = idx % kRow4;
+        const float *src = xyz + min(f0 + row, last) * fstride;
+        const int64_t e = 3 * t0 + 4 * col;
+        if (e + 3 < lim) {
+          pre[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(src + e));
+        } else {  // selection tail: never read past the selection
+          pre[k] = f32x4{e < lim ? src[e] : 0.f, e + 1 < lim ? src[e + 1] : 0.f, e + 2 < lim ? src[e + 2] : 0.f, 0.f};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kNEl; ++k) {
+        const int idx = threadIdx.x + k * kBlock;
+        const int row = idx / kTA, j = idx % kTA;
+        const int64_t a = t0 + j;
+        const float *src = xyz + min(f0 + row, last) * fstride;
+        if (a < a_end) {
+          const int64_t off = GATHER ? 3 * (int64_t)sel[a] : 3 * a;
+          pel[3 * k] = __builtin_nontemporal_load(src + off);
+          pel[3 * k + 1] = __builtin_nontemporal_load(src + off + 1);
+          pel[3 * k + 2] = __builtin_nontemporal_load(src + off + 2);
+        } else {
+          pel[3 * k] = pel[3 * k + 1] = pel[3 * k + 2] = 0.f;
+        }
+      }
+    }
+  };
+  auto lstore = [&]() {
+    if (VEC4) {
+#pragma unroll
+      for (int k = 0; k < kNPre; ++k) {
+        const int idx = threadIdx.x + k * kBlock;
+        const int row = idx / kRow4, col = idx % kRow4;
+        *reinterpret_cast<f32x4 *>(tile + row * kPitch + 4 * col) = pre[k];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kNEl; ++k) {
+        const int idx = threadIdx.x + k * kBlock;
+        const int row = idx / kTA, j = idx % kTA;
+        float *d = tile + row * kPitch + 3 * j;
+        d[0] = pel[3 * k];
+        d[1] = pel[3 * k + 1];
+        d[2] = pel[3 * k + 2];
+      }
+    }
+  };
+
+  gload(a_beg);
+  for (int64_t t0 = a_beg; t0 < a_end; t0 += kTA) {
+    __syncthreads();
+    lstore();
+    __syncthreads();
+    if (t0 + kTA < a_end) gload(t0 + kTA);
+    const f32x4 *my = reinterpret_cast<const f32x4 *>(tile + lane * kPitch + w * 3 * kAPW);
+    const int64_t ab = t0 + w * kAPW;  // first atom of this wave's slab (uniform)
+#pragma unroll 1
+    for (int g = 0; g < kAPW / 4; ++g) {
+      const int64_t a4 = ab + 4 * g;
+      if (a4 >= a_end) break;  // uniform
+      const f32x4 q0 = my[3 * g], q1 = my[3 * g + 1], q2 = my[3 * g + 2];
+      const float c[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+      const double *rr = ref + 3 * a4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (a4 + i >= a_end) break;  // uniform
+        const double r0 = rr[3 * i], r1 = rr[3 * i + 1], r2 = rr[3 * i + 2];
+        const double x = (double)c[3 * i] - px, y = (double)c[3 * i + 1] - py, z = (double)c[3 * i + 2] - pz;
+        acc[0] += x;
+        acc[1] += y;
+        acc[2] += z;
+        if (MASSES) {
+          const double m = masses[a4 + i];
+          acc[3] = fma(m, x, acc[3]);
+          acc[4] = fma(m, y, acc[4]);
+          acc[5] = fma(m, z, acc[5]);
+        }
+        acc[6] = fma(x, r0, acc[6]);
+        acc[7] = fma(x, r1, acc[7]);
+        acc[8] = fma(x, r2, acc[8]);
+        acc[9] = fma(y, r0, acc[9]);
+        acc[10] = fma(y, r1, acc[10]);
+        acc[11] = fma(y, r2, acc[11]);
+        acc[12] = fma(z, r0, acc[12]);
+        acc[13] = fma(z, r1, acc[13]);
+        acc[14] = fma(z, r2, acc[14]);
+        acc[15] = fma(x, x, fma(y, y, fma(z, z, acc[15])));
+      }
+    }
+  }
+  // fold waves 1..3 into wave 0 through the (now free) tile buffer, in a
+  // fixed order (deterministic), then each lane of wave 0 writes its frame.
+  __syncthreads();
+  double *red = reinterpret_cast<double *>(tile);
+  if (w > 0) {
+#pragma unroll
+    for (int j = 0; j < kStats; ++j) red[((w - 1) * kStats + j) * 64 + lane] = acc[j];
   }
   __syncthreads();
-  if (threadIdx.x < kStats) {
-    double t = 0.0;
+  if (w == 0 && f < n_frames) {
+    double *o = part + (f * n_chunks + ch) * kStats;
 #pragma unroll
-    for (int i = 0; i < kBlock / 64; ++i) t += red[i][threadIdx.x];
-    part[((int64_t)f * n_chunks + ch) * kStats + threadIdx.x] = t;
+    for (int j = 0; j < kStats; ++j) {
+      double t = acc[j];
+#pragma unroll
+      for (int v = 0; v < kBlock / 64 - 1; ++v) t += red[(v * kStats + j) * 64 + lane];
+      o[j] = t;
+    }
   }
 }
 
@@ -706,7 +806,17 @@ __global__ __launch_bounds__(kBlock) void k_synth(float *__restrict__ out, int64
 
 inline unsigned grid1(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
-int64_t n_chunks_for(int64_t n_sel) { return (n_sel + kChunkAtoms - 1) / kChunkAtoms; }
+// Atom chunk per block of k_frame_stats: as long as possible (fewer partials)
+// while the grid still has >= kStatsBlocks blocks; a multiple of the tile.
+void stats_chunks(int64_t n_sel, int64_t n_frames, int64_t *chunk, int64_t *n_chunks) {
+  const int64_t groups = std::max<int64_t>(1, (n_frames + kTF - 1) / kTF);
+  int64_t nc = (kStatsBlocks + groups - 1) / groups;
+  nc = std::max<int64_t>(1, std::min<int64_t>(nc, std::min<int64_t>((n_sel + kTA - 1) / kTA, 65535)));
+  int64_t c = (n_sel + nc - 1) / nc;
+  c = (c + kTA - 1) / kTA * kTA;
+  *chunk = c;
+  *n_chunks = (n_sel + c - 1) / c;
+}
 
 }  // namespace
 
@@ -800,7 +910,9 @@ RMSF_EXPORT int rmsf_reference_setup(const float *d_frame, const double *d_avg, 
 
 RMSF_EXPORT size_t rmsf_superpose_workspace_bytes(int64_t n_sel, int64_t n_frames) {
   if (n_sel < 1 || n_frames < 0) return 0;
-  return (size_t)n_frames * (size_t)n_chunks_for(n_sel) * kStats * sizeof(double);
+  int64_t chunk, nch;
+  stats_chunks(n_sel, n_frames, &chunk, &nch);
+  return (size_t)n_frames * (size_t)nch * kStats * sizeof(double);
 }
 
 RMSF_EXPORT int rmsf_superpose(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
@@ -811,27 +923,24 @@ RMSF_EXPORT int rmsf_superpose(const float *d_xyz, int64_t fstride, int64_t n_fr
   if (!d_xyz || !d_ref || !d_refinfo || !d_xform || !d_work || n_sel < 1 || n_frames < 0 ||
       fstride < (d_sel ? 3 : 3 * n_sel))
     return fail(RMSF_EINVAL, "rmsf_superpose: bad arguments");
-  const int64_t nch = n_chunks_for(n_sel);
-  if (nch > 65535) return fail(RMSF_EINVAL, "rmsf_superpose: selection too large");
+  int64_t chunk, nch;
+  stats_chunks(n_sel, n_frames, &chunk, &nch);
   if (work_bytes < rmsf_superpose_workspace_bytes(n_sel, n_frames))
     return fail(RMSF_ENOMEM, "rmsf_superpose: workspace too small");
   hipStream_t s = S(stream);
   double *part = static_cast<double *>(d_work);
   const bool g = d_sel != nullptr, m = d_masses != nullptr;
-  // frames go to grid.x (up to 2^31-1), chunks to grid.y.
-  for (int64_t f0 = 0; f0 < n_frames; f0 += 0x7fffffff) {
-    const int64_t nf = std::min<int64_t>(n_frames - f0, 0x7fffffff);
-    dim3 grid((unsigned)nf, (unsigned)nch);
-    const float *x = d_xyz + f0 * fstride;
-    double *pp = part + f0 * nch * kStats;
-#define ST_LAUNCH(G, M) \
-  hipLaunchKernelGGL((k_frame_stats<G, M>), grid, dim3(kBlock), 0, s, x, fstride, n_sel, d_sel, d_masses, d_ref, (int)nch, pp)
-    if (g && m) ST_LAUNCH(true, true);
-    else if (g) ST_LAUNCH(true, false);
-    else if (m) ST_LAUNCH(false, true);
-    else ST_LAUNCH(false, false);
+  const bool vec4 = !g && fstride % 4 == 0 && reinterpret_cast<uintptr_t>(d_xyz) % 16 == 0;
+  dim3 grid((unsigned)((n_frames + kTF - 1) / kTF), (unsigned)nch);
+#define ST_LAUNCH(G, M, V) \
+  hipLaunchKernelGGL((k_frame_stats<G, M, V>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, chunk, (int)nch, part)
+  if (g && m) ST_LAUNCH(true, true, false);
+  else if (g) ST_LAUNCH(true, false, false);
+  else if (m && vec4) ST_LAUNCH(false, true, true);
+  else if (m) ST_LAUNCH(false, true, false);
+  else if (vec4) ST_LAUNCH(false, false, true);
+  else ST_LAUNCH(false, false, false);
 #undef ST_LAUNCH
-  }
   int rc = after_launch("k_frame_stats");
   if (rc) return rc;
   const unsigned gq = (unsigned)((n_frames + 3) / 4);
