@@ -60,7 +60,7 @@ def parse():
     ap.add_argument("--splits", type=int, default=None)
     ap.add_argument("--batch-frames", type=int, default=None, help="aligned modes: frames per superpose batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=64, help="frames per CPU process in the baseline sample")
+    ap.add_argument("--cpu-frames", type=int, default=640, help="frames per CPU process in the baseline sample")
     ap.add_argument("--no-modes", action="store_true", help="skip the aligned-mode measurements at N=1")
     ap.add_argument("--mode-steps", type=int, default=3)
     return ap.parse_args()
@@ -169,10 +169,12 @@ def main():
                    "parallelism": f"frame-sharded x{world} (RMSF.py:65-69 blocks), RCCL Chan merge"},
         "roofline": {"bound": "hbm", "kernel": "k_accum_atoms" if wl["align"] else "k_welford_flat",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic, "algorithmic_bytes_per_launch": bytes_launch,
+                     "traffic": traffic, "traffic_source": f"profiles/pmc_{a.workload}.json" if traffic else None,
+                     "algorithmic_bytes_per_launch": bytes_launch,
                      "avg_launch_ms": kern_s * 1e3, "launches": len(acc_ms)},
         "cpu_baseline": cpu,
-        "pipeline_hbm_gbs": B_PER_ATOM_FRAME * n_atoms * n_local * a.steps / dt / 1e9 * (1 if not wl["align"] else 1),
+        # whole-step rate in algorithmic bytes (incl. merges, finalise, launch gaps)
+        "pipeline_hbm_gbs": B_PER_ATOM_FRAME * n_atoms * n_local * a.steps / dt / 1e9,
     }
     if wl["align"]:
         sup_ms = timer.ms("superpose")
