@@ -138,23 +138,37 @@ class PipelineResult:
 
 
 def reference_from_frame(eng: Engine, source, frame: int, n_sel: int, masses, owner: int | None = None):
-    """RMSF.py:80-87: centred f64 reference of frame ``frame``.  In a sharded
-    run the rank holding the frame computes it and broadcasts (RMSF.py has
-    every rank re-read frame 0 from disk; the device equivalent is one
-    broadcast of 3*n_sel + 16 doubles)."""
+    """RMSF.py:80-87: centred f64 reference of trajectory frame ``frame``.
+
+    RMSF.py has every rank re-read that frame from disk.  Here, if every rank
+    holds it (host / full-trajectory sources) each computes it locally;
+    otherwise (sharded HBM-resident trajectories) the lowest rank holding it
+    computes it and broadcasts 3*n_sel + 16 doubles."""
     rank, size = parallel.world()
-    if size > 1 and owner is not None:
-        ref = eng.empty(n_sel, 3)
-        info = eng.empty(16)
-        if rank == owner:
-            b = source.reference(frame, eng.stream)
-            r, i = eng.reference_setup(n_sel, frame_ptr=b.ptr, sel=b.sel, masses=masses)
-            b.done()
-            ref.copy_(r)
-            info.copy_(i)
-        parallel.broadcast_(ref, owner)
-        parallel.broadcast_(info, owner)
-        return ref, info
+    if size > 1:
+        if owner is None:
+            have = bool(source.holds(frame))
+            t = torch.tensor([rank if have else size, 0 if have else 1], dtype=torch.int64, device=eng.device)
+            lo = t[:1].clone()
+            missing = t[1:].clone()
+            torch.distributed.all_reduce(lo, op=torch.distributed.ReduceOp.MIN)
+            torch.distributed.all_reduce(missing, op=torch.distributed.ReduceOp.SUM)
+            lo, missing = int(lo.item()), int(missing.item())
+            if lo >= size:
+                raise IndexError(f"reference frame {frame} is not held by any rank")
+            owner = None if missing == 0 else lo
+        if owner is not None:
+            ref = eng.empty(n_sel, 3)
+            info = eng.empty(16)
+            if rank == owner:
+                b = source.reference(frame, eng.stream)
+                r, i = eng.reference_setup(n_sel, frame_ptr=b.ptr, sel=b.sel, masses=masses)
+                b.done()
+                ref.copy_(r)
+                info.copy_(i)
+            parallel.broadcast_(ref, owner)
+            parallel.broadcast_(info, owner)
+            return ref, info
     b = source.reference(frame, eng.stream)
     r, i = eng.reference_setup(n_sel, frame_ptr=b.ptr, sel=b.sel, masses=masses)
     b.done()

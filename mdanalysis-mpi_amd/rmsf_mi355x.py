@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Script mode: ``RMSF.py`` on MI355X.
+
+    # RMSF.py's own run (mpirun -n P python RMSF.py) -> one process per GPU
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \\
+        --master-addr 127.0.0.1 --master-port 29500 rmsf_mi355x.py \\
+        --topology adk.gro --trajectory adk.xtc
+
+    # without MDAnalysis: a synthetic trajectory generated in HBM
+    python rmsf_mi355x.py --synthetic 100000 2000 --align frame0
+
+Defaults mirror RMSF.py: selection "protein and name CA" (RMSF.py:77),
+ref_frame 0 (RMSF.py:63), the two-sweep average alignment (RMSF.py:89-140),
+frame blocks per rank (RMSF.py:65-69) with the per-rank range printed as at
+RMSF.py:74, and the RMSF computed on rank 0 (RMSF.py:145-146) -- which this
+script also writes out (``--out``), where RMSF.py only says "#Do something
+with RMSF" (RMSF.py:147).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import numpy as np
+
+
+def main(argv=None) -> int:
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--topology")
+    ap.add_argument("--trajectory")
+    ap.add_argument("--select", default="protein and name CA")
+    ap.add_argument("--synthetic", nargs=2, type=int, metavar=("N_ATOMS", "N_FRAMES"))
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--align", choices=["average", "frame0", "none"], default="average")
+    ap.add_argument("--ref-frame", type=int, default=0)
+    ap.add_argument("--out", default=None, help="write rank 0's RMSF (.npy)")
+    a = ap.parse_args(argv)
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from rmsf_amd import RMSF, parallel
+    from rmsf_amd.engine import Engine
+    from rmsf_amd.pipeline import run_pipeline
+    from rmsf_amd.sources import DeviceSource, FrameList
+    from rmsf_amd.synth import generate, motion_table
+
+    align = None if a.align == "none" else a.align
+    rank, size = parallel.world()
+    if a.synthetic:
+        n_atoms, n_frames = a.synthetic
+        eng = Engine()
+        b0, b1 = parallel.blocks(n_frames, size)[rank]
+        print("Process:%3d --> Frames: %10d -- %10d" % (rank, b0, b1), flush=True)
+        motion = motion_table(a.seed + 1, n_frames) if align else None
+        shard = generate(eng, n_atoms, b0, max(b1 - b0, 1), seed=a.seed, motion=motion)[: b1 - b0]
+        res = run_pipeline(eng, DeviceSource(shard, offset=b0, n_traj=n_frames), FrameList(n_frames),
+                           align=align, ref_frame=a.ref_frame)
+        rmsf = res.rmsf.cpu().numpy()
+    else:
+        if not (a.topology and a.trajectory):
+            ap.error("--topology/--trajectory (MDAnalysis) or --synthetic is required")
+        import MDAnalysis as mda  # not installed in the build container
+
+        u = mda.Universe(a.topology, a.trajectory)
+        ag = u.select_atoms(a.select)
+        rmsf = RMSF(ag, align=align, ref_frame=a.ref_frame, verbose=True).run().results.rmsf
+    if rank == 0:
+        print(f"RMSF over {len(rmsf)} atoms: mean {rmsf.mean():.6f} A, max {rmsf.max():.6f} A", flush=True)
+        if a.out:
+            np.save(a.out, rmsf)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
