@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=640, help="frames per CPU process in the baseline sample")
     ap.add_argument("--no-modes", action="store_true", help="skip the aligned-mode measurements at N=1")
     ap.add_argument("--mode-steps", type=int, default=3)
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo only "
+                                                     "to rehearse several ranks on one GPU)")
     return ap.parse_args()
 
 
@@ -103,9 +105,14 @@ def main():
     import torch
     import torch.distributed as dist
 
+    if a.backend == "gloo":  # rehearsal: all ranks share the visible device(s)
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(a.backend)
     from rmsf_amd import parallel
     from rmsf_amd.engine import Engine
     from rmsf_amd.pipeline import KernelTimer, run_pipeline

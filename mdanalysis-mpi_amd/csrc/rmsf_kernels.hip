@@ -60,6 +60,8 @@ constexpr int kBlock = 256;
 constexpr int kXform = RMSF_XFORM_DOUBLES;
 constexpr int kRefInfo = RMSF_REFINFO_DOUBLES;
 constexpr int kStats = 16;       // doubles per (frame, chunk) partial
+constexpr int64_t kAccumBlocks = 3584;       // target workgroups, k_welford_flat
+constexpr int64_t kAccumBlocksAtom = 16384;  // target workgroups, k_accum_atoms
 constexpr int64_t kStatsBlocks = 16384;  // aim for >= this many (frame-group, chunk) blocks
 
 // ---------------------------------------------------------------------------
@@ -960,16 +962,19 @@ RMSF_EXPORT int64_t rmsf_split_count(int64_t n_frames, int n_splits, int s) {
 }
 
 RMSF_EXPORT int rmsf_accumulate_splits(int64_t n_sel, int64_t n_frames, int aligned) {
-  (void)aligned;
   if (n_frames <= 0) return 1;
-  // Enough (lane-groups x splits) to fill 256 CUs several times over, with
-  // splits of <= kCoefN frames; the partial I/O (16 B per coordinate per
-  // split) stays ~1-2% of the frame stream.
-  const int64_t lanes = (3 * n_sel + 3) / 4;
+  // Frame tiles ("splits") per launch.  Measured on MI355X (tools/
+  // ubench_welford.hip, 100k atoms x 20k frames): for k_welford_flat long
+  // tiles win -- 12 splits (3.5k workgroups, ~1.75 waves of the 2048 resident
+  // slots) stream at 6.45 TB/s, 56 splits (16k workgroups) at 6.1 TB/s; the
+  // aligned k_accum_atoms measured 4.15 ms at 10 splits vs ~4.0 ms at 42, so
+  // it keeps a 16k-workgroup target.  Splits never exceed kCoefN frames.
+  const int64_t lanes = aligned ? n_sel : (3 * n_sel + 3) / 4;
   const int64_t blocks_x = std::max<int64_t>(1, (lanes + kBlock - 1) / kBlock);
-  int64_t want = (16384 + blocks_x - 1) / blocks_x;  // ~16k workgroups in flight overall
-  want = std::max<int64_t>(want, (n_frames + kCoefN - 1) / kCoefN);
-  want = std::min<int64_t>(want, std::max<int64_t>(1, n_frames / 32));
+  // the one-atom-per-lane kernel (aligned / gathered) prefers the larger grid
+  const int64_t target = aligned ? kAccumBlocksAtom : kAccumBlocks;
+  int64_t want = (target + blocks_x - 1) / blocks_x;
+  want = std::min<int64_t>(want, std::max<int64_t>(1, n_frames / 32));  // tiles of >= 32 frames
   want = std::max<int64_t>(want, (n_frames + kCoefN - 1) / kCoefN);
   want = std::min<int64_t>(want, 65535);
   return (int)std::max<int64_t>(1, want);
