@@ -46,6 +46,9 @@ WORKLOADS = {
                     name="RMSF.py two-sweep: 100k atoms x 20k frames per GPU, align to frame 0, average, re-align"),
     "c4": dict(n_atoms=1_000_000, frames_per_gpu=2_500, align=None,
                name="C4 share: synthetic 1M atoms x 2.5k frames fp32 per GPU (N=8: 1M x 20k, 240 GB)"),
+    "c5": dict(n_atoms=250_000, frames_per_gpu=1_000, align=None, host=True,
+               name="C5: 250k atoms x 1k frames fp32 in host memory, streamed via the pinned multi-buffer "
+                    "stager (PCIe-inclusive rate; frames pre-decoded, no XTC decode)"),
 }
 
 
@@ -63,6 +66,9 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=640, help="frames per CPU process in the baseline sample")
     ap.add_argument("--no-modes", action="store_true", help="skip the aligned-mode measurements at N=1")
     ap.add_argument("--mode-steps", type=int, default=3)
+    ap.add_argument("--stager-threads", type=int, default=4)
+    ap.add_argument("--stager-batch", type=int, default=None, help="c5: frames per staged batch")
+    ap.add_argument("--align", choices=["none", "frame0", "average"], default=None, help="override the workload's")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo only "
                                                      "to rehearse several ranks on one GPU)")
     return ap.parse_args()
@@ -94,13 +100,19 @@ def main():
         wl["n_atoms"] = a.n_atoms
     if a.frames_per_gpu:
         wl["frames_per_gpu"] = a.frames_per_gpu
+    if a.align is not None:
+        wl["align"] = None if a.align == "none" else a.align
     n_atoms, per_gpu = wl["n_atoms"], wl["frames_per_gpu"]
 
     # -- CPU baseline first: no process has touched the GPU yet ---------------
-    cpu = None
+    cpu = cpu_c3 = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import cpu_baseline
         cpu = cpu_baseline.run(n_atoms, a.cpu_frames, align="none")
+        if not a.no_modes and wl["align"] is None and not wl.get("host"):
+            from rmsf_amd.synth import motion_table as _mt  # numpy only: no GPU touched
+            cpu_c3 = cpu_baseline.run(n_atoms, max(1, a.cpu_frames // 4), align="frame0",
+                                      motion=_mt(1, per_gpu))
 
     import torch
     import torch.distributed as dist
@@ -126,7 +138,18 @@ def main():
     motion = motion_table(1, n_total) if wl["align"] else None
     traj = generate(eng, n_atoms, b0, n_local, seed=0, motion=motion)
     torch.cuda.synchronize()
-    src = DeviceSource(traj, offset=b0, n_traj=n_total)
+    if wl.get("host"):
+        # C5: the frames live in (pageable) host memory and every step streams
+        # them through the stager: host gather -> pinned slot -> H2D -> kernels
+        from rmsf_amd.sources import HostSource
+
+        host = traj.cpu().numpy()
+        del traj
+        torch.cuda.empty_cache()
+        src = HostSource(host, None, batch_frames=a.stager_batch, n_threads=a.stager_threads, offset=b0,
+                         n_traj=n_total)
+    else:
+        src = DeviceSource(traj, offset=b0, n_traj=n_total)
     fl = FrameList(n_total)
 
     def run(align, timer=None):
@@ -193,7 +216,12 @@ def main():
                                 "hbm_gbs": B_PER_ATOM_FRAME * n_atoms * n_local / s / 1e9}
 
     # -- aligned modes at N=1 (reported beside the headline) ------------------
-    if world == 1 and not a.no_modes and wl["align"] is None:
+    if wl.get("host"):
+        out["stager"] = {"h2d_gbs": B_PER_ATOM_FRAME * n_atoms * n_local * a.steps / dt / 1e9,
+                         "threads": a.stager_threads, "batch_frames": src.batch_frames,
+                         "host_link_spec_gbs": 63.0}
+        out["roofline"]["note"] = "C5 is PCIe/host bound; the kernel roofline above is the device-side launch"
+    if world == 1 and not a.no_modes and wl["align"] is None and not wl.get("host"):
         del traj, src
         torch.cuda.empty_cache()
         motion = motion_table(1, n_total)
@@ -217,6 +245,8 @@ def main():
                 "accumulate_avg_ms": sum(acc) / len(acc),
                 "accumulate_hbm_gbs": B_PER_ATOM_FRAME * n_atoms * n_local / (sum(acc) / len(acc) / 1e3) / 1e9,
             }
+        if cpu_c3 is not None:
+            modes["c3_frame0"]["cpu_baseline"] = cpu_c3
         out["modes"] = modes
     if rank == 0:
         print(json.dumps(out), flush=True)

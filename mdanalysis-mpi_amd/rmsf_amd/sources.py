@@ -146,15 +146,19 @@ class DeviceSource:
 
 
 class HostSource:
-    """Host float32 array [F, n_atoms, 3] streamed through the pinned stager."""
+    """Host float32 array [F, n_atoms, 3] streamed through the pinned stager.
+    Row r holds global frame ``offset + r`` of a trajectory of ``n_traj``
+    frames (a rank's shard; default: the whole trajectory)."""
 
     def __init__(self, traj: np.ndarray, sel=None, batch_frames: int | None = None, n_slots: int = 3,
-                 n_threads: int = 4):
+                 n_threads: int = 4, offset: int = 0, n_traj: int | None = None):
         traj = np.ascontiguousarray(traj, dtype=np.float32)
         if traj.ndim != 3 or traj.shape[2] != 3:
             raise ValueError("trajectory must be [n_frames, n_atoms, 3]")
         self.traj = traj
-        self.n_traj, self.n_atoms = traj.shape[0], traj.shape[1]
+        self.n_atoms = traj.shape[1]
+        self.offset = offset
+        self.n_traj = traj.shape[0] + offset if n_traj is None else n_traj
         sel_arr = None if sel is None else np.ascontiguousarray(sel, dtype=np.int64)
         if sel_arr is not None and sel_arr.size and (sel_arr.min() < 0 or sel_arr.max() >= self.n_atoms):
             raise IndexError("selection index out of range")
@@ -165,17 +169,22 @@ class HostSource:
         self.stager = Stager(self.n_atoms, self.n_sel, sel_arr, batch_frames, n_slots, n_threads)
 
     def holds(self, frame: int) -> bool:
-        return 0 <= frame < self.n_traj
+        return self.offset <= frame < self.offset + self.traj.shape[0]
+
+    def _row(self, frame: int) -> int:
+        if not self.holds(frame):
+            raise IndexError(f"frame {frame} is not in this host shard")
+        return frame - self.offset
 
     def reference(self, frame: int, stream: int) -> Batch:
-        slot, ptr = self.stager.stage(self.traj, frame, 1, 1, stream)
+        slot, ptr = self.stager.stage(self.traj, self._row(frame), 1, 1, stream)
         return Batch(ptr, 3 * self.n_sel, 1, None, lambda: self.stager.release(slot, stream))
 
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
         bf = min(max_frames, self.batch_frames)
         for i in range(b0, b1, bf):
             n = min(bf, b1 - i)
-            slot, ptr = self.stager.stage(self.traj, frames.r[i], frames.step, n, stream)
+            slot, ptr = self.stager.stage(self.traj, self._row(frames.r[i]), frames.step, n, stream)
             yield Batch(ptr, 3 * self.n_sel, n, None, lambda s=slot: self.stager.release(s, stream))
 
 
