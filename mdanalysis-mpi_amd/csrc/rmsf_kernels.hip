@@ -61,7 +61,7 @@ constexpr int kXform = RMSF_XFORM_DOUBLES;
 constexpr int kRefInfo = RMSF_REFINFO_DOUBLES;
 constexpr int kStats = 16;       // doubles per (frame, chunk) partial
 constexpr int64_t kAccumBlocks = 3584;       // target workgroups, k_welford_flat
-constexpr int64_t kAccumBlocksAtom = 16384;  // target workgroups, k_accum_atoms
+constexpr int64_t kAccumBlocksAtom = 4608;   // target workgroups, k_accum_atoms
 constexpr int64_t kStatsBlocks = 16384;  // aim for >= this many (frame-group, chunk) blocks
 
 // ---------------------------------------------------------------------------
@@ -967,11 +967,10 @@ RMSF_EXPORT int rmsf_accumulate_splits(int64_t n_sel, int64_t n_frames, int alig
   // ubench_welford.hip, 100k atoms x 20k frames): for k_welford_flat long
   // tiles win -- 12 splits (3.5k workgroups, ~1.75 waves of the 2048 resident
   // slots) stream at 6.45 TB/s, 56 splits (16k workgroups) at 6.1 TB/s; the
-  // aligned k_accum_atoms measured 4.15 ms at 10 splits vs ~4.0 ms at 42, so
-  // it keeps a 16k-workgroup target.  Splits never exceed kCoefN frames.
+  // aligned k_accum_atoms (tools/ubench_accum.hip, same-process A/B) runs
+  // 3.96 ms at 12 splits vs 4.08 ms at 42.  Splits never exceed kCoefN frames.
   const int64_t lanes = aligned ? n_sel : (3 * n_sel + 3) / 4;
   const int64_t blocks_x = std::max<int64_t>(1, (lanes + kBlock - 1) / kBlock);
-  // the one-atom-per-lane kernel (aligned / gathered) prefers the larger grid
   const int64_t target = aligned ? kAccumBlocksAtom : kAccumBlocks;
   int64_t want = (target + blocks_x - 1) / blocks_x;
   want = std::min<int64_t>(want, std::max<int64_t>(1, n_frames / 32));  // tiles of >= 32 frames
