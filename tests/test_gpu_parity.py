@@ -137,3 +137,15 @@ def test_full_size_aligned_slices():
     host = traj.cpu().numpy()
     exp = O.rmsf_script(host, None, align="frame0")["rmsf"]
     np.testing.assert_allclose(r.results.rmsf, exp, atol=TOL)
+
+
+def test_bitwise_reproducible(c1):
+    """Fixed-order reductions, no atomics: two runs agree bit for bit."""
+    from rmsf_amd import RMSF
+    d, traj = c1
+    x = torch.tensor(traj, device="cuda")
+    a = RMSF(x, select=d["sel"], align="average").run().results
+    b = RMSF(x, select=d["sel"], align="average").run().results
+    np.testing.assert_array_equal(a.rmsf, b.rmsf)
+    np.testing.assert_array_equal(a.sumsquares, b.sumsquares)
+    np.testing.assert_array_equal(a.average, b.average)
