@@ -47,8 +47,11 @@ WORKLOADS = {
     "c4": dict(n_atoms=1_000_000, frames_per_gpu=2_500, align=None,
                name="C4 share: synthetic 1M atoms x 2.5k frames fp32 per GPU (N=8: 1M x 20k, 240 GB)"),
     "c5": dict(n_atoms=250_000, frames_per_gpu=1_000, align=None, host=True,
-               name="C5: 250k atoms x 1k frames fp32 in host memory, streamed via the pinned multi-buffer "
-                    "stager (PCIe-inclusive rate; frames pre-decoded, no XTC decode)"),
+               name="C5 (pre-decoded): 250k atoms x 1k frames fp32 in host memory, streamed via the pinned "
+                    "multi-buffer stager (PCIe-inclusive rate; no XTC decode)"),
+    "c5xtc": dict(n_atoms=250_000, frames_per_gpu=400, align=None, host=True, xtc=True,
+                  name="C5: 250k-atom XTC file (precision 1000) decoded frame-parallel on host threads into "
+                       "the pinned stager and streamed to the GPU (decode + PCIe inclusive)"),
 }
 
 
@@ -146,8 +149,25 @@ def main():
         host = traj.cpu().numpy()
         del traj
         torch.cuda.empty_cache()
-        src = HostSource(host, None, batch_frames=a.stager_batch, n_threads=a.stager_threads, offset=b0,
-                         n_traj=n_total)
+        if wl.get("xtc"):
+            import tempfile
+
+            from rmsf_amd.sources import XtcSource
+            from rmsf_amd.xtc import write_xtc
+
+            if world > 1:
+                raise SystemExit("c5xtc is a single-GPU I/O workload")
+            xtc_dir = tempfile.mkdtemp(prefix="rmsf_c5_")
+            xtc_path = os.path.join(xtc_dir, "c5.xtc")
+            t_w = time.perf_counter()
+            for f in range(0, n_local, 50):  # untimed: produce the input file
+                write_xtc(xtc_path, host[f:f + 50], append=f > 0)
+            t_w = time.perf_counter() - t_w
+            del host
+            src = XtcSource(xtc_path, None, batch_frames=a.stager_batch, n_threads=a.stager_threads)
+        else:
+            src = HostSource(host, None, batch_frames=a.stager_batch, n_threads=a.stager_threads, offset=b0,
+                             n_traj=n_total)
     else:
         src = DeviceSource(traj, offset=b0, n_traj=n_total)
     fl = FrameList(n_total)
@@ -220,6 +240,10 @@ def main():
         out["stager"] = {"h2d_gbs": B_PER_ATOM_FRAME * n_atoms * n_local * a.steps / dt / 1e9,
                          "threads": a.stager_threads, "batch_frames": src.batch_frames,
                          "host_link_spec_gbs": 63.0}
+        if wl.get("xtc"):
+            out["stager"].update(xtc_bytes=os.path.getsize(xtc_path), xtc_write_s=t_w,
+                                 xtc_frames_per_s=n_local * a.steps / dt,
+                                 xtc_gb_per_s_compressed=os.path.getsize(xtc_path) * a.steps / dt / 1e9)
         out["roofline"]["note"] = "C5 is PCIe/host bound; the kernel roofline above is the device-side launch"
     if world == 1 and not a.no_modes and wl["align"] is None and not wl.get("host"):
         del traj, src

@@ -199,10 +199,37 @@ int rmsf_stager_stage(rmsf_stager *st, const float *h_frames,
 int rmsf_stager_stage_ptrs(rmsf_stager *st, const float *const *h_frame_ptrs,
                            int64_t n_frames, void *consumer_stream, int *slot,
                            float **d_batch);
+/* Decode XTC frames f0, f0+step, ... (n_frames of them) frame-parallel
+ * straight into the next pinned slot (selection applied), then DMA it. */
+typedef struct rmsf_xtc rmsf_xtc;
+int rmsf_stager_stage_xtc(rmsf_stager *st, const rmsf_xtc *x, int64_t f0,
+                          int64_t n_frames, int64_t step,
+                          void *consumer_stream, int *slot, float **d_batch);
 /* Mark the slot free once the work queued so far on consumer_stream ends. */
 int rmsf_stager_release(rmsf_stager *st, int slot, void *consumer_stream);
 /* Wait until every copy issued by the stager has completed. */
 int rmsf_stager_synchronize(rmsf_stager *st);
+
+/* ---- GROMACS XTC trajectories ---------------------------
+ * Host reader/writer replacing libxdrfile behind MDAnalysis' XTCReader, the
+ * frame source of RMSF.py:56,92,124 (GRO/XTC input, RMSF.py:34).  Published
+ * xdrfile format (magic 1995, xdr3dfcoord compression).  Positions are in
+ * Angstrom, rounded as MDAnalysis does: f32(f32(int * f32(1/prec)) * 10).
+ * Host-only code: no HIP calls.                                             */
+int rmsf_xtc_open(const char *path, rmsf_xtc **out, int64_t *n_atoms,
+                  int64_t *n_frames);
+int rmsf_xtc_close(rmsf_xtc *x);
+int rmsf_xtc_frame_info(const rmsf_xtc *x, int64_t frame, int32_t *step,
+                        float *time, float *box9);
+/* Decode frames f0, f0+step, ... (n) into h_out[n][rows][3] (rows = n_sel
+ * when h_sel != NULL, else n_atoms), frame-parallel on n_threads threads. */
+int rmsf_xtc_read(const rmsf_xtc *x, int64_t f0, int64_t n, int64_t step,
+                  const int32_t *h_sel, int64_t n_sel, float *h_out,
+                  int n_threads);
+/* Write (append != 0: append) n_frames frames given in Angstrom. */
+int rmsf_xtc_write(const char *path, const float *h_xyz, int64_t n_frames,
+                   int64_t n_atoms, float precision, const float *h_box9,
+                   int append);
 
 #ifdef __cplusplus
 }

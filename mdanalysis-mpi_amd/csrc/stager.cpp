@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstring>
 #include <functional>
@@ -26,6 +27,10 @@
 
 // error reporting shared with rmsf_kernels.hip through this small hook
 extern "C" int rmsf_internal_set_error(int code, const char *msg);
+extern "C" int rmsf_internal_xtc_decode(const rmsf_xtc *x, int64_t f0, int64_t n, int64_t step, const int32_t *sel,
+                                        int64_t n_sel, float *out, int64_t out_stride, int n_threads);
+extern "C" int64_t rmsf_internal_xtc_natoms(const rmsf_xtc *x);
+extern "C" int64_t rmsf_internal_xtc_nframes(const rmsf_xtc *x);
 
 namespace {
 
@@ -120,6 +125,7 @@ struct rmsf_stager {
   std::vector<char> copy_pending, release_pending;
   hipStream_t copy_stream = nullptr;
   Pool *pool = nullptr;
+  int n_threads = 1;
 };
 
 namespace {
@@ -140,9 +146,10 @@ void destroy(rmsf_stager *st) {
   delete st;
 }
 
-// Gather frame rows into the pinned slot; `frame(i)` yields host frame i.
-int fill_and_copy(rmsf_stager *st, int64_t n_frames, const std::function<const float *(int64_t)> &frame,
-                  void *consumer_stream, int *slot, float **d_batch) {
+// Take the next slot, let `fill(dst)` write n_frames compact frames into its
+// pinned buffer, then queue the DMA and make the consumer wait for it.
+int fill_and_copy(rmsf_stager *st, int64_t n_frames, const std::function<int(float *)> &fill, void *consumer_stream,
+                  int *slot, float **d_batch) {
   if (n_frames < 1 || n_frames > st->batch)
     return fail(RMSF_EINVAL, "rmsf_stager_stage: n_frames must be in [1, batch_frames]");
   const int s = st->next;
@@ -152,14 +159,33 @@ int fill_and_copy(rmsf_stager *st, int64_t n_frames, const std::function<const f
     ST_HIP(hipEventSynchronize(st->copied[s]));
     st->copy_pending[s] = 0;
   }
-  float *dst = st->h_slot[s];
+  const int rc = fill(st->h_slot[s]);
+  if (rc != RMSF_OK) return rc;
+  // the device slot may still be read by the consumer's kernels
+  if (st->release_pending[s]) {
+    ST_HIP(hipStreamWaitEvent(st->copy_stream, st->released[s], 0));
+    st->release_pending[s] = 0;
+  }
+  const int64_t row = 3 * st->n_sel;
+  ST_HIP(hipMemcpyAsync(st->d_slot[s], st->h_slot[s], (size_t)n_frames * row * sizeof(float), hipMemcpyHostToDevice,
+                        st->copy_stream));
+  ST_HIP(hipEventRecord(st->copied[s], st->copy_stream));
+  st->copy_pending[s] = 1;
+  ST_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(consumer_stream), st->copied[s], 0));
+  *slot = s;
+  *d_batch = st->d_slot[s];
+  return RMSF_OK;
+}
+
+// Gather the selection rows of host frames into dst; `frame(i)` yields frame i.
+int gather(rmsf_stager *st, int64_t n_frames, const std::function<const float *(int64_t)> &frame, float *dst) {
   const int64_t row = 3 * st->n_sel;
   const int32_t *sel = st->sel.empty() ? nullptr : st->sel.data();
   const int64_t n_sel = st->n_sel;
   // split work into (frame, atom-range) pieces so one big frame still spreads
   const int64_t piece = 1 << 16;
   const int64_t per_frame = (n_sel + piece - 1) / piece;
-  bool bad = false;
+  std::atomic<bool> bad{false};
   st->pool->run(n_frames * per_frame, [&](int64_t w) {
     const int64_t f = w / per_frame, a0 = (w % per_frame) * piece, a1 = std::min(n_sel, a0 + piece);
     const float *src = frame(f);
@@ -179,20 +205,7 @@ int fill_and_copy(rmsf_stager *st, int64_t n_frames, const std::function<const f
       }
     }
   });
-  if (bad) return fail(RMSF_EINVAL, "rmsf_stager_stage: null frame pointer");
-  // the device slot may still be read by the consumer's kernels
-  if (st->release_pending[s]) {
-    ST_HIP(hipStreamWaitEvent(st->copy_stream, st->released[s], 0));
-    st->release_pending[s] = 0;
-  }
-  ST_HIP(hipMemcpyAsync(st->d_slot[s], dst, (size_t)n_frames * row * sizeof(float), hipMemcpyHostToDevice,
-                        st->copy_stream));
-  ST_HIP(hipEventRecord(st->copied[s], st->copy_stream));
-  st->copy_pending[s] = 1;
-  ST_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(consumer_stream), st->copied[s], 0));
-  *slot = s;
-  *d_batch = st->d_slot[s];
-  return RMSF_OK;
+  return bad ? fail(RMSF_EINVAL, "rmsf_stager_stage: null frame pointer") : RMSF_OK;
 }
 
 }  // namespace
@@ -237,6 +250,7 @@ RMSF_EXPORT int rmsf_stager_create(int64_t n_atoms_frame, int64_t n_sel, const i
     return fail(RMSF_ENOMEM, std::string("rmsf_stager_create: ") + hipGetErrorString(e));
   }
   st->pool = new Pool(std::max(0, n_threads - 1));
+  st->n_threads = std::max(1, n_threads);
   *out = st;
   return RMSF_OK;
 }
@@ -251,14 +265,32 @@ RMSF_EXPORT int rmsf_stager_stage(rmsf_stager *st, const float *h_frames, int64_
   if (!st || !h_frames || !slot || !d_batch || h_frame_stride < 3 * st->n_atoms_frame)
     return fail(RMSF_EINVAL, "rmsf_stager_stage: bad arguments");
   return fill_and_copy(
-      st, n_frames, [&](int64_t f) { return h_frames + f * h_frame_stride; }, consumer_stream, slot, d_batch);
+      st, n_frames, [&](float *dst) { return gather(st, n_frames, [&](int64_t f) { return h_frames + f * h_frame_stride; }, dst); },
+      consumer_stream, slot, d_batch);
 }
 
 RMSF_EXPORT int rmsf_stager_stage_ptrs(rmsf_stager *st, const float *const *h_frame_ptrs, int64_t n_frames,
                                        void *consumer_stream, int *slot, float **d_batch) {
   if (!st || !h_frame_ptrs || !slot || !d_batch) return fail(RMSF_EINVAL, "rmsf_stager_stage_ptrs: bad arguments");
   return fill_and_copy(
-      st, n_frames, [&](int64_t f) { return h_frame_ptrs[f]; }, consumer_stream, slot, d_batch);
+      st, n_frames, [&](float *dst) { return gather(st, n_frames, [&](int64_t f) { return h_frame_ptrs[f]; }, dst); },
+      consumer_stream, slot, d_batch);
+}
+
+RMSF_EXPORT int rmsf_stager_stage_xtc(rmsf_stager *st, const rmsf_xtc *x, int64_t f0, int64_t n_frames, int64_t step,
+                                      void *consumer_stream, int *slot, float **d_batch) {
+  if (!st || !x || !slot || !d_batch || step < 1 || f0 < 0)
+    return fail(RMSF_EINVAL, "rmsf_stager_stage_xtc: bad arguments");
+  if (rmsf_internal_xtc_natoms(x) != st->n_atoms_frame)
+    return fail(RMSF_EINVAL, "rmsf_stager_stage_xtc: atom count differs from the stager's frame size");
+  if (n_frames > 0 && f0 + (n_frames - 1) * step >= rmsf_internal_xtc_nframes(x))
+    return fail(RMSF_EINVAL, "rmsf_stager_stage_xtc: frame out of range");
+  const int32_t *sel = st->sel.empty() ? nullptr : st->sel.data();
+  const int nt = st->n_threads;
+  return fill_and_copy(
+      st, n_frames,
+      [&](float *dst) { return rmsf_internal_xtc_decode(x, f0, n_frames, step, sel, st->n_sel, dst, 3 * st->n_sel, nt); },
+      consumer_stream, slot, d_batch);
 }
 
 RMSF_EXPORT int rmsf_stager_release(rmsf_stager *st, int slot, void *consumer_stream) {

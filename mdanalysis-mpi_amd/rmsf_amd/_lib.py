@@ -70,8 +70,14 @@ SIGNATURES = {
     "rmsf_stager_destroy": (c_int, [P]),
     "rmsf_stager_stage": (c_int, [P, P, c_int64, c_int64, P, POINTER(c_int), POINTER(c_void_p)]),
     "rmsf_stager_stage_ptrs": (c_int, [P, P, c_int64, P, POINTER(c_int), POINTER(c_void_p)]),
+    "rmsf_stager_stage_xtc": (c_int, [P, P, c_int64, c_int64, c_int64, P, POINTER(c_int), POINTER(c_void_p)]),
     "rmsf_stager_release": (c_int, [P, c_int, P]),
     "rmsf_stager_synchronize": (c_int, [P]),
+    "rmsf_xtc_open": (c_int, [c_char_p, POINTER(c_void_p), POINTER(c_int64), POINTER(c_int64)]),
+    "rmsf_xtc_close": (c_int, [P]),
+    "rmsf_xtc_frame_info": (c_int, [P, c_int64, POINTER(c_int32), POINTER(ctypes.c_float), P]),
+    "rmsf_xtc_read": (c_int, [P, c_int64, c_int64, c_int64, P, c_int64, P, c_int]),
+    "rmsf_xtc_write": (c_int, [c_char_p, P, c_int64, c_int64, ctypes.c_float, P, c_int]),
 }
 
 _lib = None

@@ -14,7 +14,8 @@ superposes every frame on ``ref_frame`` first (config C3).  Under
 contiguous blocks of RMSF.py:65-69 and merged with RCCL.
 
 Inputs: an MDAnalysis AtomGroup, a host ``numpy`` float32 array
-[n_frames, n_atoms, 3], or an HBM-resident torch tensor of that shape.
+[n_frames, n_atoms, 3], an HBM-resident torch tensor of that shape, or the
+path of a GROMACS ``.xtc`` file (decoded natively, selection by ``select``).
 """
 from __future__ import annotations
 
@@ -24,7 +25,7 @@ import torch
 from . import parallel
 from .engine import Engine
 from .pipeline import run_pipeline
-from .sources import AtomGroupSource, DeviceSource, FrameList, HostSource
+from .sources import AtomGroupSource, DeviceSource, FrameList, HostSource, XtcSource
 
 
 class Results(dict):
@@ -116,6 +117,12 @@ class RMSF:
                 return DeviceSource(x, self.select), self.masses
         if isinstance(x, np.ndarray):
             return HostSource(x, self.select, batch_frames=self.batch_frames), self.masses
+        if isinstance(x, (str, bytes)) or hasattr(x, "__fspath__"):
+            import os
+            path = os.fspath(x)
+            if not str(path).lower().endswith(".xtc"):
+                raise ValueError(f"only .xtc trajectory files are read natively, got {path!r}")
+            return XtcSource(path, self.select, batch_frames=self.batch_frames), self.masses
         if hasattr(x, "universe") and hasattr(x, "positions"):
             masses = self.masses
             if masses is None and self.align is not None:

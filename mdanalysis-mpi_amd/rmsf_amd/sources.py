@@ -188,6 +188,46 @@ class HostSource:
             yield Batch(ptr, 3 * self.n_sel, n, None, lambda s=slot: self.stager.release(s, stream))
 
 
+class XtcSource:
+    """GROMACS XTC file: frames decoded frame-parallel on host threads straight
+    into the stager's pinned slots (selection applied), then DMA'd -- the
+    C5 path (XTC-decoded trajectory streamed from the host)."""
+
+    def __init__(self, path, sel=None, batch_frames: int | None = None, n_slots: int = 3, n_threads: int = 8):
+        from .xtc import XTCFile
+
+        self.xtc = XTCFile(path)
+        self.n_traj, self.n_atoms = self.xtc.n_frames, self.xtc.n_atoms
+        sel_arr = None if sel is None else np.ascontiguousarray(sel, dtype=np.int64)
+        if sel_arr is not None and sel_arr.size and (sel_arr.min() < 0 or sel_arr.max() >= self.n_atoms):
+            raise IndexError("selection index out of range")
+        self.n_sel = self.n_atoms if sel_arr is None else len(sel_arr)
+        if batch_frames is None:
+            batch_frames = max(1, min(4096, (64 << 20) // max(1, 12 * self.n_sel)))
+        self.batch_frames = batch_frames
+        self.stager = Stager(self.n_atoms, self.n_sel, sel_arr, batch_frames, n_slots, n_threads)
+
+    def holds(self, frame: int) -> bool:
+        return 0 <= frame < self.n_traj
+
+    def _stage(self, first: int, step: int, n: int, stream: int):
+        slot, dptr = ctypes.c_int(), ctypes.c_void_p()
+        call("rmsf_stager_stage_xtc", self.stager._h, self.xtc.handle, first, n, step, stream, ctypes.byref(slot),
+             ctypes.byref(dptr))
+        return slot.value, dptr.value
+
+    def reference(self, frame: int, stream: int) -> Batch:
+        slot, ptr = self._stage(frame, 1, 1, stream)
+        return Batch(ptr, 3 * self.n_sel, 1, None, lambda: self.stager.release(slot, stream))
+
+    def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
+        bf = min(max_frames, self.batch_frames)
+        for i in range(b0, b1, bf):
+            n = min(bf, b1 - i)
+            slot, ptr = self._stage(frames.r[i], frames.step, n, stream)
+            yield Batch(ptr, 3 * self.n_sel, n, None, lambda s=slot: self.stager.release(s, stream))
+
+
 class AtomGroupSource:
     """MDAnalysis AtomGroup: per-Timestep ``ag.positions`` (the selection rows,
     RMSF.py:95,128) packed into a host batch and staged to the device."""
@@ -235,4 +275,4 @@ class AtomGroupSource:
             yield Batch(ptr, 3 * self.n_sel, n, None, lambda s=slot: self.stager.release(s, stream))
 
 
-__all__ = ["Batch", "Stager", "FrameList", "DeviceSource", "HostSource", "AtomGroupSource", "_lib"]
+__all__ = ["Batch", "Stager", "FrameList", "DeviceSource", "HostSource", "XtcSource", "AtomGroupSource", "_lib"]
