@@ -1,0 +1,213 @@
+"""Minimal GRO topology + selection fallback.
+
+RMSF.py builds ``mda.Universe(GRO, XTC)`` (RMSF.py:34,56) and selects
+``"protein and name CA"`` (RMSF.py:77,116,120,126).  When MDAnalysis is not
+installed, this module reads the GRO file itself and evaluates a subset of
+the MDAnalysis selection language, so the whole script runs natively:
+
+    top = GroTopology("adk.gro")
+    sel = top.select("protein and name CA")        # sorted atom indices
+    RMSF("adk.xtc", select=sel, align="average").run()
+
+Supported selection grammar (MDAnalysis keywords and precedence: ``not`` >
+``and`` > ``or``, parentheses): ``all``, ``none``, ``protein``, ``backbone``
+(protein and name N CA C O), ``name``/``resname`` with shell-style wildcards,
+``resid a``/``resid a-b``/``resid a:b``, ``index``/``bynum`` (0- / 1-based,
+ranges).  ``protein`` uses MDAnalysis' ProteinSelection residue-name set as
+far as restated here (standard, CHARMM, GROMACS OPLS/GROMOS/AMBER variants).
+Host-only pure Python; results are plain index arrays, so selections made by
+MDAnalysis (``ag.indices``) can always be passed instead.  Parity with
+MDAnalysis selections is UNPINNED here (MDAnalysis absent).
+"""
+from __future__ import annotations
+
+import fnmatch
+import re
+
+import numpy as np
+
+# MDAnalysis ProteinSelection.prot_res (restated; upstream not vendored)
+PROTEIN_RESNAMES = frozenset("""
+ALA ARG ASN ASP CYS GLN GLU GLY HSD HSE HSP ILE LEU LYS MET PHE PRO SER THR TRP TYR VAL ALAD
+HIS MSE
+ARGN ASPH CYS2 CYSH QLN PGLU GLUH HIS1 HISD HISE HISH LYSH
+ASN1 CYS1 HISA HISB HIS2
+HID HIE HIP ORN DAB LYN HYP CYM CYX ASH GLH ACE NME
+NALA NGLY NSER NTHR NLEU NILE NVAL NASN NGLN NARG NHID NHIE NHIP NTRP NPHE NTYR NGLU NASP NLYS NPRO NCYS NCYX NMET
+CALA CGLY CSER CTHR CLEU CILE CVAL CASN CGLN CARG CHID CHIE CHIP CTRP CPHE CTYR CGLU CASP CLYS CPRO CCYS CCYX CMET
+CME ASF
+""".split())
+BACKBONE_NAMES = frozenset(["N", "CA", "C", "O"])
+
+
+class GroTopology:
+    """Atoms (resid, resname, name) and the frames of a .gro file.
+
+    ``positions`` follow MDAnalysis' GROReader rounding: the text is parsed
+    into float32 nm, then converted in place to Angstrom (x10 in float32)."""
+
+    def __init__(self, path: str):
+        self.path = path
+        frames, atoms = self._parse(path)
+        self.resids = np.array([a[0] for a in atoms], dtype=np.int64)
+        self.resnames = np.array([a[1] for a in atoms], dtype=object)
+        self.names = np.array([a[2] for a in atoms], dtype=object)
+        self.n_atoms = len(atoms)
+        self.frames = np.stack(frames)  # [n_frames, n_atoms, 3] float32 Angstrom
+
+    @property
+    def positions(self) -> np.ndarray:
+        return self.frames[0]
+
+    @staticmethod
+    def _parse(path):
+        lines = open(path).read().splitlines()
+        frames, atoms = [], None
+        i = 0
+        while i + 1 < len(lines):
+            n = int(lines[i + 1].split()[0])
+            body = lines[i + 2:i + 2 + n]
+            if len(body) < n:
+                break
+            # coordinate field width from the decimal-point spacing (GRO variable precision)
+            first = body[0]
+            d0 = first.find(".", 20)
+            d1 = first.find(".", d0 + 1)
+            cs = d1 - d0 if d0 > 0 and d1 > 0 else 8
+            xyz = np.empty((n, 3), dtype=np.float32)
+            rows = []
+            for k, line in enumerate(body):
+                if atoms is None:
+                    rows.append((int(line[0:5]), line[5:10].strip(), line[10:15].strip()))
+                for c in range(3):
+                    xyz[k, c] = float(line[20 + cs * c:20 + cs * (c + 1)])
+            if atoms is None:
+                atoms = rows
+            elif n != len(atoms):
+                raise ValueError(f"{path}: frame {len(frames)} has {n} atoms, expected {len(atoms)}")
+            xyz *= np.float32(10.0)  # nm -> Angstrom, in place in float32 (MDAnalysis convert_pos_from_native)
+            frames.append(xyz)
+            i += 2 + n + 1  # title, count, atoms, box
+        if not frames:
+            raise ValueError(f"{path}: no complete GRO frame")
+        return frames, atoms
+
+    def select(self, selection: str) -> np.ndarray:
+        """Sorted unique atom indices (MDAnalysis ordering) matching ``selection``."""
+        mask = _Parser(selection, self).parse()
+        return np.flatnonzero(mask)
+
+
+# ---------------------------------------------------------------------------
+_TOKEN = re.compile(r"\(|\)|[^\s()]+")
+
+
+class _Parser:
+    """Recursive-descent evaluation: or_expr := and_expr ('or' and_expr)*,
+    and_expr := unary ('and' unary)*, unary := 'not' unary | atom."""
+
+    KEYWORDS = {"and", "or", "not", "(", ")"}
+    SELECTORS = {"all", "none", "protein", "backbone", "name", "resname", "resid", "index", "bynum"}
+
+    def __init__(self, text: str, top: GroTopology):
+        self.tok = _TOKEN.findall(text)
+        self.i = 0
+        self.top = top
+
+    def peek(self):
+        return self.tok[self.i] if self.i < len(self.tok) else None
+
+    def take(self):
+        t = self.peek()
+        if t is None:
+            raise ValueError("unexpected end of selection")
+        self.i += 1
+        return t
+
+    def parse(self) -> np.ndarray:
+        m = self.or_expr()
+        if self.peek() is not None:
+            raise ValueError(f"unexpected token {self.peek()!r} in selection")
+        return m
+
+    def or_expr(self):
+        m = self.and_expr()
+        while self.peek() == "or":
+            self.take()
+            m = m | self.and_expr()
+        return m
+
+    def and_expr(self):
+        m = self.unary()
+        while self.peek() == "and":
+            self.take()
+            m = m & self.unary()
+        return m
+
+    def unary(self):
+        if self.peek() == "not":
+            self.take()
+            return ~self.unary()
+        if self.peek() == "(":
+            self.take()
+            m = self.or_expr()
+            if self.take() != ")":
+                raise ValueError("missing ')' in selection")
+            return m
+        return self.atom()
+
+    def _values(self):
+        vals = []
+        while self.peek() is not None and self.peek() not in self.KEYWORDS and self.peek() not in self.SELECTORS:
+            vals.append(self.take())
+        if not vals:
+            raise ValueError("selection keyword without values")
+        return vals
+
+    def atom(self):
+        t = self.take()
+        top = self.top
+        n = top.n_atoms
+        if t == "all":
+            return np.ones(n, bool)
+        if t == "none":
+            return np.zeros(n, bool)
+        if t == "protein":
+            return np.array([r in PROTEIN_RESNAMES for r in top.resnames], bool)
+        if t == "backbone":
+            prot = np.array([r in PROTEIN_RESNAMES for r in top.resnames], bool)
+            return prot & np.array([a in BACKBONE_NAMES for a in top.names], bool)
+        if t in ("name", "resname"):
+            pats = self._values()
+            field = top.names if t == "name" else top.resnames
+            return np.array([any(fnmatch.fnmatchcase(v, p) for p in pats) for v in field], bool)
+        if t in ("resid", "index", "bynum"):
+            field = top.resids if t == "resid" else np.arange(n) + (1 if t == "bynum" else 0)
+            m = np.zeros(n, bool)
+            for v in self._values():
+                lo, hi = _range(v)
+                m |= (field >= lo) & (field <= hi)
+            return m
+        raise ValueError(f"unsupported selection keyword {t!r} (native fallback; use MDAnalysis for the full language)")
+
+
+def _range(v: str):
+    for sep in ("-", ":"):
+        if sep in v[1:]:
+            a, b = v.split(sep, 1) if not v.startswith("-") else (v, v)
+            return int(a), int(b)
+    return int(v), int(v)
+
+
+def write_gro(path: str, resids, resnames, names, frames_angstrom, box=(10.0, 10.0, 10.0), title="rmsf_amd"):
+    """Write a (multi-frame) .gro file, %8.3f nm coordinates (tests/tools)."""
+    frames = np.asarray(frames_angstrom, dtype=np.float32)
+    if frames.ndim == 2:
+        frames = frames[None]
+    with open(path, "w") as fh:
+        for f in frames:
+            fh.write(f"{title}\n{len(names):5d}\n")
+            for k, (ri, rn, an) in enumerate(zip(resids, resnames, names)):
+                x, y, z = (f[k].astype(np.float64) / 10.0)
+                fh.write(f"{int(ri) % 100000:5d}{rn:<5s}{an:>5s}{(k + 1) % 100000:5d}{x:8.3f}{y:8.3f}{z:8.3f}\n")
+            fh.write("".join(f"{b:10.5f}" for b in box) + "\n")

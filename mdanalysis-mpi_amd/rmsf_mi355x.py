@@ -9,6 +9,10 @@
     # without MDAnalysis: a synthetic trajectory generated in HBM
     python rmsf_mi355x.py --synthetic 100000 2000 --align frame0
 
+Without MDAnalysis, a .gro topology and an .xtc (or multi-frame .gro)
+trajectory are read natively (rmsf_amd.topology / rmsf_amd.xtc) and the
+selection is evaluated by the native subset of the selection language.
+
 Defaults mirror RMSF.py: selection "protein and name CA" (RMSF.py:77),
 ref_frame 0 (RMSF.py:63), the two-sweep average alignment (RMSF.py:89-140),
 frame blocks per rank (RMSF.py:65-69) with the per-rank range printed as at
@@ -67,11 +71,24 @@ def main(argv=None) -> int:
     else:
         if not (a.topology and a.trajectory):
             ap.error("--topology/--trajectory (MDAnalysis) or --synthetic is required")
-        import MDAnalysis as mda  # not installed in the build container
+        try:
+            import MDAnalysis as mda
+        except ImportError:
+            mda = None
+        if mda is not None:
+            u = mda.Universe(a.topology, a.trajectory)
+            ag = u.select_atoms(a.select)
+            rmsf = RMSF(ag, align=align, ref_frame=a.ref_frame, verbose=True).run().results.rmsf
+        else:
+            # native fallback: GRO topology + selection subset, XTC (or multi-frame GRO) trajectory
+            from rmsf_amd.topology import GroTopology
 
-        u = mda.Universe(a.topology, a.trajectory)
-        ag = u.select_atoms(a.select)
-        rmsf = RMSF(ag, align=align, ref_frame=a.ref_frame, verbose=True).run().results.rmsf
+            if not a.topology.lower().endswith(".gro"):
+                ap.error("without MDAnalysis only .gro topologies are read natively")
+            top = GroTopology(a.topology)
+            sel = top.select(a.select)
+            traj = a.trajectory if a.trajectory.lower().endswith(".xtc") else GroTopology(a.trajectory).frames
+            rmsf = RMSF(traj, select=sel, align=align, ref_frame=a.ref_frame, verbose=True).run().results.rmsf
     if rank == 0:
         print(f"RMSF over {len(rmsf)} atoms: mean {rmsf.mean():.6f} A, max {rmsf.max():.6f} A", flush=True)
         if a.out:
