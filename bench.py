@@ -93,6 +93,59 @@ def load_traffic(workload: str, n_atoms: int, n_frames: int):
     return None
 
 
+def c1_latency(eng, no_cpu: bool) -> dict:
+    """Config C1 shape (BASELINE configs[0]): 3341 atoms, 214 selected, 98
+    frames, RMSF.py's two-sweep average alignment -- latency of one full
+    RMSF.py computation, HBM-resident (synthetic data of that shape; the adk
+    files are not available).  The CPU figure is the numpy restatement of
+    the same computation on one core (RMSF.py:23-25 pins one thread/rank)."""
+    import numpy as np
+    import torch
+
+    from rmsf_amd.pipeline import run_pipeline
+    from rmsf_amd.sources import DeviceSource, FrameList
+    from rmsf_amd.synth import generate, motion_table
+
+    n_atoms, nf = 3341, 98
+    sel = np.sort(np.random.default_rng(12).choice(n_atoms, 214, replace=False))
+    mt = motion_table(13, nf)
+    traj = generate(eng, n_atoms, 0, nf, seed=11, motion=mt)
+    src = DeviceSource(traj, sel)
+    fl = FrameList(nf)
+    for _ in range(5):
+        run_pipeline(eng, src, fl, align="average")
+    torch.cuda.synchronize()
+    reps = 50
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        res = run_pipeline(eng, src, fl, align="average")
+    torch.cuda.synchronize()
+    gpu_ms = (time.perf_counter() - t0) / reps * 1e3
+    from rmsf_amd.pipeline import CapturedPipeline
+
+    cap = CapturedPipeline(eng, src, fl, align="average")
+    for _ in range(5):
+        cap.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        cap.replay()
+    torch.cuda.synchronize()
+    graph_ms = (time.perf_counter() - t0) / reps * 1e3
+    same = bool(torch.equal(cap.result.rmsf, res.rmsf))
+    out = {"workload": "C1 shape: 3341 atoms, 214 selected, 98 frames, RMSF.py two-sweep",
+           "gpu_ms_eager": gpu_ms, "gpu_ms_hipgraph": graph_ms, "hipgraph_bitwise_equal": same}
+    if not no_cpu:
+        from oracle import rmsf_oracle as O
+
+        host = traj.cpu().numpy()
+        t0 = time.perf_counter()
+        O.rmsf_script(host, sel, None, size=1, align="average")
+        out["cpu_ms_1core_numpy"] = (time.perf_counter() - t0) * 1e3
+        out["note"] = "CPU: oracle restatement on 1 core (no XTC decode, no re-selection): optimistic"
+    return out
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", 0))
@@ -271,6 +324,7 @@ def main():
             }
         if cpu_c3 is not None:
             modes["c3_frame0"]["cpu_baseline"] = cpu_c3
+        modes["c1_rmsf_py"] = c1_latency(eng, a.no_cpu_baseline)
         out["modes"] = modes
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -236,3 +236,40 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     return PipelineResult(rmsf=rmsf, mean=mean.view(n_sel, 3), m2=m2.view(n_sel, 3), n_frames=n_total,
                           n_local=n_local, block=(b0, b1),
                           average=None if average is None else average.view(n_sel, 3), rmsd=rmsd)
+
+
+class CapturedPipeline:
+    """The whole pipeline of ``run_pipeline`` recorded once into a hipGraph
+    (``torch.cuda.CUDAGraph``) and replayed with no per-kernel host work.
+
+    For latency-bound sizes (e.g. config C1: 214 atoms x 98 frames, ~15
+    launches whose kernels run for microseconds) the eager path is bound by
+    host launch overhead; replay removes it.  Every ABI entry point used here
+    is asynchronous and performs no allocation or synchronisation, so the
+    launch sequence is capture-safe.  Restrictions: single process, and an
+    HBM-resident ``DeviceSource`` (host stagers synchronise on events).  The
+    input frames may be overwritten in place between replays; ``result``
+    tensors are rewritten by every replay."""
+
+    def __init__(self, eng: Engine, source, frames: FrameList, **kw):
+        from .sources import DeviceSource
+
+        if parallel.world()[1] > 1:
+            raise NotImplementedError("graph capture is single-process (the RCCL merge is not captured)")
+        if not isinstance(source, DeviceSource):
+            raise TypeError("only HBM-resident (DeviceSource) pipelines can be captured")
+        if kw.get("timer") is not None:
+            raise ValueError("a KernelTimer cannot be captured")
+        dev = eng.device
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # warm-up outside capture (allocator pools, lazy init)
+            run_pipeline(eng, source, frames, **kw)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.result = run_pipeline(eng, source, frames, **kw)
+
+    def replay(self) -> PipelineResult:
+        self.graph.replay()
+        return self.result

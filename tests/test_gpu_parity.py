@@ -149,3 +149,26 @@ def test_bitwise_reproducible(c1):
     np.testing.assert_array_equal(a.rmsf, b.rmsf)
     np.testing.assert_array_equal(a.sumsquares, b.sumsquares)
     np.testing.assert_array_equal(a.average, b.average)
+
+
+def test_captured_pipeline_replay(c1):
+    """hipGraph replay == eager run bit for bit, and tracks in-place input
+    updates (frames rewritten between replays)."""
+    from rmsf_amd.engine import Engine
+    from rmsf_amd.pipeline import CapturedPipeline, run_pipeline
+    from rmsf_amd.sources import DeviceSource, FrameList
+    d, traj = c1
+    eng = Engine()
+    x = torch.tensor(traj, device="cuda")
+    src, fl = DeviceSource(x, d["sel"]), FrameList(len(traj))
+    cap = CapturedPipeline(eng, src, fl, align="average")
+    eager = run_pipeline(eng, src, fl, align="average")
+    r = cap.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(r.rmsf, eager.rmsf) and torch.equal(r.average, eager.average)
+    np.testing.assert_allclose(r.rmsf.cpu().numpy(), d["rmsf_average_P1"], atol=TOL)
+    x.copy_(torch.flip(x, dims=[0]))  # new data, same buffer
+    r = cap.replay()
+    torch.cuda.synchronize()
+    exp = O.rmsf_script(traj[::-1].copy(), d["sel"], None, size=1, align="average")["rmsf"]
+    np.testing.assert_allclose(r.rmsf.cpu().numpy(), exp, atol=TOL)
