@@ -48,9 +48,10 @@ extern "C" {
  * R[9] (row-major, applied as x @ R, RMSF.py:100), mobile COM[3], rmsd, pad[3] */
 #define RMSF_XFORM_DOUBLES 16
 /* Size of the reference record written by rmsf_reference_setup():
- * ref_com[3], sum_r[3] (= sum of centred ref coords), G_ref (= sum |r|^2),
- * total mass, n_sel, pad[7]                                                   */
-#define RMSF_REFINFO_DOUBLES 16
+ * [0..15]  ref_com[3], sum_r[3] (= sum of centred ref coords),
+ *          G_ref (= sum |r|^2), total mass, n_sel, pad[7]
+ * [16..]   scratch for the setup's fixed-order block reductions             */
+#define RMSF_REFINFO_DOUBLES 2064
 
 /* ---- library / device helpers (for callers without their own allocator) */
 int rmsf_abi_version(void);

@@ -13,7 +13,7 @@
 //                        and the qcprot inner product (RMSF.py:94-97,127-131).
 //   * k_qcp_frames       per-frame QCP (qcprot FastCalcRMSDAndRotation, the
 //                        published Theobald/Liu algorithm), one wave per frame.
-//   * k_reference        RMSF.py:80-87 / 113-118 reference centring.
+//   * k_ref_com/center/finish  RMSF.py:80-87 / 113-118 reference centring.
 //   * k_chan_merge       second_order_moments, RMSF.py:36-41.
 //   * k_finalize         RMSF.py:146.
 //   * k_synth            counter-based synthetic trajectory generator.
@@ -58,7 +58,6 @@ inline hipStream_t S(void *stream) { return reinterpret_cast<hipStream_t>(stream
 
 constexpr int kBlock = 256;
 constexpr int kXform = RMSF_XFORM_DOUBLES;
-constexpr int kRefInfo = RMSF_REFINFO_DOUBLES;
 constexpr int kStats = 16;       // doubles per (frame, chunk) partial
 constexpr int64_t kAccumBlocks = 3584;       // target workgroups, k_welford_flat
 constexpr int64_t kAccumBlocksAtom = 4608;   // target workgroups, k_accum_atoms
@@ -586,31 +585,96 @@ __device__ __forceinline__ void block_sum_1024(double (&v)[N], double (*red)[N])
   }
 }
 
-// k_reference: one 1024-thread block.  RMSF.py:84-85 / 117-118.
+// Reference setup, RMSF.py:84-85 / 117-118, as three launches over
+// kRefBlocks-bounded grids with fixed-order (deterministic) reductions whose
+// per-block partials live in the scratch tail of the caller's refinfo record:
+//   k_ref_com     per-block sum m x, sum m            -> scratch1[b][4]
+//   k_ref_center  COM from scratch1 (same order in every block), r = x - com
+//                 -> d_ref; per-block sum r, sum |r|^2 -> scratch2[b][4]
+//   k_ref_finish  one block folds scratch2            -> info[0..8]
+constexpr int kRefBlocks = 256;
+constexpr int kRefThreads = 256;
+static_assert(RMSF_REFINFO_DOUBLES >= 16 + 2 * 4 * kRefBlocks, "refinfo scratch");
+
+template <bool FROM_F32, bool GATHER>
+__device__ __forceinline__ void ref_load(const float *__restrict__ frame, const double *__restrict__ avg,
+                                         const int32_t *__restrict__ sel, int64_t a, double &x, double &y,
+                                         double &z) {
+  if (FROM_F32) {
+    const float *p = frame + (GATHER ? 3 * (int64_t)sel[a] : 3 * a);
+    x = (double)p[0];
+    y = (double)p[1];
+    z = (double)p[2];
+  } else {
+    x = avg[3 * a];
+    y = avg[3 * a + 1];
+    z = avg[3 * a + 2];
+  }
+}
+
+__device__ __forceinline__ void block_sum4(double (&v)[4], double *out) {
+  __shared__ double red[kRefThreads / 64][4];
+  wave_sum(v);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0)
+    for (int j = 0; j < 4; ++j) red[w][j] = v[j];
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double t = 0.0;
+    for (int i = 0; i < kRefThreads / 64; ++i) t += red[i][threadIdx.x];
+    out[threadIdx.x] = t;
+  }
+}
+
+// One wave folds nb [4]-partials: lane-strided sums, then the xor butterfly
+// (fixed order, every lane ends with the same totals).
+__device__ __forceinline__ void fold_partials(const double *__restrict__ p, int nb, double (&t)[4]) {
+  const int lane = threadIdx.x & 63;
+  for (int j = 0; j < 4; ++j) t[j] = 0.0;
+  for (int b = lane; b < nb; b += 64)
+    for (int j = 0; j < 4; ++j) t[j] += p[4 * b + j];
+  wave_sum(t);
+}
+
 template <bool FROM_F32, bool GATHER, bool MASSES>
-__global__ __launch_bounds__(1024) void k_reference(const float *__restrict__ frame,
-                                                    const double *__restrict__ avg, int64_t n_sel,
-                                                    const int32_t *__restrict__ sel,
-                                                    const double *__restrict__ masses,
-                                                    double *__restrict__ ref, double *__restrict__ info) {
-  __shared__ double red4[16][4];
-  auto coord = [&](int64_t a, int c) -> double {
-    if (FROM_F32) return (double)frame[(GATHER ? 3 * (int64_t)sel[a] : 3 * a) + c];
-    return avg[3 * a + c];
-  };
-  double v[4] = {0, 0, 0, 0};  // sum m x, sum m y, sum m z, sum m
-  for (int64_t a = threadIdx.x; a < n_sel; a += blockDim.x) {
+__global__ __launch_bounds__(kRefThreads) void k_ref_com(const float *__restrict__ frame,
+                                                         const double *__restrict__ avg, int64_t n_sel,
+                                                         const int32_t *__restrict__ sel,
+                                                         const double *__restrict__ masses,
+                                                         double *__restrict__ info) {
+  double v[4] = {0, 0, 0, 0};
+  const int64_t stride = (int64_t)gridDim.x * kRefThreads;
+  for (int64_t a = (int64_t)blockIdx.x * kRefThreads + threadIdx.x; a < n_sel; a += stride) {
+    double x, y, z;
+    ref_load<FROM_F32, GATHER>(frame, avg, sel, a, x, y, z);
     const double m = MASSES ? masses[a] : 1.0;
-    v[0] = fma(coord(a, 0), m, v[0]);
-    v[1] = fma(coord(a, 1), m, v[1]);
-    v[2] = fma(coord(a, 2), m, v[2]);
+    v[0] = fma(x, m, v[0]);
+    v[1] = fma(y, m, v[1]);
+    v[2] = fma(z, m, v[2]);
     v[3] += m;
   }
-  block_sum_1024(v, red4);
-  const double c0 = v[0] / v[3], c1 = v[1] / v[3], c2 = v[2] / v[3];
-  double w[4] = {0, 0, 0, 0};  // sum r (3), sum |r|^2
-  for (int64_t a = threadIdx.x; a < n_sel; a += blockDim.x) {
-    const double r0 = coord(a, 0) - c0, r1 = coord(a, 1) - c1, r2 = coord(a, 2) - c2;
+  block_sum4(v, info + 16 + 4 * blockIdx.x);
+}
+
+template <bool FROM_F32, bool GATHER>
+__global__ __launch_bounds__(kRefThreads) void k_ref_center(const float *__restrict__ frame,
+                                                            const double *__restrict__ avg, int64_t n_sel,
+                                                            const int32_t *__restrict__ sel,
+                                                            double *__restrict__ ref, double *__restrict__ info) {
+  __shared__ double com[4];
+  if (threadIdx.x < 64) {
+    double t[4];
+    fold_partials(info + 16, gridDim.x, t);
+    if (threadIdx.x < 4) com[threadIdx.x] = t[threadIdx.x];
+  }
+  __syncthreads();
+  const double c0 = com[0] / com[3], c1 = com[1] / com[3], c2 = com[2] / com[3];
+  double w[4] = {0, 0, 0, 0};
+  const int64_t stride = (int64_t)gridDim.x * kRefThreads;
+  for (int64_t a = (int64_t)blockIdx.x * kRefThreads + threadIdx.x; a < n_sel; a += stride) {
+    double x, y, z;
+    ref_load<FROM_F32, GATHER>(frame, avg, sel, a, x, y, z);
+    const double r0 = x - c0, r1 = y - c1, r2 = z - c2;
     ref[3 * a] = r0;
     ref[3 * a + 1] = r1;
     ref[3 * a + 2] = r2;
@@ -619,18 +683,18 @@ __global__ __launch_bounds__(1024) void k_reference(const float *__restrict__ fr
     w[2] += r2;
     w[3] = fma(r0, r0, fma(r1, r1, fma(r2, r2, w[3])));
   }
-  block_sum_1024(w, red4);
+  block_sum4(w, info + 16 + 4 * kRefBlocks + 4 * blockIdx.x);
+  if (blockIdx.x == 0 && threadIdx.x < 3) info[threadIdx.x] = threadIdx.x == 0 ? c0 : (threadIdx.x == 1 ? c1 : c2);
+  if (blockIdx.x == 0 && threadIdx.x == 3) info[7] = com[3];
+}
+
+__global__ __launch_bounds__(64) void k_ref_finish(int nb, int64_t n_sel, double *__restrict__ info) {
+  double t[4];
+  fold_partials(info + 16 + 4 * kRefBlocks, nb, t);
+  if (threadIdx.x < 4) info[3 + threadIdx.x] = t[threadIdx.x];  // sum r (3), sum |r|^2
   if (threadIdx.x == 0) {
-    info[0] = c0;
-    info[1] = c1;
-    info[2] = c2;
-    info[3] = w[0];
-    info[4] = w[1];
-    info[5] = w[2];
-    info[6] = w[3];
-    info[7] = v[3];
     info[8] = (double)n_sel;
-    for (int j = 9; j < kRefInfo; ++j) info[j] = 0.0;
+    for (int j = 9; j < 16; ++j) info[j] = 0.0;
   }
 }
 
@@ -895,19 +959,26 @@ RMSF_EXPORT int rmsf_reference_setup(const float *d_frame, const double *d_avg, 
   if (n_sel < 1 || !d_ref || !d_refinfo) return fail(RMSF_EINVAL, "rmsf_reference_setup: bad arguments");
   const bool g = d_sel != nullptr, m = d_masses != nullptr;
   hipStream_t s = S(stream);
-#define REF_LAUNCH(F, G, M) \
-  hipLaunchKernelGGL((k_reference<F, G, M>), dim3(1), dim3(1024), 0, s, d_frame, d_avg, n_sel, d_sel, d_masses, d_ref, d_refinfo)
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(kRefBlocks, (n_sel + 4 * kRefThreads - 1) / (4 * kRefThreads)));
+  const dim3 grid(nb), block(kRefThreads);
+#define COM_LAUNCH(F, G, M) hipLaunchKernelGGL((k_ref_com<F, G, M>), grid, block, 0, s, d_frame, d_avg, n_sel, d_sel, d_masses, d_refinfo)
+#define CEN_LAUNCH(F, G) hipLaunchKernelGGL((k_ref_center<F, G>), grid, block, 0, s, d_frame, d_avg, n_sel, d_sel, d_ref, d_refinfo)
   if (d_frame) {
-    if (g && m) REF_LAUNCH(true, true, true);
-    else if (g) REF_LAUNCH(true, true, false);
-    else if (m) REF_LAUNCH(true, false, true);
-    else REF_LAUNCH(true, false, false);
+    if (g && m) COM_LAUNCH(true, true, true);
+    else if (g) COM_LAUNCH(true, true, false);
+    else if (m) COM_LAUNCH(true, false, true);
+    else COM_LAUNCH(true, false, false);
+    if (g) CEN_LAUNCH(true, true);
+    else CEN_LAUNCH(true, false);
   } else {
-    if (m) REF_LAUNCH(false, false, true);
-    else REF_LAUNCH(false, false, false);
+    if (m) COM_LAUNCH(false, false, true);
+    else COM_LAUNCH(false, false, false);
+    CEN_LAUNCH(false, false);
   }
-#undef REF_LAUNCH
-  return after_launch("k_reference");
+#undef COM_LAUNCH
+#undef CEN_LAUNCH
+  hipLaunchKernelGGL(k_ref_finish, dim3(1), dim3(64), 0, s, nb, n_sel, d_refinfo);
+  return after_launch("k_ref_*");
 }
 
 RMSF_EXPORT size_t rmsf_superpose_workspace_bytes(int64_t n_sel, int64_t n_frames) {

@@ -21,7 +21,7 @@ RMSF_EEMPTY = -4
 RMSF_MODE_WELFORD = 0
 RMSF_MODE_SUM = 1
 RMSF_XFORM_DOUBLES = 16
-RMSF_REFINFO_DOUBLES = 16
+RMSF_REFINFO_DOUBLES = 2064  # 16-double record + reduction scratch
 ABI_VERSION = 1
 
 

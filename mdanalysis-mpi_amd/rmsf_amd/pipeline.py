@@ -21,7 +21,7 @@ import numpy as np
 import torch
 
 from . import parallel
-from ._lib import RMSF_MODE_SUM, RMSF_MODE_WELFORD, RMSF_XFORM_DOUBLES, RmsfEmptyError
+from ._lib import RMSF_MODE_SUM, RMSF_MODE_WELFORD, RMSF_REFINFO_DOUBLES, RMSF_XFORM_DOUBLES, RmsfEmptyError
 from .engine import Engine
 from .sources import Batch, FrameList
 
@@ -159,7 +159,7 @@ def reference_from_frame(eng: Engine, source, frame: int, n_sel: int, masses, ow
             owner = None if missing == 0 else lo
         if owner is not None:
             ref = eng.empty(n_sel, 3)
-            info = eng.empty(16)
+            info = eng.empty(RMSF_REFINFO_DOUBLES)
             if rank == owner:
                 b = source.reference(frame, eng.stream)
                 r, i = eng.reference_setup(n_sel, frame_ptr=b.ptr, sel=b.sel, masses=masses)
@@ -167,7 +167,7 @@ def reference_from_frame(eng: Engine, source, frame: int, n_sel: int, masses, ow
                 ref.copy_(r)
                 info.copy_(i)
             parallel.broadcast_(ref, owner)
-            parallel.broadcast_(info, owner)
+            parallel.broadcast_(info[:16], owner)  # the record; the rest is setup scratch
             return ref, info
     b = source.reference(frame, eng.stream)
     r, i = eng.reference_setup(n_sel, frame_ptr=b.ptr, sel=b.sel, masses=masses)
