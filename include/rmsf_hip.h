@@ -232,6 +232,120 @@ int rmsf_xtc_write(const char *path, const float *h_xyz, int64_t n_frames,
                    int64_t n_atoms, float precision, const float *h_box9,
                    int append);
 
+/* ---- RMSF context: the whole per-rank loop behind one opaque handle -------
+ * SURVEY.md 8(b)'s minimal export set, for hosts that bring neither torch
+ * nor their own device allocator (a C/C++ program, an MPI code, ctypes).
+ * A context owns, on one device: the selection and masses, the centred
+ * reference, the running Welford (n, mean, M2) and sweep-1 sum partials,
+ * workspaces, a host stager and a non-blocking stream.  Calls on one context
+ * are not re-entrant; different contexts may be driven from different host
+ * threads.  Every call makes the context's device current for its duration
+ * and restores the caller's device.  Work is asynchronous on the context
+ * stream; rmsf_get_* synchronise.
+ *
+ * RMSF.py's per-rank loop (RMSF.py:80-146) in these terms:
+ *   rmsf_ctx_create(dev, n_atoms, n_sel, ca_indices, masses, 0, &c);
+ *   rmsf_set_reference_frame(c, frame0, is_dev);            RMSF.py:80-87
+ *   rmsf_push_frames(c, block, n, 0, RMSF_PUSH_ALIGN_SUM, is_dev);  :89-105
+ *   rmsf_multi_allreduce_sum(&c, 1)   (or the callback form)  :107-110
+ *   rmsf_set_reference_average(c);                           :111-118
+ *   rmsf_push_frames(c, block, n, 0, RMSF_PUSH_ALIGN_WELFORD, is_dev); :120-138
+ *   rmsf_multi_chan_merge(&c, 1)      (or the callback form)  :140-143
+ *   rmsf_get_rmsf(c, h_rmsf);                                 :145-146    */
+typedef struct rmsf_ctx rmsf_ctx;
+
+/* push modes for rmsf_push_frames() / rmsf_push_xtc() */
+#define RMSF_PUSH_WELFORD 0       /* Welford on the raw frames (rms.RMSF)     */
+#define RMSF_PUSH_ALIGN_SUM 1     /* superpose, f64 sum      (RMSF.py:91-105) */
+#define RMSF_PUSH_ALIGN_WELFORD 2 /* superpose, Welford      (RMSF.py:123-138)*/
+#define RMSF_PUSH_SUM 3           /* f64 sum of the raw frames                */
+
+/* h_sel: n_sel int64 atom indices (MDAnalysis AtomGroup.indices; copied),
+ * NULL = atoms 0..n_sel-1.  h_masses: n_sel f64 (copied) or NULL = uniform
+ * (RMSF.py:84 center_of_mass).  flags must be 0.      */
+int rmsf_ctx_create(int device, int64_t n_atoms, int64_t n_sel,
+                    const int64_t *h_sel, const double *h_masses, int flags,
+                    rmsf_ctx **out);
+int rmsf_ctx_destroy(rmsf_ctx *ctx);
+/* the context's hipStream_t (order producer work of device frames on it) */
+int rmsf_ctx_stream(rmsf_ctx *ctx, void **stream);
+int rmsf_ctx_synchronize(rmsf_ctx *ctx);
+/* Host-frame staging: frames per pinned slot (<= 0: ~64 MiB worth), slots
+ * (>= 1) and gather threads.  Takes effect at the next host push.           */
+int rmsf_ctx_set_staging(rmsf_ctx *ctx, int64_t batch_frames, int n_slots,
+                         int n_threads);
+/* Zero the running Welford (what & 1) and/or sweep-1 sum (what & 2) state. */
+int rmsf_ctx_reset(rmsf_ctx *ctx, int what);
+
+/* Reference given directly: h_ref_centered f64 [n_sel][3], h_ref_com f64[3]
+ * (RMSF.py:85-86 ref_ca / ref_com).                                         */
+int rmsf_set_reference(rmsf_ctx *ctx, const double *h_ref_centered,
+                       const double *h_ref_com);
+/* Reference from a float32 frame of n_atoms atoms (RMSF.py:80-87). */
+int rmsf_set_reference_frame(rmsf_ctx *ctx, const float *xyz,
+                             int is_device_ptr);
+/* Reference = the context's sweep-1 average sum/n (RMSF.py:111-118);
+ * RMSF_EEMPTY when no frame was summed.                                      */
+int rmsf_set_reference_average(rmsf_ctx *ctx);
+
+/* Push n_frames float32 frames of n_atoms atoms (frame_stride floats apart,
+ * 0 = 3*n_atoms; a multiple of it implements `step`).  is_device_ptr != 0:
+ * the frames are in HBM and must stay valid and unmodified until the
+ * context is synchronised; otherwise they are host memory, gathered to the
+ * selection and streamed through the context's pinned stager (the host
+ * buffer may be reused when the call returns).                               */
+int rmsf_push_frames(rmsf_ctx *ctx, const float *xyz, int64_t n_frames,
+                     int64_t frame_stride, int mode, int is_device_ptr);
+/* Push XTC frames f0, f0+step, ... (n_frames) decoded by the native reader
+ * straight into the stager (RMSF.py:92,124 frame source).                    */
+int rmsf_push_xtc(rmsf_ctx *ctx, const rmsf_xtc *x, int64_t f0,
+                  int64_t n_frames, int64_t step, int mode);
+
+/* Running Welford partial (RMSF.py:120-121,137-138): *n frames, mean and M2
+ * f64 [n_sel][3] (any output may be NULL).  Synchronises.                    */
+int rmsf_get_partial(rmsf_ctx *ctx, int64_t *n, double *h_mean, double *h_m2);
+/* Sweep-1 sum (RMSF.py:103,105): *n frames and f64 [n_sel][3]. */
+int rmsf_get_sum(rmsf_ctx *ctx, int64_t *n, double *h_sum);
+/* Average structure sum/n (RMSF.py:111; AverageStructure.results.positions). */
+int rmsf_get_average(rmsf_ctx *ctx, double *h_avg);
+/* rmsf = sqrt(M2.sum(axis=1)/n) (RMSF.py:146), f64 [n_sel]. */
+int rmsf_get_rmsf(rmsf_ctx *ctx, double *h_rmsf);
+/* Replace the running Welford state (checkpoint restore / external merge). */
+int rmsf_set_partial(rmsf_ctx *ctx, int64_t n, const double *h_mean,
+                     const double *h_m2);
+
+/* ---- cross-rank exchange (RMSF.py:107-110 all-reduce, :140-143 reduce) -----
+ * Each exchange leaves the GLOBAL result in every participating context:
+ *   allreduce_sum: sweep-1 sum and frame count summed over ranks;
+ *   chan_merge:    exact k-way Chan of the Welford partials, as three
+ *                  all-reduce(SUM) steps -- n, sum w_k mean_k (w_k=n_k/n),
+ *                  sum M2_k + n_k (mean_k - mean)^2.  Empty ranks contribute
+ *                  nothing; RMSF_EEMPTY if n == 0.
+ * Three transports, the same arithmetic:
+ *   (1) a caller callback -- fn sums the device buffer d_buf[0..count) in
+ *       place over all ranks (MPI, gloo, ...) and returns 0.  d_buf is
+ *       produced by work queued on `stream` (the context's): fn orders its
+ *       reduction after it (enqueues on `stream`, or synchronises it first),
+ *       and the sum is complete when fn returns or is queued on `stream`;
+ *   (2) RCCL communicators (rmsf_multi_init / rmsf_multi_init_all);
+ *   (3) neither: the n contexts of this process are reduced among themselves
+ *       on the host, in context order (one process, any devices).          */
+typedef int (*rmsf_allreduce_fn)(double *d_buf, int64_t count, void *stream,
+                                 void *user);
+int rmsf_ctx_allreduce_sum(rmsf_ctx *ctx, rmsf_allreduce_fn fn, void *user);
+int rmsf_ctx_chan_merge(rmsf_ctx *ctx, rmsf_allreduce_fn fn, void *user);
+
+/* RCCL (librccl.so.1, loaded on first use).  One process per GPU:
+ * rank 0 calls rmsf_multi_unique_id, the host broadcasts the 128 bytes, each
+ * rank calls rmsf_multi_init.  One process, many GPUs: rmsf_multi_init_all
+ * (ncclCommInitAll over the contexts' devices).                              */
+#define RMSF_UNIQUE_ID_BYTES 128
+int rmsf_multi_unique_id(void *id_out);
+int rmsf_multi_init(rmsf_ctx *ctx, const void *id, int nranks, int rank);
+int rmsf_multi_init_all(rmsf_ctx **ctxs, int n);
+int rmsf_multi_allreduce_sum(rmsf_ctx **ctxs, int n);
+int rmsf_multi_chan_merge(rmsf_ctx **ctxs, int n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,753 @@
+// context.cpp -- the RMSF context (rmsf_ctx_*, rmsf_push_*, rmsf_get_*,
+// rmsf_multi_*): RMSF.py's whole per-rank loop (RMSF.py:80-146) behind one
+// opaque handle, for hosts that bring neither torch nor a device allocator.
+//
+// Host-side orchestration only -- every device step is one of the kernel
+// entry points of rmsf_kernels.hip (reference setup, superpose, accumulate,
+// Chan merge, ...), the stager of stager.cpp, or an RCCL all-reduce.
+//
+// State on the context's device:
+//   sel[n_sel] int32 (NULL = contiguous), masses[n_sel] f64 (NULL = uniform)
+//   ref[3 n_sel] + refinfo[RMSF_REFINFO_DOUBLES]      centred reference
+//   wel: parts [1+S][3 n_sel] x2 (slot 0 = running mean / M2, 1..S = the
+//        current chunk's split partials), n               (RMSF.py:120-138)
+//   sum: parts [1+S][3 n_sel] (slot 0 = running sum), n   (RMSF.py:89-105)
+//   xform[chunk][16] + superpose workspace, exchange buffers, rmsf[n_sel]
+#include <hip/hip_runtime.h>
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <type_traits>
+#include <string>
+#include <vector>
+
+#include "rmsf_hip.h"
+
+#define RMSF_EXPORT __attribute__((visibility("default")))
+
+extern "C" int rmsf_internal_set_error(int code, const char *msg);
+
+namespace {
+
+int fail(int code, const std::string &m) { return rmsf_internal_set_error(code, m.c_str()); }
+
+#define CX_HIP(expr)                                                                                \
+  do {                                                                                              \
+    hipError_t e_ = (expr);                                                                         \
+    if (e_ != hipSuccess) return fail(RMSF_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define CX_OK(expr)              \
+  do {                           \
+    int rc_ = (expr);            \
+    if (rc_ != RMSF_OK) return rc_; \
+  } while (0)
+
+constexpr int64_t kChunkFrames = 16384;         // frames per superpose/accumulate launch group
+constexpr int64_t kStageBytes = 64ll << 20;     // default pinned slot size
+
+// ---- RCCL, resolved at first use (the library torch already loaded, if any,
+// shares the soname and is reused) -------------------------------------------
+struct Rccl {
+  ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommInitAll)(ncclComm_t *, int, const int *) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                            hipStream_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  const char *(*GetErrorString)(ncclResult_t) = nullptr;
+  bool ok = false;
+  std::string why;
+};
+
+const Rccl &rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      r.why = std::string("cannot load librccl.so.1: ") + dlerror();
+      return;
+    }
+    bool all = true;
+    auto sym = [&](auto &fp, const char *name) {
+      fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+      if (!fp) all = false;
+    };
+    sym(r.GetUniqueId, "ncclGetUniqueId");
+    sym(r.CommInitRank, "ncclCommInitRank");
+    sym(r.CommInitAll, "ncclCommInitAll");
+    sym(r.CommDestroy, "ncclCommDestroy");
+    sym(r.AllReduce, "ncclAllReduce");
+    sym(r.GroupStart, "ncclGroupStart");
+    sym(r.GroupEnd, "ncclGroupEnd");
+    sym(r.GetErrorString, "ncclGetErrorString");
+    r.ok = all;
+    if (!all) r.why = "librccl.so.1 lacks a required symbol";
+  });
+  return r;
+}
+
+int nccl_fail(const char *what, ncclResult_t e) {
+  const Rccl &r = rccl();
+  return fail(RMSF_EHIP, std::string(what) + ": " + (r.GetErrorString ? r.GetErrorString(e) : "rccl error"));
+}
+
+// Make `dev` current for a scope, restoring the caller's device.
+struct DeviceScope {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceScope(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) err = hipSetDevice(dev);
+  }
+  ~DeviceScope() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  // grow to >= need bytes; work queued on `s` may still use the old buffer,
+  // so it is drained first (keep: the old contents are carried over)
+  int ensure(size_t need, hipStream_t s, bool keep = false) {
+    if (need <= bytes) return RMSF_OK;
+    if (p) {
+      hipError_t e0 = hipStreamSynchronize(s);
+      if (e0 != hipSuccess) return fail(RMSF_EHIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(e0));
+    }
+    void *q = nullptr;
+    hipError_t e = hipMalloc(&q, need);
+    if (e != hipSuccess) return fail(RMSF_ENOMEM, std::string("hipMalloc(") + std::to_string(need) + "): " + hipGetErrorString(e));
+    if (keep && p && bytes) (void)hipMemcpy(q, p, bytes, hipMemcpyDeviceToDevice);
+    if (p) (void)hipFree(p);
+    p = q;
+    bytes = need;
+    return RMSF_OK;
+  }
+  double *d() const { return static_cast<double *>(p); }
+};
+
+// Running partial over pushed chunks: slot 0 of parts0/parts1 is the result.
+struct Running {
+  DevBuf parts0, parts1;
+  int slots = 0;  // split slots available after slot 0
+  int64_t n = 0;
+};
+
+}  // namespace
+
+struct rmsf_ctx {
+  int dev = 0;
+  int64_t n_atoms = 0, n_sel = 0, n_coord = 0;
+  std::vector<int32_t> h_sel;  // empty = contiguous
+  bool has_masses = false;
+  std::vector<double> h_masses;
+  hipStream_t stream = nullptr;
+  DevBuf sel, masses, ref, refinfo, xform, work, frame, avg, rmsf, xa, xb, cnt;
+  bool ref_set = false;
+  Running wel, sum;
+  rmsf_stager *stager = nullptr;
+  int64_t stage_batch = 0;  // 0 = auto
+  int stage_slots = 2, stage_threads = 4;
+  bool stager_dirty = true;
+  ncclComm_t comm = nullptr;
+
+  const int32_t *d_sel() const { return h_sel.empty() ? nullptr : static_cast<const int32_t *>(sel.p); }
+  const double *d_masses() const { return has_masses ? masses.d() : nullptr; }
+};
+
+namespace {
+
+int check_ctx(const rmsf_ctx *c, const char *fn) {
+  if (!c) return fail(RMSF_EINVAL, std::string(fn) + ": null context");
+  return RMSF_OK;
+}
+
+int zero_running(rmsf_ctx *c, Running &r, bool two) {
+  const size_t row = sizeof(double) * c->n_coord;
+  CX_OK(r.parts0.ensure(row, c->stream, true));
+  CX_HIP(hipMemsetAsync(r.parts0.p, 0, row, c->stream));
+  if (two) {
+    CX_OK(r.parts1.ensure(row, c->stream, true));
+    CX_HIP(hipMemsetAsync(r.parts1.p, 0, row, c->stream));
+  }
+  r.n = 0;
+  return RMSF_OK;
+}
+
+// grow the split slots of a running partial to >= s, keeping slot 0
+int ensure_slots(rmsf_ctx *c, Running &r, int s, bool two) {
+  if (s <= r.slots) return RMSF_OK;
+  const size_t need = sizeof(double) * c->n_coord * (size_t)(1 + s);
+  CX_OK(r.parts0.ensure(need, c->stream, true));
+  if (two) CX_OK(r.parts1.ensure(need, c->stream, true));
+  r.slots = s;
+  return RMSF_OK;
+}
+
+// one launch group over n_frames device frames: [superpose] + accumulate + fold
+int process(rmsf_ctx *c, const float *d_xyz, int64_t stride, int64_t n_frames, const int32_t *d_sel, int mode) {
+  const bool aligned = mode == RMSF_PUSH_ALIGN_SUM || mode == RMSF_PUSH_ALIGN_WELFORD;
+  const bool welford = mode == RMSF_PUSH_WELFORD || mode == RMSF_PUSH_ALIGN_WELFORD;
+  const double *xf = nullptr;
+  if (aligned) {
+    if (!c->ref_set) return fail(RMSF_EINVAL, "rmsf_push: aligned mode before a reference was set");
+    CX_OK(c->xform.ensure(sizeof(double) * RMSF_XFORM_DOUBLES * (size_t)n_frames, c->stream));
+    const size_t wb = rmsf_superpose_workspace_bytes(c->n_sel, n_frames);
+    CX_OK(c->work.ensure(std::max<size_t>(wb, 8), c->stream));
+    CX_OK(rmsf_superpose(d_xyz, stride, n_frames, c->n_sel, d_sel, c->d_masses(), c->ref.d(), c->refinfo.d(),
+                         c->xform.d(), c->work.p, c->work.bytes, c->stream));
+    xf = c->xform.d();
+  }
+  Running &r = welford ? c->wel : c->sum;
+  const int s = rmsf_accumulate_splits(c->n_sel, n_frames, aligned ? 1 : 0);
+  if (s <= 0) return fail(RMSF_EINVAL, "rmsf_push: no split layout for this chunk");
+  CX_OK(ensure_slots(c, r, s, welford));
+  double *p0 = r.parts0.d(), *p1 = welford ? r.parts1.d() : nullptr;
+  CX_OK(rmsf_accumulate(d_xyz, stride, n_frames, c->n_sel, d_sel, xf, aligned ? c->refinfo.d() : nullptr,
+                        welford ? RMSF_MODE_WELFORD : RMSF_MODE_SUM, s, p0 + c->n_coord,
+                        welford ? p1 + c->n_coord : nullptr, c->stream));
+  if (welford) {
+    std::vector<int64_t> counts(1 + s);
+    counts[0] = r.n;
+    for (int i = 0; i < s; ++i) counts[1 + i] = rmsf_split_count(n_frames, s, i);
+    CX_OK(rmsf_chan_merge(p0, p1, counts.data(), 1 + s, c->n_coord, p0, p1, c->stream));
+  } else {
+    CX_OK(rmsf_sum_splits(p0, 1 + s, c->n_coord, p0, c->stream));
+  }
+  r.n += n_frames;
+  return RMSF_OK;
+}
+
+int check_mode(int mode, const char *fn) {
+  if (mode < RMSF_PUSH_WELFORD || mode > RMSF_PUSH_SUM) return fail(RMSF_EINVAL, std::string(fn) + ": bad mode");
+  return RMSF_OK;
+}
+
+int ensure_stager(rmsf_ctx *c) {
+  if (c->stager && !c->stager_dirty) return RMSF_OK;
+  if (c->stager) {
+    CX_OK(rmsf_stager_destroy(c->stager));
+    c->stager = nullptr;
+  }
+  int64_t batch = c->stage_batch;
+  if (batch <= 0) batch = std::max<int64_t>(1, std::min<int64_t>(4096, kStageBytes / (12 * std::max<int64_t>(1, c->n_sel))));
+  CX_OK(rmsf_stager_create(c->n_atoms, c->n_sel, c->h_sel.empty() ? nullptr : c->h_sel.data(), batch, c->stage_slots,
+                           c->stage_threads, &c->stager));
+  c->stage_batch = batch;
+  c->stager_dirty = false;
+  return RMSF_OK;
+}
+
+// ---- cross-rank exchange ----------------------------------------------------
+// reduce(count, bufs): sum bufs[i][0..count) over all ranks, in place, for the
+// n local contexts (each buffer on its context's stream).
+using Reduce = std::function<int(int64_t, double *const *)>;
+
+int count_exchange(rmsf_ctx **cs, int n, const Reduce &red, const std::vector<int64_t> &local, int64_t *total) {
+  std::vector<double *> bufs(n);
+  for (int i = 0; i < n; ++i) {
+    DeviceScope ds(cs[i]->dev);
+    CX_OK(cs[i]->cnt.ensure(sizeof(double), cs[i]->stream));
+    double v = (double)local[i];
+    CX_HIP(hipMemcpyAsync(cs[i]->cnt.p, &v, sizeof(double), hipMemcpyHostToDevice, cs[i]->stream));
+    CX_HIP(hipStreamSynchronize(cs[i]->stream));
+    bufs[i] = cs[i]->cnt.d();
+  }
+  CX_OK(red(1, bufs.data()));
+  double t = 0.0;
+  for (int i = 0; i < n; ++i) {
+    DeviceScope ds(cs[i]->dev);
+    double v = 0.0;
+    CX_HIP(hipMemcpyAsync(&v, cs[i]->cnt.p, sizeof(double), hipMemcpyDeviceToHost, cs[i]->stream));
+    CX_HIP(hipStreamSynchronize(cs[i]->stream));
+    if (i == 0) t = v;
+    else if (v != t) return fail(RMSF_EINVAL, "exchange: ranks disagree on the frame count");
+  }
+  *total = (int64_t)t;
+  return RMSF_OK;
+}
+
+int exchange_sum(rmsf_ctx **cs, int n, const Reduce &red) {
+  std::vector<int64_t> local(n);
+  for (int i = 0; i < n; ++i) {
+    if (cs[i]->sum.parts0.bytes == 0) {
+      DeviceScope ds(cs[i]->dev);
+      CX_OK(zero_running(cs[i], cs[i]->sum, false));
+    }
+    local[i] = cs[i]->sum.n;
+  }
+  int64_t total = 0;
+  CX_OK(count_exchange(cs, n, red, local, &total));
+  std::vector<double *> bufs(n);
+  for (int i = 0; i < n; ++i) bufs[i] = cs[i]->sum.parts0.d();
+  CX_OK(red(cs[0]->n_coord, bufs.data()));
+  for (int i = 0; i < n; ++i) cs[i]->sum.n = total;
+  return RMSF_OK;
+}
+
+int exchange_chan(rmsf_ctx **cs, int n, const Reduce &red) {
+  std::vector<int64_t> local(n);
+  for (int i = 0; i < n; ++i) {
+    if (cs[i]->wel.parts0.bytes == 0) {
+      DeviceScope ds(cs[i]->dev);
+      CX_OK(zero_running(cs[i], cs[i]->wel, true));
+    }
+    local[i] = cs[i]->wel.n;
+  }
+  int64_t total = 0;
+  CX_OK(count_exchange(cs, n, red, local, &total));
+  if (total == 0) return fail(RMSF_EEMPTY, "rmsf chan merge: no frames on any rank (RMSF.py:39 ZeroDivisionError)");
+  const int64_t nc = cs[0]->n_coord;
+  std::vector<double *> a(n), b(n);
+  // step 1: global mean = sum_k (n_k/n) mean_k
+  for (int i = 0; i < n; ++i) {
+    rmsf_ctx *c = cs[i];
+    DeviceScope ds(c->dev);
+    CX_OK(c->xa.ensure(sizeof(double) * nc, c->stream));
+    CX_OK(c->xb.ensure(sizeof(double) * nc, c->stream));
+    CX_OK(rmsf_chan_weight(c->wel.parts0.d(), (double)local[i] / (double)total, nc, c->xa.d(), c->stream));
+    a[i] = c->xa.d();
+    b[i] = c->xb.d();
+  }
+  CX_OK(red(nc, a.data()));
+  // step 2: global M2 = sum_k M2_k + n_k (mean_k - mean)^2
+  for (int i = 0; i < n; ++i) {
+    rmsf_ctx *c = cs[i];
+    DeviceScope ds(c->dev);
+    CX_OK(rmsf_chan_deviation(c->wel.parts0.d(), c->wel.parts1.d(), c->xa.d(), (double)local[i], nc, c->xb.d(),
+                              c->stream));
+  }
+  CX_OK(red(nc, b.data()));
+  for (int i = 0; i < n; ++i) {
+    rmsf_ctx *c = cs[i];
+    DeviceScope ds(c->dev);
+    CX_HIP(hipMemcpyAsync(c->wel.parts0.p, c->xa.p, sizeof(double) * nc, hipMemcpyDeviceToDevice, c->stream));
+    CX_HIP(hipMemcpyAsync(c->wel.parts1.p, c->xb.p, sizeof(double) * nc, hipMemcpyDeviceToDevice, c->stream));
+    c->wel.n = total;
+  }
+  return RMSF_OK;
+}
+
+Reduce callback_reduce(rmsf_ctx *c, rmsf_allreduce_fn fn, void *user) {
+  return [c, fn, user](int64_t count, double *const *bufs) -> int {
+    DeviceScope ds(c->dev);
+    int rc = fn(bufs[0], count, (void *)c->stream, user);
+    if (rc != 0) return fail(RMSF_EINVAL, "allreduce callback returned " + std::to_string(rc));
+    return RMSF_OK;
+  };
+}
+
+Reduce rccl_reduce(rmsf_ctx **cs, int n) {
+  return [cs, n](int64_t count, double *const *bufs) -> int {
+    const Rccl &r = rccl();
+    ncclResult_t e = r.GroupStart();
+    if (e != ncclSuccess) return nccl_fail("ncclGroupStart", e);
+    for (int i = 0; i < n; ++i) {
+      DeviceScope ds(cs[i]->dev);
+      e = r.AllReduce(bufs[i], bufs[i], (size_t)count, ncclFloat64, ncclSum, cs[i]->comm, cs[i]->stream);
+      if (e != ncclSuccess) {
+        (void)r.GroupEnd();
+        return nccl_fail("ncclAllReduce", e);
+      }
+    }
+    e = r.GroupEnd();
+    if (e != ncclSuccess) return nccl_fail("ncclGroupEnd", e);
+    return RMSF_OK;
+  };
+}
+
+// contexts of one process, no communicator: fold on the host in context order
+Reduce local_reduce(rmsf_ctx **cs, int n) {
+  return [cs, n](int64_t count, double *const *bufs) -> int {
+    std::vector<double> acc((size_t)count, 0.0), tmp((size_t)count);
+    for (int i = 0; i < n; ++i) {
+      DeviceScope ds(cs[i]->dev);
+      CX_HIP(hipMemcpyAsync(tmp.data(), bufs[i], sizeof(double) * count, hipMemcpyDeviceToHost, cs[i]->stream));
+      CX_HIP(hipStreamSynchronize(cs[i]->stream));
+      for (int64_t j = 0; j < count; ++j) acc[j] += tmp[j];
+    }
+    for (int i = 0; i < n; ++i) {
+      DeviceScope ds(cs[i]->dev);
+      CX_HIP(hipMemcpyAsync(bufs[i], acc.data(), sizeof(double) * count, hipMemcpyHostToDevice, cs[i]->stream));
+      CX_HIP(hipStreamSynchronize(cs[i]->stream));
+    }
+    return RMSF_OK;
+  };
+}
+
+int multi_reduce(rmsf_ctx **cs, int n, const char *fn, Reduce *out) {
+  if (!cs || n <= 0) return fail(RMSF_EINVAL, std::string(fn) + ": no contexts");
+  int with = 0;
+  for (int i = 0; i < n; ++i) {
+    CX_OK(check_ctx(cs[i], fn));
+    if (cs[i]->n_coord != cs[0]->n_coord) return fail(RMSF_EINVAL, std::string(fn) + ": contexts differ in n_sel");
+    with += cs[i]->comm != nullptr;
+  }
+  if (with == n) {
+    *out = rccl_reduce(cs, n);
+  } else if (with == 0) {
+    *out = local_reduce(cs, n);
+  } else {
+    return fail(RMSF_EINVAL, std::string(fn) + ": some contexts have an RCCL communicator and some do not");
+  }
+  return RMSF_OK;
+}
+
+}  // namespace
+
+// ============================================================================
+extern "C" {
+
+RMSF_EXPORT int rmsf_ctx_create(int device, int64_t n_atoms, int64_t n_sel, const int64_t *h_sel,
+                                const double *h_masses, int flags, rmsf_ctx **out) {
+  if (!out) return fail(RMSF_EINVAL, "rmsf_ctx_create: out is NULL");
+  *out = nullptr;
+  if (flags != 0) return fail(RMSF_EINVAL, "rmsf_ctx_create: flags must be 0");
+  if (n_atoms <= 0 || n_sel <= 0 || n_atoms > (int64_t)INT32_MAX)
+    return fail(RMSF_EINVAL, "rmsf_ctx_create: n_atoms/n_sel must be positive (n_atoms < 2^31)");
+  if (!h_sel && n_sel > n_atoms) return fail(RMSF_EINVAL, "rmsf_ctx_create: n_sel > n_atoms without a selection");
+  int nd = 0;
+  CX_HIP(hipGetDeviceCount(&nd));
+  if (device < 0 || device >= nd) return fail(RMSF_EINVAL, "rmsf_ctx_create: no such device");
+  rmsf_ctx *c = new (std::nothrow) rmsf_ctx;
+  if (!c) return fail(RMSF_ENOMEM, "rmsf_ctx_create: out of host memory");
+  c->dev = device;
+  c->n_atoms = n_atoms;
+  c->n_sel = n_sel;
+  c->n_coord = 3 * n_sel;
+  auto bail = [&](int rc) {
+    rmsf_ctx_destroy(c);
+    return rc;
+  };
+  if (h_sel) {
+    c->h_sel.resize(n_sel);
+    bool identity = true;
+    for (int64_t i = 0; i < n_sel; ++i) {
+      if (h_sel[i] < 0 || h_sel[i] >= n_atoms)
+        return bail(fail(RMSF_EINVAL, "rmsf_ctx_create: selection index " + std::to_string(h_sel[i]) + " out of range"));
+      c->h_sel[i] = (int32_t)h_sel[i];
+      identity = identity && h_sel[i] == i;
+    }
+    if (identity) c->h_sel.clear();  // atoms 0..n_sel-1: the contiguous path
+  }
+  DeviceScope ds(device);
+  if (ds.err != hipSuccess) return bail(fail(RMSF_EHIP, "rmsf_ctx_create: hipSetDevice failed"));
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail(RMSF_EHIP, "rmsf_ctx_create: hipStreamCreate failed"));
+  int rc;
+  if (!c->h_sel.empty()) {
+    if ((rc = c->sel.ensure(sizeof(int32_t) * n_sel, c->stream)) != RMSF_OK) return bail(rc);
+    if (hipMemcpy(c->sel.p, c->h_sel.data(), sizeof(int32_t) * n_sel, hipMemcpyHostToDevice) != hipSuccess)
+      return bail(fail(RMSF_EHIP, "rmsf_ctx_create: selection upload failed"));
+  }
+  if (h_masses) {
+    c->has_masses = true;
+    c->h_masses.assign(h_masses, h_masses + n_sel);
+    if ((rc = c->masses.ensure(sizeof(double) * n_sel, c->stream)) != RMSF_OK) return bail(rc);
+    if (hipMemcpy(c->masses.p, h_masses, sizeof(double) * n_sel, hipMemcpyHostToDevice) != hipSuccess)
+      return bail(fail(RMSF_EHIP, "rmsf_ctx_create: masses upload failed"));
+  }
+  if ((rc = c->ref.ensure(sizeof(double) * c->n_coord, c->stream)) != RMSF_OK) return bail(rc);
+  if ((rc = c->refinfo.ensure(sizeof(double) * RMSF_REFINFO_DOUBLES, c->stream)) != RMSF_OK) return bail(rc);
+  if ((rc = zero_running(c, c->wel, true)) != RMSF_OK) return bail(rc);
+  if ((rc = zero_running(c, c->sum, false)) != RMSF_OK) return bail(rc);
+  *out = c;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_ctx_destroy(rmsf_ctx *c) {
+  if (!c) return RMSF_OK;
+  {
+    DeviceScope ds(c->dev);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->stager) rmsf_stager_destroy(c->stager);
+    if (c->comm && rccl().ok) rccl().CommDestroy(c->comm);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;  // DevBufs free on the context's device
+  }
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_ctx_stream(rmsf_ctx *c, void **stream) {
+  CX_OK(check_ctx(c, "rmsf_ctx_stream"));
+  if (!stream) return fail(RMSF_EINVAL, "rmsf_ctx_stream: stream is NULL");
+  *stream = (void *)c->stream;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_ctx_synchronize(rmsf_ctx *c) {
+  CX_OK(check_ctx(c, "rmsf_ctx_synchronize"));
+  DeviceScope ds(c->dev);
+  CX_HIP(hipStreamSynchronize(c->stream));
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_ctx_set_staging(rmsf_ctx *c, int64_t batch_frames, int n_slots, int n_threads) {
+  CX_OK(check_ctx(c, "rmsf_ctx_set_staging"));
+  if (n_slots < 1 || n_threads < 0) return fail(RMSF_EINVAL, "rmsf_ctx_set_staging: n_slots >= 1, n_threads >= 0");
+  c->stage_batch = batch_frames > 0 ? batch_frames : 0;
+  c->stage_slots = n_slots;
+  c->stage_threads = n_threads;
+  c->stager_dirty = true;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_ctx_reset(rmsf_ctx *c, int what) {
+  CX_OK(check_ctx(c, "rmsf_ctx_reset"));
+  DeviceScope ds(c->dev);
+  if (what & 1) CX_OK(zero_running(c, c->wel, true));
+  if (what & 2) CX_OK(zero_running(c, c->sum, false));
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_set_reference(rmsf_ctx *c, const double *h_ref, const double *h_com) {
+  CX_OK(check_ctx(c, "rmsf_set_reference"));
+  if (!h_ref || !h_com) return fail(RMSF_EINVAL, "rmsf_set_reference: NULL reference");
+  // the record rmsf_reference_setup() would write (RMSF.py:84-86)
+  double info[16] = {0};
+  info[0] = h_com[0];
+  info[1] = h_com[1];
+  info[2] = h_com[2];
+  for (int64_t a = 0; a < c->n_sel; ++a) {
+    const double *r = h_ref + 3 * a;
+    info[3] += r[0];
+    info[4] += r[1];
+    info[5] += r[2];
+    info[6] += r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+    info[7] += c->has_masses ? c->h_masses[a] : 1.0;
+  }
+  info[8] = (double)c->n_sel;
+  DeviceScope ds(c->dev);
+  CX_HIP(hipMemcpyAsync(c->ref.p, h_ref, sizeof(double) * c->n_coord, hipMemcpyHostToDevice, c->stream));
+  CX_HIP(hipMemcpyAsync(c->refinfo.p, info, sizeof(info), hipMemcpyHostToDevice, c->stream));
+  CX_HIP(hipStreamSynchronize(c->stream));  // the host sources are the caller's / on this stack
+  c->ref_set = true;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_set_reference_frame(rmsf_ctx *c, const float *xyz, int is_device_ptr) {
+  CX_OK(check_ctx(c, "rmsf_set_reference_frame"));
+  if (!xyz) return fail(RMSF_EINVAL, "rmsf_set_reference_frame: NULL frame");
+  DeviceScope ds(c->dev);
+  const float *d = xyz;
+  if (!is_device_ptr) {
+    const size_t bytes = sizeof(float) * 3 * (size_t)c->n_atoms;
+    CX_OK(c->frame.ensure(bytes, c->stream));
+    CX_HIP(hipMemcpyAsync(c->frame.p, xyz, bytes, hipMemcpyHostToDevice, c->stream));
+    CX_HIP(hipStreamSynchronize(c->stream));
+    d = static_cast<const float *>(c->frame.p);
+  }
+  CX_OK(rmsf_reference_setup(d, nullptr, c->n_sel, c->d_sel(), c->d_masses(), c->ref.d(), c->refinfo.d(), c->stream));
+  c->ref_set = true;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_set_reference_average(rmsf_ctx *c) {
+  CX_OK(check_ctx(c, "rmsf_set_reference_average"));
+  if (c->sum.n <= 0) return fail(RMSF_EEMPTY, "rmsf_set_reference_average: no frames summed (RMSF.py:111)");
+  DeviceScope ds(c->dev);
+  CX_OK(c->avg.ensure(sizeof(double) * c->n_coord, c->stream));
+  CX_OK(rmsf_divide(c->sum.parts0.d(), (double)c->sum.n, c->n_coord, c->avg.d(), c->stream));
+  CX_OK(rmsf_reference_setup(nullptr, c->avg.d(), c->n_sel, nullptr, c->d_masses(), c->ref.d(), c->refinfo.d(),
+                             c->stream));
+  c->ref_set = true;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_push_frames(rmsf_ctx *c, const float *xyz, int64_t n_frames, int64_t stride, int mode,
+                                 int is_device_ptr) {
+  CX_OK(check_ctx(c, "rmsf_push_frames"));
+  CX_OK(check_mode(mode, "rmsf_push_frames"));
+  if (n_frames < 0) return fail(RMSF_EINVAL, "rmsf_push_frames: n_frames < 0");
+  if (n_frames == 0) return RMSF_OK;
+  if (!xyz) return fail(RMSF_EINVAL, "rmsf_push_frames: NULL frames");
+  if (stride == 0) stride = 3 * c->n_atoms;
+  if (stride < 3 * c->n_atoms) return fail(RMSF_EINVAL, "rmsf_push_frames: frame_stride < 3*n_atoms");
+  DeviceScope ds(c->dev);
+  if (ds.err != hipSuccess) return fail(RMSF_EHIP, "rmsf_push_frames: hipSetDevice failed");
+  if (is_device_ptr) {
+    for (int64_t f = 0; f < n_frames; f += kChunkFrames) {
+      const int64_t nf = std::min(kChunkFrames, n_frames - f);
+      CX_OK(process(c, xyz + f * stride, stride, nf, c->d_sel(), mode));
+    }
+    return RMSF_OK;
+  }
+  CX_OK(ensure_stager(c));
+  for (int64_t f = 0; f < n_frames; f += c->stage_batch) {
+    const int64_t nf = std::min(c->stage_batch, n_frames - f);
+    int slot = -1;
+    float *d = nullptr;
+    CX_OK(rmsf_stager_stage(c->stager, xyz + f * stride, stride, nf, c->stream, &slot, &d));
+    int rc = process(c, d, 3 * c->n_sel, nf, nullptr, mode);
+    int rc2 = rmsf_stager_release(c->stager, slot, c->stream);
+    CX_OK(rc);
+    CX_OK(rc2);
+  }
+  // the host buffer is free once the gathers returned; copies run from pinned slots
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_push_xtc(rmsf_ctx *c, const rmsf_xtc *x, int64_t f0, int64_t n_frames, int64_t step, int mode) {
+  CX_OK(check_ctx(c, "rmsf_push_xtc"));
+  CX_OK(check_mode(mode, "rmsf_push_xtc"));
+  if (!x || n_frames < 0 || step < 1 || f0 < 0) return fail(RMSF_EINVAL, "rmsf_push_xtc: bad arguments");
+  if (n_frames == 0) return RMSF_OK;
+  DeviceScope ds(c->dev);
+  CX_OK(ensure_stager(c));
+  for (int64_t i = 0; i < n_frames; i += c->stage_batch) {
+    const int64_t nf = std::min(c->stage_batch, n_frames - i);
+    int slot = -1;
+    float *d = nullptr;
+    CX_OK(rmsf_stager_stage_xtc(c->stager, x, f0 + i * step, nf, step, c->stream, &slot, &d));
+    int rc = process(c, d, 3 * c->n_sel, nf, nullptr, mode);
+    int rc2 = rmsf_stager_release(c->stager, slot, c->stream);
+    CX_OK(rc);
+    CX_OK(rc2);
+  }
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_get_partial(rmsf_ctx *c, int64_t *n, double *h_mean, double *h_m2) {
+  CX_OK(check_ctx(c, "rmsf_get_partial"));
+  DeviceScope ds(c->dev);
+  const size_t row = sizeof(double) * c->n_coord;
+  if (h_mean) CX_HIP(hipMemcpyAsync(h_mean, c->wel.parts0.p, row, hipMemcpyDeviceToHost, c->stream));
+  if (h_m2) CX_HIP(hipMemcpyAsync(h_m2, c->wel.parts1.p, row, hipMemcpyDeviceToHost, c->stream));
+  CX_HIP(hipStreamSynchronize(c->stream));
+  if (n) *n = c->wel.n;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_get_sum(rmsf_ctx *c, int64_t *n, double *h_sum) {
+  CX_OK(check_ctx(c, "rmsf_get_sum"));
+  DeviceScope ds(c->dev);
+  if (h_sum)
+    CX_HIP(hipMemcpyAsync(h_sum, c->sum.parts0.p, sizeof(double) * c->n_coord, hipMemcpyDeviceToHost, c->stream));
+  CX_HIP(hipStreamSynchronize(c->stream));
+  if (n) *n = c->sum.n;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_get_average(rmsf_ctx *c, double *h_avg) {
+  CX_OK(check_ctx(c, "rmsf_get_average"));
+  if (!h_avg) return fail(RMSF_EINVAL, "rmsf_get_average: NULL output");
+  if (c->sum.n <= 0) return fail(RMSF_EEMPTY, "rmsf_get_average: no frames summed");
+  DeviceScope ds(c->dev);
+  CX_OK(c->avg.ensure(sizeof(double) * c->n_coord, c->stream));
+  CX_OK(rmsf_divide(c->sum.parts0.d(), (double)c->sum.n, c->n_coord, c->avg.d(), c->stream));
+  CX_HIP(hipMemcpyAsync(h_avg, c->avg.p, sizeof(double) * c->n_coord, hipMemcpyDeviceToHost, c->stream));
+  CX_HIP(hipStreamSynchronize(c->stream));
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_get_rmsf(rmsf_ctx *c, double *h_rmsf) {
+  CX_OK(check_ctx(c, "rmsf_get_rmsf"));
+  if (!h_rmsf) return fail(RMSF_EINVAL, "rmsf_get_rmsf: NULL output");
+  if (c->wel.n <= 0) return fail(RMSF_EEMPTY, "rmsf_get_rmsf: no frames accumulated");
+  DeviceScope ds(c->dev);
+  CX_OK(c->rmsf.ensure(sizeof(double) * c->n_sel, c->stream));
+  CX_OK(rmsf_finalize(c->wel.parts1.d(), c->n_sel, c->wel.n, c->rmsf.d(), c->stream));
+  CX_HIP(hipMemcpyAsync(h_rmsf, c->rmsf.p, sizeof(double) * c->n_sel, hipMemcpyDeviceToHost, c->stream));
+  CX_HIP(hipStreamSynchronize(c->stream));
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_set_partial(rmsf_ctx *c, int64_t n, const double *h_mean, const double *h_m2) {
+  CX_OK(check_ctx(c, "rmsf_set_partial"));
+  if (n < 0 || (n > 0 && (!h_mean || !h_m2))) return fail(RMSF_EINVAL, "rmsf_set_partial: bad arguments");
+  DeviceScope ds(c->dev);
+  CX_OK(zero_running(c, c->wel, true));
+  if (n > 0) {
+    const size_t row = sizeof(double) * c->n_coord;
+    CX_HIP(hipMemcpyAsync(c->wel.parts0.p, h_mean, row, hipMemcpyHostToDevice, c->stream));
+    CX_HIP(hipMemcpyAsync(c->wel.parts1.p, h_m2, row, hipMemcpyHostToDevice, c->stream));
+    CX_HIP(hipStreamSynchronize(c->stream));
+  }
+  c->wel.n = n;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_ctx_allreduce_sum(rmsf_ctx *c, rmsf_allreduce_fn fn, void *user) {
+  CX_OK(check_ctx(c, "rmsf_ctx_allreduce_sum"));
+  if (!fn) return fail(RMSF_EINVAL, "rmsf_ctx_allreduce_sum: NULL callback");
+  return exchange_sum(&c, 1, callback_reduce(c, fn, user));
+}
+
+RMSF_EXPORT int rmsf_ctx_chan_merge(rmsf_ctx *c, rmsf_allreduce_fn fn, void *user) {
+  CX_OK(check_ctx(c, "rmsf_ctx_chan_merge"));
+  if (!fn) return fail(RMSF_EINVAL, "rmsf_ctx_chan_merge: NULL callback");
+  return exchange_chan(&c, 1, callback_reduce(c, fn, user));
+}
+
+RMSF_EXPORT int rmsf_multi_unique_id(void *id_out) {
+  if (!id_out) return fail(RMSF_EINVAL, "rmsf_multi_unique_id: NULL output");
+  const Rccl &r = rccl();
+  if (!r.ok) return fail(RMSF_EHIP, r.why);
+  static_assert(sizeof(ncclUniqueId) == RMSF_UNIQUE_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId id;
+  ncclResult_t e = r.GetUniqueId(&id);
+  if (e != ncclSuccess) return nccl_fail("ncclGetUniqueId", e);
+  std::memcpy(id_out, &id, sizeof(id));
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_multi_init(rmsf_ctx *c, const void *id, int nranks, int rank) {
+  CX_OK(check_ctx(c, "rmsf_multi_init"));
+  if (!id || nranks < 1 || rank < 0 || rank >= nranks) return fail(RMSF_EINVAL, "rmsf_multi_init: bad arguments");
+  if (c->comm) return fail(RMSF_EINVAL, "rmsf_multi_init: context already has a communicator");
+  const Rccl &r = rccl();
+  if (!r.ok) return fail(RMSF_EHIP, r.why);
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  DeviceScope ds(c->dev);
+  ncclResult_t e = r.CommInitRank(&c->comm, nranks, uid, rank);
+  if (e != ncclSuccess) {
+    c->comm = nullptr;
+    return nccl_fail("ncclCommInitRank", e);
+  }
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_multi_init_all(rmsf_ctx **cs, int n) {
+  if (!cs || n < 1) return fail(RMSF_EINVAL, "rmsf_multi_init_all: no contexts");
+  std::vector<int> devs(n);
+  for (int i = 0; i < n; ++i) {
+    CX_OK(check_ctx(cs[i], "rmsf_multi_init_all"));
+    if (cs[i]->comm) return fail(RMSF_EINVAL, "rmsf_multi_init_all: a context already has a communicator");
+    devs[i] = cs[i]->dev;
+  }
+  const Rccl &r = rccl();
+  if (!r.ok) return fail(RMSF_EHIP, r.why);
+  std::vector<ncclComm_t> comms(n, nullptr);
+  ncclResult_t e = r.CommInitAll(comms.data(), n, devs.data());
+  if (e != ncclSuccess) return nccl_fail("ncclCommInitAll", e);
+  for (int i = 0; i < n; ++i) cs[i]->comm = comms[i];
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_multi_allreduce_sum(rmsf_ctx **cs, int n) {
+  Reduce red;
+  CX_OK(multi_reduce(cs, n, "rmsf_multi_allreduce_sum", &red));
+  return exchange_sum(cs, n, red);
+}
+
+RMSF_EXPORT int rmsf_multi_chan_merge(rmsf_ctx **cs, int n) {
+  Reduce red;
+  CX_OK(multi_reduce(cs, n, "rmsf_multi_chan_merge", &red));
+  return exchange_chan(cs, n, red);
+}
+
+}  // extern "C"

@@ -78,7 +78,36 @@ SIGNATURES = {
     "rmsf_xtc_frame_info": (c_int, [P, c_int64, POINTER(c_int32), POINTER(ctypes.c_float), P]),
     "rmsf_xtc_read": (c_int, [P, c_int64, c_int64, c_int64, P, c_int64, P, c_int]),
     "rmsf_xtc_write": (c_int, [c_char_p, P, c_int64, c_int64, ctypes.c_float, P, c_int]),
+    # RMSF context (rmsf_ctx_*) and cross-rank exchange
+    "rmsf_ctx_create": (c_int, [c_int, c_int64, c_int64, P, P, c_int, POINTER(c_void_p)]),
+    "rmsf_ctx_destroy": (c_int, [P]),
+    "rmsf_ctx_stream": (c_int, [P, POINTER(c_void_p)]),
+    "rmsf_ctx_synchronize": (c_int, [P]),
+    "rmsf_ctx_set_staging": (c_int, [P, c_int64, c_int, c_int]),
+    "rmsf_ctx_reset": (c_int, [P, c_int]),
+    "rmsf_set_reference": (c_int, [P, P, P]),
+    "rmsf_set_reference_frame": (c_int, [P, P, c_int]),
+    "rmsf_set_reference_average": (c_int, [P]),
+    "rmsf_push_frames": (c_int, [P, P, c_int64, c_int64, c_int, c_int]),
+    "rmsf_push_xtc": (c_int, [P, P, c_int64, c_int64, c_int64, c_int]),
+    "rmsf_get_partial": (c_int, [P, POINTER(c_int64), P, P]),
+    "rmsf_get_sum": (c_int, [P, POINTER(c_int64), P]),
+    "rmsf_get_average": (c_int, [P, P]),
+    "rmsf_get_rmsf": (c_int, [P, P]),
+    "rmsf_set_partial": (c_int, [P, c_int64, P, P]),
+    "rmsf_ctx_allreduce_sum": (c_int, [P, P, P]),
+    "rmsf_ctx_chan_merge": (c_int, [P, P, P]),
+    "rmsf_multi_unique_id": (c_int, [P]),
+    "rmsf_multi_init": (c_int, [P, P, c_int, c_int]),
+    "rmsf_multi_init_all": (c_int, [P, c_int]),
+    "rmsf_multi_allreduce_sum": (c_int, [P, c_int]),
+    "rmsf_multi_chan_merge": (c_int, [P, c_int]),
 }
+
+# int (*rmsf_allreduce_fn)(double *d_buf, int64_t count, void *stream, void *user)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int64, c_void_p, c_void_p)
+RMSF_PUSH_WELFORD, RMSF_PUSH_ALIGN_SUM, RMSF_PUSH_ALIGN_WELFORD, RMSF_PUSH_SUM = 0, 1, 2, 3
+RMSF_UNIQUE_ID_BYTES = 128
 
 _lib = None
 

@@ -1,0 +1,255 @@
+"""``Context`` -- the C ABI's RMSF context (rmsf_ctx_*) from Python.
+
+The context API is the torch-free boundary of include/rmsf_hip.h: one opaque
+handle per device owning the selection, reference, running Welford / sweep-1
+sum partials, a pinned stager and a stream.  RMSF.py's per-rank loop
+(RMSF.py:80-146) in these terms::
+
+    c = Context(n_atoms, sel=ca.indices, masses=None, device=0)
+    c.set_reference_frame(frame0)                      # RMSF.py:80-87
+    c.push(block, PUSH_ALIGN_SUM)                      # RMSF.py:89-105
+    c.allreduce_sum()                                  # RMSF.py:107-110
+    c.set_reference_average()                          # RMSF.py:111-118
+    c.push(block, PUSH_ALIGN_WELFORD)                  # RMSF.py:120-138
+    c.chan_merge()                                     # RMSF.py:140-143
+    rmsf = c.rmsf()                                    # RMSF.py:145-146
+
+Frames are numpy float32 [n, n_atoms, 3] (host: gathered and streamed by the
+stager) or HIP torch tensors (device: read in place).  Exchanges run over a
+torch.distributed process group when one is initialised with world > 1
+(through the C callback transport), otherwise over the contexts of this
+process (``Context.multi_*``: RCCL when ``init_rccl``/``init_all`` gave them
+communicators, else an in-process host fold).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._lib import (ALLREDUCE_FN, RMSF_PUSH_ALIGN_SUM, RMSF_PUSH_ALIGN_WELFORD, RMSF_PUSH_SUM, RMSF_PUSH_WELFORD,
+                   RMSF_UNIQUE_ID_BYTES, call, load)
+
+PUSH_WELFORD = RMSF_PUSH_WELFORD
+PUSH_ALIGN_SUM = RMSF_PUSH_ALIGN_SUM
+PUSH_ALIGN_WELFORD = RMSF_PUSH_ALIGN_WELFORD
+PUSH_SUM = RMSF_PUSH_SUM
+
+
+def _f64(a, n: int, name: str) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    if a.size != n:
+        raise ValueError(f"{name}: expected {n} values, got {a.size}")
+    return a
+
+
+def dist_allreduce(d_buf: int, count: int, stream: int, user) -> int:
+    """rmsf_allreduce_fn over the default torch.distributed group: the
+    device buffer is staged through host memory (a once-per-run exchange of
+    3*n_sel doubles) and summed with dist.all_reduce."""
+    import torch
+    import torch.distributed as dist
+
+    try:
+        host = np.empty(count, dtype=np.float64)
+        call("rmsf_memcpy_d2h", host.ctypes.data, d_buf, 8 * count, stream)
+        call("rmsf_stream_synchronize", stream)
+        t = torch.from_numpy(host)
+        if dist.get_backend() == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t)
+        host[:] = t.cpu().numpy()
+        call("rmsf_memcpy_h2d", d_buf, host.ctypes.data, 8 * count, stream)
+        call("rmsf_stream_synchronize", stream)
+        return 0
+    except Exception:  # noqa: BLE001 -- no exception may cross the C callback
+        return 1
+
+
+_DIST_FN = ALLREDUCE_FN(lambda b, n, s, u: dist_allreduce(b, n, s, u))
+
+
+def _dist_world() -> int:
+    try:
+        import torch.distributed as dist
+        return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    except Exception:  # noqa: BLE001
+        return 1
+
+
+class Context:
+    def __init__(self, n_atoms: int, sel=None, masses=None, device: int = 0, n_sel: int | None = None):
+        load()
+        self.n_atoms = int(n_atoms)
+        self._sel = None if sel is None else np.ascontiguousarray(sel, dtype=np.int64)
+        self.n_sel = len(self._sel) if self._sel is not None else int(n_sel if n_sel is not None else n_atoms)
+        m = None if masses is None else _f64(masses, self.n_sel, "masses")
+        self.device = device
+        self._h = ctypes.c_void_p()
+        call("rmsf_ctx_create", device, self.n_atoms, self.n_sel,
+             None if self._sel is None else self._sel.ctypes.data, None if m is None else m.ctypes.data, 0,
+             ctypes.byref(self._h))
+
+    # -- lifecycle ------------------------------------------------------------
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    @property
+    def stream(self) -> int:
+        s = ctypes.c_void_p()
+        call("rmsf_ctx_stream", self._h, ctypes.byref(s))
+        return s.value or 0
+
+    def close(self) -> None:
+        if self._h:
+            call("rmsf_ctx_destroy", self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def synchronize(self) -> None:
+        call("rmsf_ctx_synchronize", self._h)
+
+    def set_staging(self, batch_frames: int = 0, n_slots: int = 2, n_threads: int = 4) -> None:
+        call("rmsf_ctx_set_staging", self._h, batch_frames, n_slots, n_threads)
+
+    def reset(self, welford: bool = True, sum: bool = True) -> None:  # noqa: A002
+        call("rmsf_ctx_reset", self._h, (1 if welford else 0) | (2 if sum else 0))
+
+    # -- reference ------------------------------------------------------------
+    def set_reference(self, ref_centered, ref_com) -> None:
+        r = _f64(ref_centered, 3 * self.n_sel, "ref_centered")
+        c = _f64(ref_com, 3, "ref_com")
+        call("rmsf_set_reference", self._h, r.ctypes.data, c.ctypes.data)
+
+    def set_reference_frame(self, frame) -> None:
+        ptr, dev, keep = self._frames_ptr(frame, 1)
+        call("rmsf_set_reference_frame", self._h, ptr, dev)
+        del keep
+
+    def set_reference_average(self) -> None:
+        call("rmsf_set_reference_average", self._h)
+
+    # -- frames ---------------------------------------------------------------
+    def _frames_ptr(self, frames, expect_frames: int | None = None):
+        """(pointer, is_device, keep-alive) for numpy host or HIP torch frames."""
+        if hasattr(frames, "is_cuda") and frames.is_cuda:
+            import torch
+            if frames.dtype != torch.float32 or not frames.is_contiguous():
+                raise ValueError("device frames must be contiguous float32")
+            if frames.numel() % (3 * self.n_atoms):
+                raise ValueError(f"device frames: not a whole number of {self.n_atoms}-atom frames")
+            return frames.data_ptr(), 1, frames
+        a = np.ascontiguousarray(frames, dtype=np.float32)
+        if a.size % (3 * self.n_atoms):
+            raise ValueError(f"host frames: not a whole number of {self.n_atoms}-atom frames")
+        return a.ctypes.data, 0, a
+
+    def push(self, frames, mode: int = PUSH_WELFORD, step: int = 1) -> None:
+        """Push frames [n, n_atoms, 3] (every ``step``-th one)."""
+        ptr, dev, keep = self._frames_ptr(frames)
+        n_all = keep.numel() if dev else keep.size
+        n_all //= 3 * self.n_atoms
+        n = len(range(0, n_all, step))
+        call("rmsf_push_frames", self._h, ptr, n, 3 * self.n_atoms * step, mode, dev)
+        if dev:
+            # device frames are read asynchronously: the caller's tensor must
+            # outlive the queued work
+            self.synchronize()
+        del keep
+
+    def push_xtc(self, xtc, start: int = 0, stop: int | None = None, step: int = 1, mode: int = PUSH_WELFORD):
+        stop = xtc.n_frames if stop is None else min(stop, xtc.n_frames)
+        n = len(range(start, stop, step))
+        call("rmsf_push_xtc", self._h, xtc.handle, start, n, step, mode)
+
+    # -- results --------------------------------------------------------------
+    def partial(self):
+        n = ctypes.c_int64()
+        mean = np.empty((self.n_sel, 3))
+        m2 = np.empty((self.n_sel, 3))
+        call("rmsf_get_partial", self._h, ctypes.byref(n), mean.ctypes.data, m2.ctypes.data)
+        return n.value, mean, m2
+
+    def sum(self):
+        n = ctypes.c_int64()
+        s = np.empty((self.n_sel, 3))
+        call("rmsf_get_sum", self._h, ctypes.byref(n), s.ctypes.data)
+        return n.value, s
+
+    def average(self) -> np.ndarray:
+        out = np.empty((self.n_sel, 3))
+        call("rmsf_get_average", self._h, out.ctypes.data)
+        return out
+
+    def rmsf(self) -> np.ndarray:
+        out = np.empty(self.n_sel)
+        call("rmsf_get_rmsf", self._h, out.ctypes.data)
+        return out
+
+    def set_partial(self, n: int, mean, m2) -> None:
+        a = _f64(mean, 3 * self.n_sel, "mean")
+        b = _f64(m2, 3 * self.n_sel, "m2")
+        call("rmsf_set_partial", self._h, n, a.ctypes.data, b.ctypes.data)
+
+    # -- exchange -------------------------------------------------------------
+    def allreduce_sum(self, fn=None) -> None:
+        """Sweep-1 sum + count over ranks (RMSF.py:107-110).  ``fn``: a ctypes
+        ALLREDUCE_FN; default: torch.distributed when world > 1, else a no-op
+        fold of this one context."""
+        if fn is None and _dist_world() > 1:
+            fn = _DIST_FN
+        if fn is None:
+            Context.multi_allreduce_sum([self])
+        else:
+            call("rmsf_ctx_allreduce_sum", self._h, ctypes.cast(fn, ctypes.c_void_p), None)
+
+    def chan_merge(self, fn=None) -> None:
+        """Exact k-way Chan merge over ranks (RMSF.py:140-143)."""
+        if fn is None and _dist_world() > 1:
+            fn = _DIST_FN
+        if fn is None:
+            Context.multi_chan_merge([self])
+        else:
+            call("rmsf_ctx_chan_merge", self._h, ctypes.cast(fn, ctypes.c_void_p), None)
+
+    # -- RCCL / in-process groups ---------------------------------------------
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(RMSF_UNIQUE_ID_BYTES)
+        call("rmsf_multi_unique_id", buf)
+        return buf.raw
+
+    def init_rccl(self, uid: bytes, nranks: int, rank: int) -> None:
+        if len(uid) != RMSF_UNIQUE_ID_BYTES:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        buf = ctypes.create_string_buffer(uid, RMSF_UNIQUE_ID_BYTES)
+        call("rmsf_multi_init", self._h, buf, nranks, rank)
+
+    @staticmethod
+    def _handles(ctxs):
+        arr = (ctypes.c_void_p * len(ctxs))(*[c.handle.value for c in ctxs])
+        return arr, len(ctxs)
+
+    @staticmethod
+    def init_all(ctxs) -> None:
+        call("rmsf_multi_init_all", *Context._handles(ctxs))
+
+    @staticmethod
+    def multi_allreduce_sum(ctxs) -> None:
+        call("rmsf_multi_allreduce_sum", *Context._handles(ctxs))
+
+    @staticmethod
+    def multi_chan_merge(ctxs) -> None:
+        call("rmsf_multi_chan_merge", *Context._handles(ctxs))

@@ -79,3 +79,21 @@ def test_product_fails_loudly_without_gpu():
     from rmsf_amd.engine import Engine
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         Engine()
+
+
+def test_context_create_fails_cleanly_without_gpu():
+    """rmsf_ctx_create reports (does not crash, does not fall back) when no
+    device is visible; argument checks come first."""
+    import torch
+    from rmsf_amd import _lib
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    assert lib.rmsf_ctx_create(0, 10, 10, None, None, 1, ctypes.byref(h)) == _lib.RMSF_EINVAL
+    assert b"flags" in lib.rmsf_last_error()
+    assert lib.rmsf_ctx_create(0, 10, 11, None, None, 0, ctypes.byref(h)) == _lib.RMSF_EINVAL
+    assert lib.rmsf_ctx_destroy(None) == _lib.RMSF_OK
+    assert lib.rmsf_get_rmsf(None, None) == _lib.RMSF_EINVAL
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    rc = lib.rmsf_ctx_create(0, 10, 10, None, None, 0, ctypes.byref(h))
+    assert rc < 0 and not h.value
