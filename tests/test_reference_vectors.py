@@ -1,0 +1,103 @@
+"""Parity against vectors produced by executing the reference's own statements.
+
+``tests/golden/reference_exec.npz`` was written by
+``tests/golden/make_reference_vectors.py``, which runs RMSF.py's own lines
+(36-41 ``second_order_moments``, 43-51 ``get_rotation_matrix``, 66-69 frame
+blocks, 85/95/97/99-103/105/111/118/128/131/133-138/140/146) on seeded
+synthetic frames, with only the absent dependencies supplied from outside
+(frames + selection, the upstream COM formula, the KAT-pinned QCP; see that
+script).  CPU tier: the oracle and the C-ABI host entry points reproduce the
+reference bit for bit.  GPU tier: the HIP path is within the north star's
+1e-6 A of the reference.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import rmsf_oracle as O
+from oracle import synth as SY
+
+TOL = 1e-6  # Angstrom, absolute (north star)
+
+
+@pytest.fixture(scope="module")
+def ref():
+    return np.load(os.path.join(GOLDEN, "reference_exec.npz"))
+
+
+@pytest.fixture(scope="module")
+def traj(ref):
+    return SY.frames(int(ref["seed"]), int(ref["n_atoms"]), 0, int(ref["n_frames"]), ref["motion"])
+
+
+# -- CPU tier ------------------------------------------------------------------
+
+def test_blocks_match_reference_lines_66_69(ref):
+    from rmsf_amd.engine import block_range
+    for n, p, r, s, e in ref["blocks"]:
+        b = O.block_ranges(int(n), int(p))[int(r)]
+        assert (b.start, b.stop) == (s, e)
+        assert block_range(int(n), int(p), int(r)) == (s, e)  # C ABI rmsf_block_range
+
+
+def test_chan_matches_reference_lines_36_41(ref):
+    for i in range(len(ref["chan_n1"])):
+        S1 = (int(ref["chan_n1"][i]), ref["chan_mu1"][i], ref["chan_M1"][i])
+        S2 = (int(ref["chan_n2"][i]), ref["chan_mu2"][i], ref["chan_M2"][i])
+        T, mu, M = O.second_order_moments(S1, S2)
+        assert T == ref["chan_T"][i]
+        np.testing.assert_array_equal(mu, ref["chan_mu"][i])
+        np.testing.assert_array_equal(M, ref["chan_M"][i])
+
+
+@pytest.mark.parametrize("tag", ["ca", "het"])
+@pytest.mark.parametrize("P", [1, 2, 3])
+def test_oracle_bitwise_vs_reference(ref, traj, tag, P):
+    """The numpy restatement (selection rows only) equals the reference's own
+    statements (all atoms transformed) bit for bit."""
+    r = O.rmsf_script(traj, ref["sel"], ref[f"masses_{tag}"], size=P, align="average")
+    np.testing.assert_array_equal(r["rmsf"], ref[f"rmsf_{tag}_P{P}"])
+    if P == 1:
+        np.testing.assert_array_equal(r["mean"], ref[f"mean_{tag}"])
+        np.testing.assert_array_equal(r["m2"], ref[f"m2_{tag}"])
+        np.testing.assert_array_equal(r["average"], ref[f"average_{tag}"])
+
+
+def test_uniform_default_vs_ca_masses(ref, traj):
+    """masses=None (centroid) vs the reference's CA masses: COM rounding moves
+    a few f32 rounding points, far inside the tolerance."""
+    r = O.rmsf_script(traj, ref["sel"], None, size=1, align="average")
+    assert np.abs(r["rmsf"] - ref["rmsf_ca_P1"]).max() < 1e-7
+
+
+# -- GPU tier ------------------------------------------------------------------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", ["ca", "het"])
+@pytest.mark.parametrize("where", ["device", "host"])
+def test_hip_rmsf_vs_reference(ref, traj, tag, where):
+    import torch
+
+    from rmsf_amd import RMSF
+    x = torch.tensor(traj, device="cuda") if where == "device" else traj
+    r = RMSF(x, select=ref["sel"], align="average", masses=ref[f"masses_{tag}"]).run()
+    np.testing.assert_allclose(r.results.rmsf, ref[f"rmsf_{tag}_P1"], rtol=0, atol=TOL)
+    np.testing.assert_allclose(r.results.average, ref[f"average_{tag}"], rtol=0, atol=1e-9)
+    assert r.results.n_frames == int(ref["n_frames"])
+    # default (uniform masses) against the reference's CA masses
+    r = RMSF(x, select=ref["sel"], align="average").run()
+    np.testing.assert_allclose(r.results.rmsf, ref["rmsf_ca_P1"], rtol=0, atol=TOL)
+
+
+@pytest.mark.gpu
+def test_hip_chan_merge_vs_reference(ref):
+    from rmsf_amd import second_order_moments
+    for i in range(len(ref["chan_n1"])):
+        S1 = (int(ref["chan_n1"][i]), ref["chan_mu1"][i], ref["chan_M1"][i])
+        S2 = (int(ref["chan_n2"][i]), ref["chan_mu2"][i], ref["chan_M2"][i])
+        T, mu, M = second_order_moments(S1, S2)
+        assert T == ref["chan_T"][i]
+        np.testing.assert_allclose(mu, ref["chan_mu"][i], rtol=1e-15, atol=0)
+        np.testing.assert_allclose(M, ref["chan_M"][i], rtol=1e-14, atol=0)
