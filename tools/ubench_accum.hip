@@ -123,6 +123,69 @@ __global__ __launch_bounds__(BS) void k_acc(const float *__restrict__ xyz, int64
   o1[o + 2] = q2;
 }
 
+// V0 with a register ring: the loads of frame k+D are issued while frame k
+// is consumed (D frames in flight per lane at all times).  XS: the per-frame
+// transform comes by scalar loads (0) or is staged in LDS in 64-frame chunks (1).
+template <int D, int BS, int XS>
+__global__ __launch_bounds__(BS) void k_acc_pf(const float *__restrict__ xyz, int64_t fstride, int64_t n_sel,
+                                               int64_t nf, int S, const double *__restrict__ xform,
+                                               const double *__restrict__ refinfo, double *__restrict__ o0,
+                                               double *__restrict__ o1) {
+  __shared__ double xl[XS ? 64 * 12 : 1];
+  const int64_t a = (int64_t)blockIdx.x * BS + threadIdx.x;
+  const bool live = a < n_sel;
+  const int64_t ac = live ? a : n_sel - 1;
+  const int s = blockIdx.y;
+  const int64_t fb = nf * s / S;
+  const int n = (int)(nf * (s + 1) / S - fb);
+  const float *p = xyz + fb * fstride + 3 * ac;
+  const double *xf = xform + fb * 16;
+  const double rc0 = refinfo[0], rc1 = refinfo[1], rc2 = refinfo[2];
+  double m0 = 0, m1 = 0, m2 = 0, q0 = 0, q1 = 0, q2 = 0;
+  float bx[D], by[D], bz[D];
+#pragma unroll
+  for (int u = 0; u < D; ++u) {
+    const float *q = p + (int64_t)min(u, n - 1) * fstride;
+    bx[u] = __builtin_nontemporal_load(q);
+    by[u] = __builtin_nontemporal_load(q + 1);
+    bz[u] = __builtin_nontemporal_load(q + 2);
+  }
+  for (int k = 0; k < n; k += D) {
+    if (XS && (k & 63) == 0) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < 64 * 12; i += BS) {
+        const int f = k + i / 12;
+        xl[i] = f < n ? xf[(int64_t)f * 16 + i % 12] : 0.0;
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      float x = bx[u], y = by[u], z = bz[u];
+      const float *q = p + (int64_t)min(k + D + u, n - 1) * fstride;
+      bx[u] = __builtin_nontemporal_load(q);
+      by[u] = __builtin_nontemporal_load(q + 1);
+      bz[u] = __builtin_nontemporal_load(q + 2);
+      if (k + u < n) {
+        const double *t = XS ? xl + ((k + u) & 63) * 12 : xf + (int64_t)(k + u) * 16;
+        apply_xform(x, y, z, t, rc0, rc1, rc2);
+        const WCoef c = g_coef.v[k + u];
+        welford(m0, q0, (double)x, c);
+        welford(m1, q1, (double)y, c);
+        welford(m2, q2, (double)z, c);
+      }
+    }
+  }
+  if (!live) return;
+  const int64_t o = (int64_t)s * 3 * n_sel + 3 * a;
+  o0[o] = m0;
+  o0[o + 1] = m1;
+  o0[o + 2] = m2;
+  o1[o] = q0;
+  o1[o + 1] = q1;
+  o1[o + 2] = q2;
+}
+
 
 // V4: 4 atoms per lane from three float4 loads at a 48-B lane stride.
 // V5: three fully coalesced float4 loads per wave-frame (768 floats = 256
@@ -254,16 +317,35 @@ int main() {
     hipLaunchKernelGGL((k_acc4<V, U, BS>), dim3((n / 4 + BS - 1) / BS, S), dim3(BS), 0, 0, x, fs, n, nf, S, xf, ri, \
                        o0, o1);                                                                                     \
   })
+#define PF(D, BS, XS, S)                                                                                    \
+  run("V0 ring D=" #D " BS=" #BS " XS=" #XS, S, [&] {                                                       \
+    hipLaunchKernelGGL((k_acc_pf<D, BS, XS>), dim3((n + BS - 1) / BS, S), dim3(BS), 0, 0, x, fs, n, nf, S, xf, \
+                       ri, o0, o1);                                                                        \
+  })
+  const char *which = getenv("UB_SET");
+  const bool layouts = which && which[0] == 'L';
   for (int rep = 0; rep < 2; ++rep) {
     AC(0, 4, 256, 12);
     AC(1, 4, 256, 12);
-    AC4(4, 2, 256, 12);
-    AC4(4, 2, 256, 48);
-    AC4(4, 1, 256, 48);
-    AC4(5, 2, 256, 12);
-    AC4(5, 2, 256, 48);
-    AC4(5, 1, 256, 48);
-    AC4(5, 2, 128, 48);
+    if (layouts) {
+      AC4(4, 2, 256, 12);
+      AC4(4, 2, 256, 48);
+      AC4(4, 1, 256, 48);
+      AC4(5, 2, 256, 12);
+      AC4(5, 2, 256, 48);
+      AC4(5, 1, 256, 48);
+      AC4(5, 2, 128, 48);
+      continue;
+    }
+    AC(0, 2, 256, 12);
+    AC(0, 8, 256, 12);
+    PF(2, 256, 0, 12);
+    PF(4, 256, 0, 12);
+    PF(4, 256, 0, 24);
+    PF(8, 256, 0, 12);
+    PF(4, 256, 1, 12);
+    PF(8, 256, 1, 12);
+    PF(4, 512, 1, 12);
   }
   return 0;
 }
