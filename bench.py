@@ -49,9 +49,10 @@ WORKLOADS = {
     "c5": dict(n_atoms=250_000, frames_per_gpu=1_000, align=None, host=True,
                name="C5 (pre-decoded): 250k atoms x 1k frames fp32 in host memory, streamed via the pinned "
                     "multi-buffer stager (PCIe-inclusive rate; no XTC decode)"),
-    "c5xtc": dict(n_atoms=250_000, frames_per_gpu=400, align=None, host=True, xtc=True,
-                  name="C5: 250k-atom XTC file (precision 1000) decoded frame-parallel on host threads into "
-                       "the pinned stager and streamed to the GPU (decode + PCIe inclusive)"),
+    "c5xtc": dict(n_atoms=250_000, frames_per_gpu=2048, align=None, host=True, xtc=True,
+                  name="C5: 250k-atom XTC file (precision 1000) streamed from the host and decoded "
+                       "(--xtc-decode gpu: compressed records via pinned slots, decompressed on the GPU; host: "
+                       "decoded on host threads into the pinned stager); read + PCIe + decode inclusive"),
 }
 
 
@@ -71,6 +72,8 @@ def parse():
     ap.add_argument("--mode-steps", type=int, default=3)
     ap.add_argument("--stager-threads", type=int, default=4)
     ap.add_argument("--stager-batch", type=int, default=None, help="c5: frames per staged batch")
+    ap.add_argument("--xtc-decode", choices=["gpu", "host"], default="gpu",
+                    help="c5xtc: decompress the XTC records on the GPU (default) or on host threads")
     ap.add_argument("--align", choices=["none", "frame0", "average"], default=None, help="override the workload's")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo only "
                                                      "to rehearse several ranks on one GPU)")
@@ -213,11 +216,13 @@ def main():
             xtc_dir = tempfile.mkdtemp(prefix="rmsf_c5_")
             xtc_path = os.path.join(xtc_dir, "c5.xtc")
             t_w = time.perf_counter()
-            for f in range(0, n_local, 50):  # untimed: produce the input file
-                write_xtc(xtc_path, host[f:f + 50], append=f > 0)
+            for f in range(0, n_local, 256):  # untimed: produce the input file
+                write_xtc(xtc_path, host[f:f + 256], append=f > 0)
             t_w = time.perf_counter() - t_w
             del host
-            src = XtcSource(xtc_path, None, batch_frames=a.stager_batch, n_threads=a.stager_threads)
+            src = XtcSource(xtc_path, None, batch_frames=a.stager_batch, decode=a.xtc_decode,
+                            n_threads=a.stager_threads if a.xtc_decode == "host" else max(a.stager_threads, 16),
+                            n_slots=4 if a.xtc_decode == "gpu" else 3)
         else:
             src = HostSource(host, None, batch_frames=a.stager_batch, n_threads=a.stager_threads, offset=b0,
                              n_traj=n_total)
@@ -294,7 +299,7 @@ def main():
                          "threads": a.stager_threads, "batch_frames": src.batch_frames,
                          "host_link_spec_gbs": 63.0}
         if wl.get("xtc"):
-            out["stager"].update(xtc_bytes=os.path.getsize(xtc_path), xtc_write_s=t_w,
+            out["stager"].update(xtc_decode=a.xtc_decode, xtc_bytes=os.path.getsize(xtc_path), xtc_write_s=t_w,
                                  xtc_frames_per_s=n_local * a.steps / dt,
                                  xtc_gb_per_s_compressed=os.path.getsize(xtc_path) * a.steps / dt / 1e9)
         out["roofline"]["note"] = "C5 is PCIe/host bound; the kernel roofline above is the device-side launch"

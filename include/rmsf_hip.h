@@ -231,6 +231,48 @@ int rmsf_xtc_read(const rmsf_xtc *x, int64_t f0, int64_t n, int64_t step,
 int rmsf_xtc_write(const char *path, const float *h_xyz, int64_t n_frames,
                    int64_t n_atoms, float precision, const float *h_box9,
                    int append);
+/* Byte offset (a multiple of 4) and length of frame f's XDR record. */
+int rmsf_xtc_frame_record(const rmsf_xtc *x, int64_t frame, int64_t *offset,
+                          int64_t *bytes);
+
+/* ---- XTC decompression on the GPU (config C5) -------------------------------
+ * The same decoder on the device: the compressed frame records (about 1/6
+ * of the decoded bytes) are read into a pinned slot (pread, n_threads host
+ * threads), copied to HBM on the slot's own stream and decompressed there,
+ * one wave per frame (the xdr3dfcoord stream of a frame is sequential;
+ * frames run in parallel), into float32 [n][n_atoms][3] Angstrom frames,
+ * bit-identical to rmsf_xtc_read().  The selection is applied downstream
+ * (rmsf_accumulate / rmsf_superpose gather it in-kernel).  Replaces the
+ * libxdrfile decode behind trajectory[frame] (RMSF.py:92,124).           */
+typedef struct rmsf_xtcdec rmsf_xtcdec;
+int rmsf_xtcdec_create(const rmsf_xtc *x, int64_t batch_frames, int n_slots,
+                       int n_threads, rmsf_xtcdec **out);
+int rmsf_xtcdec_destroy(rmsf_xtcdec *d);
+/* Decode frames f0, f0+step, ... (n_frames <= batch_frames) into the next
+ * slot; *d_frames = its device frames (frame stride 3*n_atoms floats).
+ * consumer_stream waits for the decode.  Per-frame errors (corrupt data:
+ * the frame is filled with NaN) are reported when the slot is next used or
+ * by rmsf_xtcdec_synchronize().                                             */
+int rmsf_xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n_frames,
+                       int64_t step, void *consumer_stream, int *slot,
+                       float **d_frames);
+/* The slot may be reused once the work queued so far on consumer_stream ends. */
+int rmsf_xtcdec_release(rmsf_xtcdec *d, int slot, void *consumer_stream);
+/* Wait for every outstanding decode; first per-frame error, if any. */
+int rmsf_xtcdec_synchronize(rmsf_xtcdec *d);
+/* Kernel level: decode n_frames XDR frame records (each starting at its
+ * magic word) held in device memory at 32-bit word offsets d_rec_off with
+ * lengths d_rec_len (words); d_status[f] = 0 or a per-frame error code.   */
+int rmsf_xtc_decode_records(const void *d_records, const int64_t *d_rec_off,
+                            const int64_t *d_rec_len, int64_t n_frames,
+                            int64_t n_atoms, float *d_out, int64_t out_stride,
+                            int32_t *d_status, void *stream);
+/* The device decoder's code run on the host (tests; no HIP calls). */
+int rmsf_xtc_decode_records_host(const void *h_records,
+                                 const int64_t *h_rec_off,
+                                 const int64_t *h_rec_len, int64_t n_frames,
+                                 int64_t n_atoms, float *h_out,
+                                 int64_t out_stride, int32_t *h_status);
 
 /* ---- RMSF context: the whole per-rank loop behind one opaque handle -------
  * SURVEY.md 8(b)'s minimal export set, for hosts that bring neither torch

@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "rmsf_hip.h"
+#include "xtc_internal.h"
 
 #define RMSF_EXPORT __attribute__((visibility("default")))
 
@@ -495,19 +496,7 @@ bool encode_coords(const float *ptr, int size, float precision, std::vector<unsi
 
 }  // namespace
 
-struct rmsf_xtc {
-  int fd = -1;
-  int64_t n_atoms = 0;
-  std::vector<int64_t> offset;  // byte offset of each frame
-  std::vector<int64_t> size;    // bytes of each frame
-  std::vector<int32_t> step;
-  std::vector<float> time;
-  std::vector<float> box;       // 9 per frame (nm)
-};
-
-namespace {
-
-bool pread_all(int fd, void *dst, size_t n, int64_t off) {
+bool rmsf_internal_pread_all(int fd, void *dst, size_t n, int64_t off) {
   char *d = static_cast<char *>(dst);
   while (n > 0) {
     const ssize_t r = pread(fd, d, n, (off_t)off);
@@ -519,11 +508,13 @@ bool pread_all(int fd, void *dst, size_t n, int64_t off) {
   return true;
 }
 
+namespace {
+
 // decode frame f of x into `dst` (Angstrom), selecting `sel` rows
 bool decode_frame(const rmsf_xtc *x, int64_t f, const int32_t *sel, int64_t n_sel, float *dst,
                   std::vector<unsigned char> &raw, std::vector<float> &nm) {
   raw.resize((size_t)x->size[f]);
-  if (!pread_all(x->fd, raw.data(), raw.size(), x->offset[f])) return false;
+  if (!rmsf_internal_pread_all(x->fd, raw.data(), raw.size(), x->offset[f])) return false;
   nm.resize(3 * (size_t)x->n_atoms);
   const size_t hdr = 4 * 4 + 9 * 4;
   if (decode_coords(raw.data() + hdr, raw.size() - hdr, (int)x->n_atoms, nm.data()) < 0) return false;
@@ -582,7 +573,7 @@ RMSF_EXPORT int rmsf_xtc_open(const char *path, rmsf_xtc **out, int64_t *n_atoms
   unsigned char h[4 * 4 + 9 * 4 + 4 + 4 + 24 + 4 + 4];
   while (off < fsize) {
     const size_t want = (size_t)std::min<int64_t>((int64_t)sizeof h, fsize - off);
-    if (want < 4 * 4 + 9 * 4 + 4 || !pread_all(fd, h, want, off)) break;
+    if (want < 4 * 4 + 9 * 4 + 4 || !rmsf_internal_pread_all(fd, h, want, off)) break;
     const unsigned char *p = h;
     const int magic = rd_i(p), na = rd_i(p), stp = rd_i(p);
     const float tm = rd_f(p);
@@ -608,6 +599,7 @@ RMSF_EXPORT int rmsf_xtc_open(const char *path, rmsf_xtc **out, int64_t *n_atoms
     x->n_atoms = na;
     x->offset.push_back(off);
     x->size.push_back(sz);
+    x->max_size = std::max(x->max_size, sz);
     x->step.push_back(stp);
     x->time.push_back(tm);
     x->box.insert(x->box.end(), box, box + 9);
@@ -639,6 +631,13 @@ RMSF_EXPORT int rmsf_xtc_frame_info(const rmsf_xtc *x, int64_t f, int32_t *step,
   return RMSF_OK;
 }
 
+RMSF_EXPORT int rmsf_xtc_frame_record(const rmsf_xtc *x, int64_t f, int64_t *offset, int64_t *bytes) {
+  if (!x || f < 0 || f >= (int64_t)x->offset.size()) return fail(RMSF_EINVAL, "rmsf_xtc_frame_record: bad frame");
+  if (offset) *offset = x->offset[f];
+  if (bytes) *bytes = x->size[f];
+  return RMSF_OK;
+}
+
 RMSF_EXPORT int rmsf_xtc_read(const rmsf_xtc *x, int64_t f0, int64_t n, int64_t step, const int32_t *h_sel,
                               int64_t n_sel, float *h_out, int n_threads) {
   if (!x || !h_out || n < 0 || step < 1 || f0 < 0 || (n > 0 && f0 + (n - 1) * step >= (int64_t)x->offset.size()))
@@ -656,23 +655,39 @@ RMSF_EXPORT int rmsf_xtc_write(const char *path, const float *xyz, int64_t n_fra
     return fail(RMSF_EINVAL, "rmsf_xtc_write: bad arguments");
   FILE *fp = std::fopen(path, append ? "ab" : "wb");
   if (!fp) return fail(RMSF_EINVAL, std::string("rmsf_xtc_write: cannot open ") + path);
-  std::vector<float> nm(3 * (size_t)n_atoms);
-  std::vector<unsigned char> o;
+  // frames are encoded independently on a few threads, written in order
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({n_frames, 16, (int64_t)std::thread::hardware_concurrency()}));
   int rc = RMSF_OK;
-  for (int64_t f = 0; f < n_frames && rc == RMSF_OK; ++f) {
-    const float *src = xyz + f * 3 * n_atoms;
-    for (size_t k = 0; k < nm.size(); ++k) nm[k] = src[k] * 0.1f;  // Angstrom -> nm (MDAnalysis writer)
-    o.clear();
-    wr_i(o, kMagic);
-    wr_i(o, (int)n_atoms);
-    wr_i(o, (int)f);
-    wr_f(o, (float)f);
-    for (int j = 0; j < 9; ++j) wr_f(o, box9 ? box9[j] * 0.1f : 0.0f);
-    if (!encode_coords(nm.data(), (int)n_atoms, precision, o)) {
+  std::vector<std::vector<unsigned char>> enc((size_t)nt);
+  for (int64_t f0 = 0; f0 < n_frames && rc == RMSF_OK; f0 += nt) {
+    const int64_t n = std::min<int64_t>(nt, n_frames - f0);
+    std::atomic<bool> bad{false};
+    auto work = [&](int64_t k) {
+      std::vector<unsigned char> &o = enc[(size_t)k];
+      std::vector<float> nm(3 * (size_t)n_atoms);
+      const float *src = xyz + (f0 + k) * 3 * n_atoms;
+      for (size_t i = 0; i < nm.size(); ++i) nm[i] = src[i] * 0.1f;  // Angstrom -> nm (MDAnalysis writer)
+      o.clear();
+      wr_i(o, kMagic);
+      wr_i(o, (int)n_atoms);
+      wr_i(o, (int)(f0 + k));
+      wr_f(o, (float)(f0 + k));
+      for (int j = 0; j < 9; ++j) wr_f(o, box9 ? box9[j] * 0.1f : 0.0f);
+      if (!encode_coords(nm.data(), (int)n_atoms, precision, o)) bad.store(true);
+    };
+    std::vector<std::thread> th;
+    for (int64_t k = 1; k < n; ++k) th.emplace_back(work, k);
+    work(0);
+    for (auto &t : th) t.join();
+    if (bad.load()) {
       rc = fail(RMSF_EINVAL, "rmsf_xtc_write: coordinates out of range for this precision");
       break;
     }
-    if (std::fwrite(o.data(), 1, o.size(), fp) != o.size()) rc = fail(RMSF_EINVAL, "rmsf_xtc_write: write failed");
+    for (int64_t k = 0; k < n; ++k)
+      if (std::fwrite(enc[(size_t)k].data(), 1, enc[(size_t)k].size(), fp) != enc[(size_t)k].size()) {
+        rc = fail(RMSF_EINVAL, "rmsf_xtc_write: write failed");
+        break;
+      }
   }
   std::fclose(fp);
   return rc;

@@ -1,0 +1,784 @@
+// xtc_gpu.hip -- XTC decompression on the GPU (config C5).
+//
+// The host decoder (xtc.cpp) replaces libxdrfile behind MDAnalysis'
+// XTCReader, i.e. what `universe.trajectory[frame]` runs at RMSF.py:92,124;
+// it is bound by host cores (~2k frames/s of 250k atoms on 16 threads).  Here
+// the compressed frame records themselves are streamed: read from the file
+// into a pinned slot (pread, host threads), copied to HBM (about 1/6 of the
+// decoded bytes), and decompressed on the device -- the xdr3dfcoord stream of
+// one frame is strictly sequential, so a frame is one wave's work (the
+// decoder state is wave-uniform; the wave fetches the stream 256 B at a time
+// with the next chunk in flight, and stores 64 decoded atoms at a time) and
+// frames run in parallel, one wave each.  Output: float32 [n][n_atoms][3] Angstrom frames in HBM with
+// MDAnalysis' rounding f32(f32(int * f32(1/prec)) * 10), bit-identical to the
+// host decoder.  The selection is applied downstream (the accumulate
+// kernels gather it in-kernel), as for any HBM-resident trajectory.
+//
+// Packed triples of <= 52 bits are split with two exact double-precision
+// divisions (quotient estimate by reciprocal, one correction step); wider
+// ones use the byte-wise long division of the published algorithm.  Every
+// read is bounded by the record length; a corrupt frame sets its status and
+// is filled with NaN.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "rmsf_hip.h"
+#include "xtc_internal.h"
+
+#define RMSF_EXPORT __attribute__((visibility("default")))
+
+extern "C" int rmsf_internal_set_error(int code, const char *msg);
+
+namespace {
+
+int fail(int code, const std::string &m) { return rmsf_internal_set_error(code, m.c_str()); }
+
+#define XD_HIP(expr)                                                                                  \
+  do {                                                                                                \
+    hipError_t e_ = (expr);                                                                           \
+    if (e_ != hipSuccess) return fail(RMSF_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int kMagic = 1995;
+constexpr int kFirstIdx = 9;
+constexpr int kLastIdx = 73;
+struct MagicTable {
+  int v[kLastIdx];
+};
+struct InvTable {
+  double v[kLastIdx];
+};
+constexpr MagicTable make_magic() {
+  return MagicTable{{0,        0,        0,        0,        0,        0,       0,       0,       0,       8,
+                     10,       12,       16,       20,       25,       32,      40,      50,      64,      80,
+                     101,      128,      161,      203,      256,      322,     406,     512,     645,     812,
+                     1024,     1290,     1625,     2048,     2580,     3250,    4096,    5060,    6501,    8192,
+                     10321,    13003,    16384,    20642,    26007,    32768,   41285,   52015,   65536,   82570,
+                     104031,   131072,   165140,   208063,   262144,   330280,  416127,  524287,  660561,  832255,
+                     1048576,  1321122,  1664510,  2097152,  2642245,  3329021, 4194304, 5284491, 6658042, 8388607,
+                     10568983, 13316085, 16777216}};
+}
+constexpr InvTable make_inv() {
+  InvTable t{};
+  const MagicTable m = make_magic();
+  for (int i = 0; i < kLastIdx; ++i) t.v[i] = m.v[i] ? 1.0 / (double)m.v[i] : 0.0;
+  return t;
+}
+__constant__ MagicTable g_magic = make_magic();
+__constant__ InvTable g_inv = make_inv();
+constexpr MagicTable h_magic = make_magic();
+constexpr InvTable h_inv = make_inv();
+
+// status codes per frame
+constexpr int32_t kOk = 0, kShort = 1, kBadMagic = 2, kBadNatoms = 3, kBadHeader = 4, kCorrupt = 5;
+
+__host__ __device__ inline uint32_t be32w(uint32_t w) { return __builtin_bswap32(w); }
+
+// MSB-first bit reader: Src supplies the record's big-endian words in order
+// (word()); `acc` keeps up to 64 bits.  Past the stream's words Src yields
+// zeros, and `left` goes negative: an overrun is checked once per atom.
+template <class Src>
+struct Bits {
+  Src src;
+  uint64_t acc = 0;
+  int n = 0;         // valid bits in the low end of acc
+  int64_t left = 0;  // bits left in the stream (< 0: overrun)
+  __host__ __device__ inline bool bad() const { return left < 0; }
+  __host__ __device__ inline uint32_t get(int k) {  // 0 <= k <= 32
+    left -= k;
+    if (n < k) {
+      acc = (acc << 32) | be32w(src.word());
+      n += 32;
+    }
+    n -= k;
+    return (uint32_t)(acc >> n) & (uint32_t)((1ull << k) - 1ull);
+  }
+};
+
+// host: the words straight from memory
+struct MemWords {
+  const uint32_t *w, *wend;
+  __host__ __device__ inline void start(const uint32_t *p, int64_t n_words) {
+    w = p;
+    wend = p + n_words;
+  }
+  __host__ __device__ inline uint32_t word() { return w < wend ? *w++ : 0u; }
+};
+
+// device, one wave per frame: every lane runs the (uniform) decoder; the
+// stream is fetched 64 words (256 B) at a time by the whole wave, lane j
+// holding word j of the chunk, and read back with readlane.  The next chunk
+// is always in flight, so the load latency hides behind ~50 atoms of decode.
+struct WaveWords {
+  const uint32_t *s;
+  int64_t nw, wi;
+  uint32_t cur, nxt;
+  int lane;
+  __device__ inline void start(const uint32_t *p, int64_t n_words) {
+    s = p;
+    nw = n_words;
+    wi = 0;
+    lane = (int)(threadIdx.x & 63);
+    cur = lane < nw ? p[lane] : 0u;
+    nxt = 64 + lane < nw ? p[64 + lane] : 0u;
+  }
+  __device__ inline uint32_t word() {
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)(wi & 63));
+    ++wi;
+    if ((wi & 63) == 0) {
+      cur = nxt;
+      const int64_t j = wi + 64 + lane;
+      nxt = j < nw ? s[j] : 0u;
+    }
+    return w;
+  }
+};
+
+// receiveints' byte order: the packed value's bytes arrive least significant
+// first (8 bits each), the last (1..8 bits) carrying the top.  nbits <= 64.
+template <class B>
+__host__ __device__ inline uint64_t read_packed(B &b, int nbits) {
+  int q = (nbits - 1) >> 3;
+  const int last = nbits - 8 * q;
+  uint64_t v = 0;
+  int sh = 0;
+  while (q >= 4) {
+    v |= (uint64_t)be32w(b.get(32)) << sh;
+    sh += 32;
+    q -= 4;
+  }
+  if (q > 0) {
+    v |= (uint64_t)(be32w(b.get(8 * q)) >> (32 - 8 * q)) << sh;
+    sh += 8 * q;
+  }
+  v |= (uint64_t)b.get(last) << sh;
+  return v;
+}
+
+// value = (n0*s1 + n1)*s2 + n2, value < 2^52: exact double arithmetic.
+__host__ __device__ inline void split_f64(uint64_t v, const unsigned s[3], const double inv[3], int out[3]) {
+  double d = (double)v;
+  for (int i = 2; i >= 1; --i) {
+    double q = floor(d * inv[i]);
+    double r = fma(-q, (double)s[i], d);  // exact: |r| < 2 s
+    if (r < 0.0) {
+      q -= 1.0;
+      r += (double)s[i];
+    } else if (r >= (double)s[i]) {
+      q += 1.0;
+      r -= (double)s[i];
+    }
+    out[i] = (int)r;
+    d = q;
+  }
+  out[0] = (int)(uint32_t)(uint64_t)d;
+}
+
+// the published byte-wise long division, for packed values wider than 52 bits
+template <class B>
+__host__ __device__ inline bool split_bytes(B &b, int nbits, const unsigned s[3], int out[3]) {
+  if (nbits > 96 || s[1] == 0 || s[2] == 0 || s[1] > (1u << 24) || s[2] > (1u << 24)) return false;
+  unsigned bytes[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int nb = 0;
+  while (nbits > 8) {
+    bytes[nb++] = b.get(8);
+    nbits -= 8;
+  }
+  if (nbits > 0) bytes[nb++] = b.get(nbits);
+  for (int i = 2; i > 0; --i) {
+    unsigned num = 0;
+    for (int j = nb - 1; j >= 0; --j) {
+      num = (num << 8) | bytes[j];
+      const unsigned p = num / s[i];
+      bytes[j] = p;
+      num -= p * s[i];
+    }
+    out[i] = (int)num;
+  }
+  out[0] = (int)(bytes[0] | bytes[1] << 8 | bytes[2] << 16 | bytes[3] << 24);
+  return true;
+}
+
+template <class B>
+__host__ __device__ inline bool read_triple(B &b, int nbits, const unsigned s[3], const double inv[3],
+                                            int out[3]) {
+  if (nbits <= 52) {
+    split_f64(read_packed(b, nbits), s, inv, out);
+    return true;
+  }
+  return split_bytes(b, nbits, s, out);
+}
+
+__host__ __device__ inline int sizeofint_hd(unsigned size) {
+  unsigned num = 1;
+  int nbits = 0;
+  while (size >= num && nbits < 32) {
+    nbits++;
+    num <<= 1;
+  }
+  return nbits;
+}
+
+__host__ __device__ inline int sizeofints_hd(const unsigned sizes[3]) {
+  unsigned bytes[32];
+  int nb = 1, nbits = 0;
+  bytes[0] = 1;
+  for (int i = 0; i < 3; ++i) {
+    unsigned tmp = 0;
+    int bc;
+    for (bc = 0; bc < nb; ++bc) {
+      tmp = bytes[bc] * sizes[i] + tmp;
+      bytes[bc] = tmp & 0xff;
+      tmp >>= 8;
+    }
+    while (tmp != 0 && bc < 32) {
+      bytes[bc++] = tmp & 0xff;
+      tmp >>= 8;
+    }
+    nb = bc;
+  }
+  unsigned num = 1;
+  nb--;
+  while (bytes[nb] >= num && nbits < 32) {
+    nbits++;
+    num *= 2;
+  }
+  return nbits + nb * 8;
+}
+
+__host__ __device__ inline float f32_bits(uint32_t u) { return __builtin_bit_cast(float, u); }
+
+// device, one lane per frame: the lane fetches its own stream 16 B at a
+// time (four dword loads) with the next 16 B already in flight.
+struct LaneWords {
+  const uint32_t *s;
+  int64_t nw, wi;  // wi: next word to fetch
+  uint32_t q0, q1, q2, q3, p0, p1, p2, p3;
+  int cnt;
+  __device__ inline uint32_t at(int64_t j) const { return j < nw ? s[j] : 0u; }
+  __device__ inline void start(const uint32_t *p, int64_t n_words) {
+    s = p;
+    nw = n_words;
+    q0 = at(0);
+    q1 = at(1);
+    q2 = at(2);
+    q3 = at(3);
+    p0 = at(4);
+    p1 = at(5);
+    p2 = at(6);
+    p3 = at(7);
+    wi = 8;
+    cnt = 4;
+  }
+  __device__ inline uint32_t word() {
+    const uint32_t w = q0;
+    q0 = q1;
+    q1 = q2;
+    q2 = q3;
+    if (--cnt == 0) {
+      q0 = p0;
+      q1 = p1;
+      q2 = p2;
+      q3 = p3;
+      p0 = at(wi);
+      p1 = at(wi + 1);
+      p2 = at(wi + 2);
+      p3 = at(wi + 3);
+      wi += 4;
+      cnt = 4;
+    }
+    return w;
+  }
+};
+
+// xdrfile scales to nm in f32; MDAnalysis then multiplies by 10 in f32
+__host__ __device__ inline void to_angstrom(int c0, int c1, int c2, float invp, float &a, float &b, float &c) {
+#pragma clang fp contract(off)
+  const float x = (float)c0 * invp, y = (float)c1 * invp, z = (float)c2 * invp;
+  a = x * 10.0f;
+  b = y * 10.0f;
+  c = z * 10.0f;
+}
+
+// host: atoms written in order
+struct MemSink {
+  float *o;
+  __host__ __device__ inline void put_f(float a, float b, float c) {
+    o[0] = a;
+    o[1] = b;
+    o[2] = c;
+    o += 3;
+  }
+  __host__ __device__ inline void put(int c0, int c1, int c2, float invp) {
+    float a, b, c;
+    to_angstrom(c0, c1, c2, invp, a, b, c);
+    put_f(a, b, c);
+  }
+  __host__ __device__ inline void flush() {}
+};
+
+// device: atom k of a group of 64 goes to lane k's registers;
+// a full group is stored by the whole wave, 768 contiguous bytes.
+struct WaveSink {
+  float *o;  // next group's first atom
+  int k;
+  uint32_t vx, vy, vz;
+  __device__ inline void put(int c0, int c1, int c2, float invp) {
+    float a, b, c;
+    to_angstrom(c0, c1, c2, invp, a, b, c);
+    put_f(a, b, c);
+  }
+  __device__ inline void put_f(float a, float b, float c) {
+    const bool mine = (int)(threadIdx.x & 63) == k;
+    vx = mine ? __builtin_bit_cast(uint32_t, a) : vx;
+    vy = mine ? __builtin_bit_cast(uint32_t, b) : vy;
+    vz = mine ? __builtin_bit_cast(uint32_t, c) : vz;
+    if (++k == 64) flush();
+  }
+  __device__ inline void flush() {
+    const int lane = (int)(threadIdx.x & 63);
+    if (lane < k) {
+      o[3 * lane] = __builtin_bit_cast(float, vx);
+      o[3 * lane + 1] = __builtin_bit_cast(float, vy);
+      o[3 * lane + 2] = __builtin_bit_cast(float, vz);
+    }
+    o += 3 * k;
+    k = 0;
+  }
+};
+
+// Decode one XTC frame record (starting at its magic word, `words` long)
+// into n_atoms Angstrom triples through `sink`.  Mirrors decode_coords() of
+// xtc.cpp.  Src: MemWords (host) or WaveWords (device, one wave per frame).
+template <class Src, class Sink>
+__host__ __device__ int32_t decode_record(const uint32_t *rec, int64_t words, int64_t n_atoms, Sink &sink,
+                                          const int *magic, const double *inv_magic) {
+#pragma clang fp contract(off)
+  if (words < 14) return kShort;
+  if ((int)be32w(rec[0]) != kMagic) return kBadMagic;
+  const int natoms = (int)be32w(rec[1]);
+  if (natoms != n_atoms || (int)be32w(rec[13]) != natoms) return kBadNatoms;
+  const uint32_t *p = rec + 14;  // magic natoms step time box[9] lsize
+  int64_t left = words - 14;
+  if (natoms <= 9) {
+    if (left < 3 * natoms) return kShort;
+    for (int a = 0; a < natoms; ++a)  // raw floats (nm) x 10, as MDAnalysis
+      sink.put_f(f32_bits(be32w(p[3 * a])) * 10.0f, f32_bits(be32w(p[3 * a + 1])) * 10.0f,
+                 f32_bits(be32w(p[3 * a + 2])) * 10.0f);
+    sink.flush();
+    return kOk;
+  }
+  if (left < 9) return kShort;
+  const float precision = f32_bits(be32w(p[0]));
+  int minint[3], maxint[3];
+  for (int c = 0; c < 3; ++c) {
+    minint[c] = (int)be32w(p[1 + c]);
+    maxint[c] = (int)be32w(p[4 + c]);
+  }
+  int smallidx = (int)be32w(p[7]);
+  const int nbytes = (int)be32w(p[8]);
+  p += 9;
+  left -= 9;
+  if (smallidx < kFirstIdx || smallidx >= kLastIdx || nbytes < 0 || ((int64_t)nbytes + 3) / 4 > left)
+    return kBadHeader;
+  unsigned sizeint[3], bitsizeint[3] = {0, 0, 0};
+  double invint[3];
+  for (int c = 0; c < 3; ++c) {
+    sizeint[c] = (unsigned)(maxint[c] - minint[c]) + 1u;
+    invint[c] = 1.0 / (double)sizeint[c];
+  }
+  int bitsize = 0;
+  if ((sizeint[0] | sizeint[1] | sizeint[2]) > 0xffffff) {
+    for (int c = 0; c < 3; ++c) bitsizeint[c] = sizeofint_hd(sizeint[c]);
+  } else {
+    bitsize = sizeofints_hd(sizeint);
+  }
+  int smaller = magic[smallidx - 1 > kFirstIdx ? smallidx - 1 : kFirstIdx] / 2;
+  int smallnum = magic[smallidx] / 2;
+  unsigned sizesmall[3];
+  double invsmall[3];
+  sizesmall[0] = sizesmall[1] = sizesmall[2] = magic[smallidx];
+  invsmall[0] = invsmall[1] = invsmall[2] = inv_magic[smallidx];
+  const float inv_precision = (float)(1.0 / (double)precision);
+
+  Bits<Src> b;
+  const int64_t nw = ((int64_t)nbytes + 3) / 4;
+  b.src.start(p, nw);
+  b.left = 8 * (int64_t)nbytes;
+  int prev[3] = {0, 0, 0};
+  int run = 0, i = 0;
+  while (i < natoms) {
+    int cur[3];
+    if (bitsize == 0) {
+      cur[0] = (int)b.get(bitsizeint[0]);
+      cur[1] = (int)b.get(bitsizeint[1]);
+      cur[2] = (int)b.get(bitsizeint[2]);
+    } else if (!read_triple(b, bitsize, sizeint, invint, cur)) {
+      return kCorrupt;
+    }
+    i++;
+    cur[0] += minint[0];
+    cur[1] += minint[1];
+    cur[2] += minint[2];
+    prev[0] = cur[0];
+    prev[1] = cur[1];
+    prev[2] = cur[2];
+    int is_smaller = 0;
+    if (b.get(1)) {
+      run = (int)b.get(5);
+      is_smaller = run % 3;
+      run -= is_smaller;
+      is_smaller--;
+    }
+    if (run > 0) {
+      if (i + run / 3 > natoms || sizesmall[0] == 0) return kCorrupt;
+      for (int k = 0; k < run; k += 3) {
+        int t[3];
+        if (!read_triple(b, smallidx, sizesmall, invsmall, t)) return kCorrupt;
+        i++;
+        t[0] += prev[0] - smallnum;
+        t[1] += prev[1] - smallnum;
+        t[2] += prev[2] - smallnum;
+        if (k == 0) {  // the writer swapped the first two atoms (water)
+          const int s0 = t[0], s1 = t[1], s2 = t[2];
+          t[0] = prev[0];
+          t[1] = prev[1];
+          t[2] = prev[2];
+          prev[0] = s0;
+          prev[1] = s1;
+          prev[2] = s2;
+          sink.put(prev[0], prev[1], prev[2], inv_precision);
+        } else {
+          prev[0] = t[0];
+          prev[1] = t[1];
+          prev[2] = t[2];
+        }
+        sink.put(t[0], t[1], t[2], inv_precision);
+      }
+    } else {
+      sink.put(cur[0], cur[1], cur[2], inv_precision);
+    }
+    smallidx += is_smaller;
+    if (smallidx < kFirstIdx - 1 || smallidx >= kLastIdx) return kCorrupt;
+    if (is_smaller != 0) {
+      if (is_smaller < 0) {
+        smallnum = smaller;
+        smaller = smallidx > kFirstIdx ? magic[smallidx - 1] / 2 : 0;
+      } else {
+        smaller = smallnum;
+        smallnum = magic[smallidx] / 2;
+      }
+      sizesmall[0] = sizesmall[1] = sizesmall[2] = magic[smallidx];
+      invsmall[0] = invsmall[1] = invsmall[2] = inv_magic[smallidx];
+    }
+    if (b.bad()) return kCorrupt;
+  }
+  sink.flush();
+  return b.bad() ? kCorrupt : kOk;
+}
+
+// One wave per frame (grid = n_frames blocks of 64): the decoder state is
+// wave-uniform; the stream is fetched by the whole wave (WaveWords) and the
+// output stored by it (WaveSink).
+__global__ __launch_bounds__(64) void k_xtc_decode(const uint32_t *__restrict__ words,
+                                                   const int64_t *__restrict__ rec_off,
+                                                   const int64_t *__restrict__ rec_len, int64_t n_atoms,
+                                                   float *__restrict__ out, int64_t out_stride,
+                                                   int32_t *__restrict__ status) {
+  const int64_t f = blockIdx.x;
+  float *o = out + f * out_stride;
+  WaveSink sink{o, 0, 0u, 0u, 0u};
+  const int32_t st = decode_record<WaveWords>(words + rec_off[f], rec_len[f], n_atoms, sink, g_magic.v, g_inv.v);
+  if (st != kOk) {
+    for (int64_t k = threadIdx.x; k < 3 * n_atoms; k += 64) o[k] = __builtin_nanf("");
+  }
+  if (threadIdx.x == 0) status[f] = st;
+}
+
+// One lane per frame, `lpw` frames per wave (the other lanes idle).
+__global__ __launch_bounds__(64) void k_xtc_decode_lanes(const uint32_t *__restrict__ words,
+                                                         const int64_t *__restrict__ rec_off,
+                                                         const int64_t *__restrict__ rec_len, int64_t n_frames,
+                                                         int64_t n_atoms, float *__restrict__ out,
+                                                         int64_t out_stride, int32_t *__restrict__ status,
+                                                         int lpw) {
+  const int lane = threadIdx.x;
+  if (lane >= lpw) return;
+  const int64_t f = (int64_t)blockIdx.x * lpw + lane;
+  if (f >= n_frames) return;
+  float *o = out + f * out_stride;
+  MemSink sink{o};
+  const int32_t st = decode_record<LaneWords>(words + rec_off[f], rec_len[f], n_atoms, sink, g_magic.v, g_inv.v);
+  if (st != kOk) {
+    for (int64_t k = 0; k < 3 * n_atoms; ++k) o[k] = __builtin_nanf("");
+  }
+  status[f] = st;
+}
+
+int simd_count() {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  return 4 * std::max(1, cus);
+}
+
+const char *status_text(int32_t s) {
+  switch (s) {
+    case kShort: return "truncated frame record";
+    case kBadMagic: return "bad magic number";
+    case kBadNatoms: return "atom count differs from the file's";
+    case kBadHeader: return "bad compression header";
+    case kCorrupt: return "corrupt compressed coordinates";
+    default: return "unknown error";
+  }
+}
+
+// Parallel pread of [off, off+n) into dst (n_threads chunks).
+bool pread_par(int fd, unsigned char *dst, size_t n, int64_t off, int n_threads) {
+  const size_t chunk = std::max<size_t>(1 << 20, (n + n_threads - 1) / std::max(1, n_threads));
+  std::vector<std::thread> th;
+  std::vector<char> ok((n + chunk - 1) / chunk + 1, 1);
+  size_t k = 0;
+  for (size_t s = 0; s < n; s += chunk, ++k) {
+    const size_t len = std::min(chunk, n - s);
+    th.emplace_back([&, s, len, k] { ok[k] = rmsf_internal_pread_all(fd, dst + s, len, off + (int64_t)s); });
+  }
+  for (auto &t : th) t.join();
+  return std::all_of(ok.begin(), ok.end(), [](char c) { return c != 0; });
+}
+
+}  // namespace
+
+struct rmsf_xtcdec {
+  const rmsf_xtc *x = nullptr;
+  int64_t batch = 0, n_atoms = 0;
+  int n_threads = 1;
+  struct Slot {
+    unsigned char *h_raw = nullptr;
+    int64_t *h_tab = nullptr;  // [2][batch]: record offset (words), record length (words)
+    int32_t *h_status = nullptr;
+    unsigned char *d_raw = nullptr;
+    int64_t *d_tab = nullptr;
+    int32_t *d_status = nullptr;
+    float *d_frames = nullptr;
+    size_t raw_cap = 0;
+    hipStream_t s = nullptr;
+    hipEvent_t done = nullptr, released = nullptr;
+    int64_t pending = 0;  // frames whose status is not yet checked
+    int64_t f0 = 0, step = 1;
+  };
+  std::vector<Slot> slots;
+  int next = 0;
+};
+
+namespace {
+
+int check_slot(rmsf_xtcdec *d, rmsf_xtcdec::Slot &s) {
+  if (s.pending == 0) return RMSF_OK;
+  XD_HIP(hipEventSynchronize(s.done));
+  const int64_t n = s.pending;
+  s.pending = 0;
+  for (int64_t k = 0; k < n; ++k)
+    if (s.h_status[k] != kOk)
+      return fail(RMSF_EINVAL, "xtc (GPU decode): frame " + std::to_string(s.f0 + k * s.step) + ": " +
+                                   status_text(s.h_status[k]));
+  return RMSF_OK;
+}
+
+void free_slot(rmsf_xtcdec::Slot &s) {
+  if (s.s) (void)hipStreamSynchronize(s.s);
+  if (s.h_raw) (void)hipHostFree(s.h_raw);
+  if (s.h_tab) (void)hipHostFree(s.h_tab);
+  if (s.h_status) (void)hipHostFree(s.h_status);
+  if (s.d_raw) (void)hipFree(s.d_raw);
+  if (s.d_tab) (void)hipFree(s.d_tab);
+  if (s.d_status) (void)hipFree(s.d_status);
+  if (s.d_frames) (void)hipFree(s.d_frames);
+  if (s.done) (void)hipEventDestroy(s.done);
+  if (s.released) (void)hipEventDestroy(s.released);
+  if (s.s) (void)hipStreamDestroy(s.s);
+  s = rmsf_xtcdec::Slot{};
+}
+
+}  // namespace
+
+extern "C" {
+
+RMSF_EXPORT int rmsf_xtc_decode_records(const void *d_records, const int64_t *d_rec_off, const int64_t *d_rec_len,
+                                        int64_t n_frames, int64_t n_atoms, float *d_out, int64_t out_stride,
+                                        int32_t *d_status, void *stream) {
+  if (!d_records || !d_rec_off || !d_rec_len || !d_out || !d_status || n_frames < 0 || n_atoms < 1 ||
+      out_stride < 3 * n_atoms ||
+      (reinterpret_cast<uintptr_t>(d_records) & 3))
+    return fail(RMSF_EINVAL, "rmsf_xtc_decode_records: bad arguments");
+  if (n_frames == 0) return RMSF_OK;
+  if (n_frames > 0x7fffffffLL) return fail(RMSF_EINVAL, "rmsf_xtc_decode_records: too many frames");
+  hipLaunchKernelGGL(k_xtc_decode, dim3((unsigned)n_frames), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                     static_cast<const uint32_t *>(d_records), d_rec_off, d_rec_len, n_atoms, d_out, out_stride,
+                     d_status);
+  XD_HIP(hipGetLastError());
+  return RMSF_OK;
+}
+
+// benchmarking hook (not in the public header): mode 0 = one wave per frame,
+// mode k >= 1 = one lane per frame with k frames per wave (-1: automatic)
+RMSF_EXPORT int rmsf_internal_xtc_decode_mode(const void *d_records, const int64_t *d_rec_off,
+                                              const int64_t *d_rec_len, int64_t n_frames, int64_t n_atoms,
+                                              float *d_out, int64_t out_stride, int32_t *d_status, int mode,
+                                              void *stream) {
+  if (mode == 0)
+    return rmsf_xtc_decode_records(d_records, d_rec_off, d_rec_len, n_frames, n_atoms, d_out, out_stride, d_status,
+                                   stream);
+  int lpw = mode;
+  if (lpw < 0) lpw = (int)std::max<int64_t>(1, std::min<int64_t>(64, (n_frames + simd_count() - 1) / simd_count()));
+  lpw = std::min(lpw, 64);
+  const int64_t blocks = (n_frames + lpw - 1) / lpw;
+  hipLaunchKernelGGL(k_xtc_decode_lanes, dim3((unsigned)blocks), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                     static_cast<const uint32_t *>(d_records), d_rec_off, d_rec_len, n_frames, n_atoms, d_out,
+                     out_stride, d_status, lpw);
+  XD_HIP(hipGetLastError());
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_xtc_decode_records_host(const void *h_records, const int64_t *h_rec_off,
+                                             const int64_t *h_rec_len, int64_t n_frames, int64_t n_atoms,
+                                             float *h_out, int64_t out_stride, int32_t *h_status) {
+  if (!h_records || !h_rec_off || !h_rec_len || !h_out || !h_status || n_frames < 0 || n_atoms < 1 ||
+      out_stride < 3 * n_atoms || (reinterpret_cast<uintptr_t>(h_records) & 3))
+    return fail(RMSF_EINVAL, "rmsf_xtc_decode_records_host: bad arguments");
+  const uint32_t *w = static_cast<const uint32_t *>(h_records);
+  for (int64_t f = 0; f < n_frames; ++f) {
+    MemSink sink{h_out + f * out_stride};
+    h_status[f] = decode_record<MemWords>(w + h_rec_off[f], h_rec_len[f], n_atoms, sink, h_magic.v, h_inv.v);
+  }
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_xtcdec_create(const rmsf_xtc *x, int64_t batch_frames, int n_slots, int n_threads,
+                                   rmsf_xtcdec **out) {
+  if (!x || !out || batch_frames < 1 || n_slots < 1 || n_slots > 16 || n_threads < 1)
+    return fail(RMSF_EINVAL, "rmsf_xtcdec_create: bad arguments");
+  *out = nullptr;
+  auto *d = new rmsf_xtcdec();
+  d->x = x;
+  d->batch = batch_frames;
+  d->n_atoms = x->n_atoms;
+  d->n_threads = n_threads;
+  d->slots.resize(n_slots);
+  const size_t raw = (size_t)batch_frames * (size_t)x->max_size;
+  const size_t frames = (size_t)batch_frames * 3 * (size_t)x->n_atoms * sizeof(float);
+  for (auto &s : d->slots) {
+    s.raw_cap = raw;
+    hipError_t e = hipHostMalloc((void **)&s.h_raw, raw, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&s.h_tab, 2 * batch_frames * sizeof(int64_t), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void **)&s.h_status, batch_frames * sizeof(int32_t), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc((void **)&s.d_raw, raw);
+    if (e == hipSuccess) e = hipMalloc((void **)&s.d_tab, 2 * batch_frames * sizeof(int64_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&s.d_status, batch_frames * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc((void **)&s.d_frames, frames);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.released, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(s.released, s.s);  // initially free
+    if (e == hipSuccess) e = hipEventRecord(s.done, s.s);
+    if (e != hipSuccess) {
+      for (auto &t : d->slots) free_slot(t);
+      delete d;
+      return fail(RMSF_ENOMEM, std::string("rmsf_xtcdec_create: ") + hipGetErrorString(e));
+    }
+  }
+  *out = d;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_xtcdec_destroy(rmsf_xtcdec *d) {
+  if (d) {
+    for (auto &s : d->slots) free_slot(s);
+    delete d;
+  }
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_t step, void *consumer_stream,
+                                   int *slot, float **d_frames) {
+  if (!d || !slot || !d_frames || n < 1 || n > d->batch || step < 1 || f0 < 0 ||
+      f0 + (n - 1) * step >= (int64_t)d->x->offset.size())
+    return fail(RMSF_EINVAL, "rmsf_xtcdec_decode: bad arguments");
+  const int si = d->next;
+  d->next = (d->next + 1) % (int)d->slots.size();
+  auto &s = d->slots[si];
+  int rc = check_slot(d, s);  // the pinned buffers are rewritten below: the previous use must be over
+  if (rc) return rc;
+  XD_HIP(hipEventSynchronize(s.done));
+  const rmsf_xtc *x = d->x;
+  int64_t *off = s.h_tab, *len = s.h_tab + d->batch;
+  size_t total = 0;
+  if (step == 1) {
+    const int64_t a = x->offset[f0], e = x->offset[f0 + n - 1] + x->size[f0 + n - 1];
+    total = (size_t)(e - a);
+    if (total > s.raw_cap) return fail(RMSF_EINVAL, "rmsf_xtcdec_decode: batch larger than the slot");
+    if (!pread_par(x->fd, s.h_raw, total, a, d->n_threads)) return fail(RMSF_EINVAL, "xtc: read failed");
+    for (int64_t k = 0; k < n; ++k) {
+      off[k] = (x->offset[f0 + k] - a) / 4;
+      len[k] = x->size[f0 + k] / 4;
+    }
+  } else {
+    for (int64_t k = 0; k < n; ++k) {
+      const int64_t f = f0 + k * step;
+      off[k] = (int64_t)(total / 4);
+      len[k] = x->size[f] / 4;
+      total += (size_t)x->size[f];
+    }
+    if (total > s.raw_cap) return fail(RMSF_EINVAL, "rmsf_xtcdec_decode: batch larger than the slot");
+    std::vector<std::thread> th;
+    std::vector<char> ok(d->n_threads, 1);
+    for (int t = 0; t < d->n_threads; ++t)
+      th.emplace_back([&, t] {
+        for (int64_t k = t; k < n; k += d->n_threads) {
+          const int64_t f = f0 + k * step;
+          if (!rmsf_internal_pread_all(x->fd, s.h_raw + 4 * off[k], (size_t)x->size[f], x->offset[f])) ok[t] = 0;
+        }
+      });
+    for (auto &t : th) t.join();
+    for (char c : ok)
+      if (!c) return fail(RMSF_EINVAL, "xtc: read failed");
+  }
+  XD_HIP(hipMemcpyAsync(s.d_raw, s.h_raw, total, hipMemcpyHostToDevice, s.s));
+  XD_HIP(hipMemcpyAsync(s.d_tab, s.h_tab, 2 * d->batch * sizeof(int64_t), hipMemcpyHostToDevice, s.s));
+  XD_HIP(hipStreamWaitEvent(s.s, s.released, 0));  // the consumer is done with the previous frames
+  rc = rmsf_xtc_decode_records(s.d_raw, s.d_tab, s.d_tab + d->batch, n, d->n_atoms, s.d_frames, 3 * d->n_atoms,
+                               s.d_status, s.s);
+  if (rc) return rc;
+  XD_HIP(hipMemcpyAsync(s.h_status, s.d_status, n * sizeof(int32_t), hipMemcpyDeviceToHost, s.s));
+  XD_HIP(hipEventRecord(s.done, s.s));
+  XD_HIP(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(consumer_stream), s.done, 0));
+  s.pending = n;
+  s.f0 = f0;
+  s.step = step;
+  *slot = si;
+  *d_frames = s.d_frames;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_xtcdec_release(rmsf_xtcdec *d, int slot, void *consumer_stream) {
+  if (!d || slot < 0 || slot >= (int)d->slots.size()) return fail(RMSF_EINVAL, "rmsf_xtcdec_release: bad slot");
+  XD_HIP(hipEventRecord(d->slots[slot].released, reinterpret_cast<hipStream_t>(consumer_stream)));
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_xtcdec_synchronize(rmsf_xtcdec *d) {
+  if (!d) return fail(RMSF_EINVAL, "rmsf_xtcdec_synchronize: null");
+  int first = RMSF_OK;
+  for (auto &s : d->slots) {
+    const int rc = check_slot(d, s);
+    if (rc && !first) first = rc;
+  }
+  return first;
+}
+
+}  // extern "C"

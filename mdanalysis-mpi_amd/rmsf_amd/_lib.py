@@ -78,6 +78,14 @@ SIGNATURES = {
     "rmsf_xtc_frame_info": (c_int, [P, c_int64, POINTER(c_int32), POINTER(ctypes.c_float), P]),
     "rmsf_xtc_read": (c_int, [P, c_int64, c_int64, c_int64, P, c_int64, P, c_int]),
     "rmsf_xtc_write": (c_int, [c_char_p, P, c_int64, c_int64, ctypes.c_float, P, c_int]),
+    "rmsf_xtc_frame_record": (c_int, [P, c_int64, POINTER(c_int64), POINTER(c_int64)]),
+    "rmsf_xtcdec_create": (c_int, [P, c_int64, c_int, c_int, POINTER(c_void_p)]),
+    "rmsf_xtcdec_destroy": (c_int, [P]),
+    "rmsf_xtcdec_decode": (c_int, [P, c_int64, c_int64, c_int64, P, POINTER(c_int), POINTER(c_void_p)]),
+    "rmsf_xtcdec_release": (c_int, [P, c_int, P]),
+    "rmsf_xtcdec_synchronize": (c_int, [P]),
+    "rmsf_xtc_decode_records": (c_int, [P, P, P, c_int64, c_int64, P, c_int64, P, P]),
+    "rmsf_xtc_decode_records_host": (c_int, [P, P, P, c_int64, c_int64, P, c_int64, P]),
     # RMSF context (rmsf_ctx_*) and cross-rank exchange
     "rmsf_ctx_create": (c_int, [c_int, c_int64, c_int64, P, P, c_int, POINTER(c_void_p)]),
     "rmsf_ctx_destroy": (c_int, [P]),

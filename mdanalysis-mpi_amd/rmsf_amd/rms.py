@@ -110,6 +110,8 @@ class RMSF:
 
     def _make_source(self, eng: Engine):
         x = self._input
+        if hasattr(x, "batches") and hasattr(x, "reference") and hasattr(x, "n_sel"):
+            return x, self.masses  # a frame source (DeviceSource, HostSource, XtcSource, ...)
         if isinstance(x, torch.Tensor):
             if x.device.type != "cuda":
                 x = x.detach().cpu().numpy()

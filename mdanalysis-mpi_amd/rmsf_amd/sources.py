@@ -188,44 +188,106 @@ class HostSource:
             yield Batch(ptr, 3 * self.n_sel, n, None, lambda s=slot: self.stager.release(s, stream))
 
 
-class XtcSource:
-    """GROMACS XTC file: frames decoded frame-parallel on host threads straight
-    into the stager's pinned slots (selection applied), then DMA'd -- the
-    C5 path (XTC-decoded trajectory streamed from the host)."""
+class XtcDecoder:
+    """ctypes handle on the pinned-slot GPU XTC decoder (rmsf_xtcdec_*)."""
 
-    def __init__(self, path, sel=None, batch_frames: int | None = None, n_slots: int = 3, n_threads: int = 8):
+    def __init__(self, xtc, batch_frames: int, n_slots: int = 3, n_threads: int = 8):
+        self._h = ctypes.c_void_p()
+        call("rmsf_xtcdec_create", xtc.handle, batch_frames, n_slots, n_threads, ctypes.byref(self._h))
+        self.batch_frames, self.n_slots = batch_frames, n_slots
+
+    def decode(self, first: int, n: int, step: int, stream: int) -> tuple[int, int]:
+        slot, dptr = ctypes.c_int(), ctypes.c_void_p()
+        call("rmsf_xtcdec_decode", self._h, first, n, step, stream, ctypes.byref(slot), ctypes.byref(dptr))
+        return slot.value, dptr.value
+
+    def release(self, slot: int, stream: int) -> None:
+        call("rmsf_xtcdec_release", self._h, slot, stream)
+
+    def synchronize(self) -> None:
+        call("rmsf_xtcdec_synchronize", self._h)
+
+    def close(self) -> None:
+        if self._h:
+            call("rmsf_xtcdec_destroy", self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class XtcSource:
+    """GROMACS XTC file (the C5 path: an XTC-decoded trajectory streamed from
+    the host).  ``decode="gpu"``: the compressed frame records are read into
+    pinned slots, copied to HBM and decompressed there, one wave per frame
+    (csrc/xtc_gpu.hip); up to ``n_slots`` batches decode concurrently ahead
+    of the consumer.  ``decode="host"``: frames are decoded frame-parallel on
+    ``n_threads`` host threads straight into the stager's pinned slots
+    (selection applied) and DMA'd.  Both give the same float32 frames."""
+
+    def __init__(self, path, sel=None, batch_frames: int | None = None, n_slots: int = 3, n_threads: int = 8,
+                 decode: str = "gpu"):
         from .xtc import XTCFile
 
+        if decode not in ("gpu", "host"):
+            raise ValueError("decode must be 'gpu' or 'host'")
         self.xtc = XTCFile(path)
         self.n_traj, self.n_atoms = self.xtc.n_frames, self.xtc.n_atoms
         sel_arr = None if sel is None else np.ascontiguousarray(sel, dtype=np.int64)
         if sel_arr is not None and sel_arr.size and (sel_arr.min() < 0 or sel_arr.max() >= self.n_atoms):
             raise IndexError("selection index out of range")
         self.n_sel = self.n_atoms if sel_arr is None else len(sel_arr)
-        if batch_frames is None:
-            batch_frames = max(1, min(4096, (64 << 20) // max(1, 12 * self.n_sel)))
+        self.decode_on = decode
+        if decode == "gpu":
+            if batch_frames is None:  # ~2 GB of decoded frames per slot
+                batch_frames = max(1, min(4096, (2 << 30) // max(1, 12 * self.n_atoms)))
+            self.decoder = XtcDecoder(self.xtc, batch_frames, n_slots, n_threads)
+            self.sel_dev = None
+            if sel_arr is not None and not np.array_equal(sel_arr, np.arange(self.n_sel)):
+                self.sel_dev = torch.as_tensor(sel_arr.astype(np.int32)).to(torch.cuda.current_device())
+        else:
+            if batch_frames is None:
+                batch_frames = max(1, min(4096, (64 << 20) // max(1, 12 * self.n_sel)))
+            self.stager = Stager(self.n_atoms, self.n_sel, sel_arr, batch_frames, n_slots, n_threads)
         self.batch_frames = batch_frames
-        self.stager = Stager(self.n_atoms, self.n_sel, sel_arr, batch_frames, n_slots, n_threads)
 
     def holds(self, frame: int) -> bool:
         return 0 <= frame < self.n_traj
 
-    def _stage(self, first: int, step: int, n: int, stream: int):
+    def _stage(self, first: int, step: int, n: int, stream: int) -> Batch:
+        if self.decode_on == "gpu":
+            slot, ptr = self.decoder.decode(first, n, step, stream)
+            return Batch(ptr, 3 * self.n_atoms, n, self.sel_dev, lambda: self.decoder.release(slot, stream))
         slot, dptr = ctypes.c_int(), ctypes.c_void_p()
         call("rmsf_stager_stage_xtc", self.stager._h, self.xtc.handle, first, n, step, stream, ctypes.byref(slot),
              ctypes.byref(dptr))
-        return slot.value, dptr.value
+        s = slot.value
+        return Batch(dptr.value, 3 * self.n_sel, n, None, lambda: self.stager.release(s, stream))
+
+    def _check(self) -> None:
+        if self.decode_on == "gpu":
+            self.decoder.synchronize()
 
     def reference(self, frame: int, stream: int) -> Batch:
-        slot, ptr = self._stage(frame, 1, 1, stream)
-        return Batch(ptr, 3 * self.n_sel, 1, None, lambda: self.stager.release(slot, stream))
+        b = self._stage(frame, 1, 1, stream)
+        self._check()
+        return b
 
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
         bf = min(max_frames, self.batch_frames)
-        for i in range(b0, b1, bf):
-            n = min(bf, b1 - i)
-            slot, ptr = self._stage(frames.r[i], frames.step, n, stream)
-            yield Batch(ptr, 3 * self.n_sel, n, None, lambda s=slot: self.stager.release(s, stream))
+        starts = list(range(b0, b1, bf))
+        ahead = self.decoder.n_slots - 1 if self.decode_on == "gpu" else 0
+        queue = []
+        for k, i in enumerate(starts):
+            queue.append(self._stage(frames.r[i], frames.step, min(bf, b1 - i), stream))
+            if len(queue) > ahead:
+                yield queue.pop(0)
+        while queue:
+            yield queue.pop(0)
+        self._check()
 
 
 class AtomGroupSource:
@@ -275,4 +337,5 @@ class AtomGroupSource:
             yield Batch(ptr, 3 * self.n_sel, n, None, lambda s=slot: self.stager.release(s, stream))
 
 
-__all__ = ["Batch", "Stager", "FrameList", "DeviceSource", "HostSource", "XtcSource", "AtomGroupSource", "_lib"]
+__all__ = ["Batch", "Stager", "FrameList", "DeviceSource", "HostSource", "XtcDecoder", "XtcSource", "AtomGroupSource",
+           "_lib"]

@@ -47,6 +47,12 @@ class XTCFile:
         call("rmsf_xtc_frame_info", self._h, f, ctypes.byref(st), ctypes.byref(tm), box.ctypes.data)
         return st.value, tm.value, box.reshape(3, 3)
 
+    def record(self, f: int) -> tuple[int, int]:
+        """(byte offset, byte length) of frame f's XDR record in the file."""
+        off, n = ctypes.c_int64(), ctypes.c_int64()
+        call("rmsf_xtc_frame_record", self._h, f, ctypes.byref(off), ctypes.byref(n))
+        return off.value, n.value
+
     def close(self) -> None:
         if self._h:
             call("rmsf_xtc_close", self._h)
