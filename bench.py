@@ -222,7 +222,7 @@ def main():
             del host
             src = XtcSource(xtc_path, None, batch_frames=a.stager_batch, decode=a.xtc_decode,
                             n_threads=a.stager_threads if a.xtc_decode == "host" else max(a.stager_threads, 16),
-                            n_slots=4 if a.xtc_decode == "gpu" else 3)
+                            n_slots=3)
         else:
             src = HostSource(host, None, batch_frames=a.stager_batch, n_threads=a.stager_threads, offset=b0,
                              n_traj=n_total)

@@ -80,8 +80,8 @@ constexpr int32_t kOk = 0, kShort = 1, kBadMagic = 2, kBadNatoms = 3, kBadHeader
 
 __host__ __device__ inline uint32_t be32w(uint32_t w) { return __builtin_bswap32(w); }
 
-// MSB-first bit reader: Src supplies the record's big-endian words in order
-// (word()); `acc` keeps up to 64 bits.  Past the stream's words Src yields
+// MSB-first bit reader: Src supplies the record's words in order, already
+// byte-swapped from XDR's big-endian (word()); `acc` keeps up to 64 bits.  Past the stream's words Src yields
 // zeros, and `left` goes negative: an overrun is checked once per atom.
 template <class Src>
 struct Bits {
@@ -93,7 +93,7 @@ struct Bits {
   __host__ __device__ inline uint32_t get(int k) {  // 0 <= k <= 32
     left -= k;
     if (n < k) {
-      acc = (acc << 32) | be32w(src.word());
+      acc = (acc << 32) | src.word();
       n += 32;
     }
     n -= k;
@@ -108,7 +108,7 @@ struct MemWords {
     w = p;
     wend = p + n_words;
   }
-  __host__ __device__ inline uint32_t word() { return w < wend ? *w++ : 0u; }
+  __host__ __device__ inline uint32_t word() { return w < wend ? be32w(*w++) : 0u; }
 };
 
 // device, one wave per frame: every lane runs the (uniform) decoder; the
@@ -125,14 +125,14 @@ struct WaveWords {
     nw = n_words;
     wi = 0;
     lane = (int)(threadIdx.x & 63);
-    cur = lane < nw ? p[lane] : 0u;
-    nxt = 64 + lane < nw ? p[64 + lane] : 0u;
+    cur = lane < nw ? be32w(p[lane]) : 0u;
+    nxt = 64 + lane < nw ? p[64 + lane] : 0u;  // swapped when it becomes current
   }
   __device__ inline uint32_t word() {
     const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)(wi & 63));
     ++wi;
     if ((wi & 63) == 0) {
-      cur = nxt;
+      cur = be32w(nxt);
       const int64_t j = wi + 64 + lane;
       nxt = j < nw ? s[j] : 0u;
     }
@@ -328,25 +328,39 @@ struct MemSink {
 struct WaveSink {
   float *o;  // next group's first atom
   int k;
-  uint32_t vx, vy, vz;
-  __device__ inline void put(int c0, int c1, int c2, float invp) {
-    float a, b, c;
-    to_angstrom(c0, c1, c2, invp, a, b, c);
-    put_f(a, b, c);
+  uint32_t vx, vy, vz;  // lane j: atom j of the group (integers, or f32 bits)
+  float invp;
+  bool raw;
+  __device__ inline void put(int c0, int c1, int c2, float inv_precision) {
+    invp = inv_precision;
+    keep((uint32_t)c0, (uint32_t)c1, (uint32_t)c2);
   }
   __device__ inline void put_f(float a, float b, float c) {
+    raw = true;
+    keep(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, c));
+  }
+  __device__ inline void keep(uint32_t a, uint32_t b, uint32_t c) {
     const bool mine = (int)(threadIdx.x & 63) == k;
-    vx = mine ? __builtin_bit_cast(uint32_t, a) : vx;
-    vy = mine ? __builtin_bit_cast(uint32_t, b) : vy;
-    vz = mine ? __builtin_bit_cast(uint32_t, c) : vz;
+    vx = mine ? a : vx;
+    vy = mine ? b : vy;
+    vz = mine ? c : vz;
     if (++k == 64) flush();
   }
+  // the group's integer -> Angstrom conversions run lane-parallel here
   __device__ inline void flush() {
     const int lane = (int)(threadIdx.x & 63);
     if (lane < k) {
-      o[3 * lane] = __builtin_bit_cast(float, vx);
-      o[3 * lane + 1] = __builtin_bit_cast(float, vy);
-      o[3 * lane + 2] = __builtin_bit_cast(float, vz);
+      float a, b, c;
+      if (raw) {
+        a = __builtin_bit_cast(float, vx);
+        b = __builtin_bit_cast(float, vy);
+        c = __builtin_bit_cast(float, vz);
+      } else {
+        to_angstrom((int)vx, (int)vy, (int)vz, invp, a, b, c);
+      }
+      o[3 * lane] = a;
+      o[3 * lane + 1] = b;
+      o[3 * lane + 2] = c;
     }
     o += 3 * k;
     k = 0;
@@ -493,7 +507,7 @@ __global__ __launch_bounds__(64) void k_xtc_decode(const uint32_t *__restrict__ 
                                                    int32_t *__restrict__ status) {
   const int64_t f = blockIdx.x;
   float *o = out + f * out_stride;
-  WaveSink sink{o, 0, 0u, 0u, 0u};
+  WaveSink sink{o, 0, 0u, 0u, 0u, 1.0f, false};
   const int32_t st = decode_record<WaveWords>(words + rec_off[f], rec_len[f], n_atoms, sink, g_magic.v, g_inv.v);
   if (st != kOk) {
     for (int64_t k = threadIdx.x; k < 3 * n_atoms; k += 64) o[k] = __builtin_nanf("");

@@ -224,11 +224,12 @@ class XtcSource:
     the host).  ``decode="gpu"``: the compressed frame records are read into
     pinned slots, copied to HBM and decompressed there, one wave per frame
     (csrc/xtc_gpu.hip); up to ``n_slots`` batches decode concurrently ahead
-    of the consumer.  ``decode="host"``: frames are decoded frame-parallel on
+    of the consumer (3 slots: one hardware queue each beside the consumer's,
+    HIP's default being 4 per process).  ``decode="host"``: frames are decoded frame-parallel on
     ``n_threads`` host threads straight into the stager's pinned slots
     (selection applied) and DMA'd.  Both give the same float32 frames."""
 
-    def __init__(self, path, sel=None, batch_frames: int | None = None, n_slots: int = 3, n_threads: int = 8,
+    def __init__(self, path, sel=None, batch_frames: int | None = None, n_slots: int = 3, n_threads: int = 16,
                  decode: str = "gpu"):
         from .xtc import XTCFile
 
