@@ -7,9 +7,10 @@
 // into a pinned slot (pread, host threads), copied to HBM (about 1/6 of the
 // decoded bytes), and decompressed on the device -- the xdr3dfcoord stream of
 // one frame is strictly sequential, so a frame is one wave's work (the
-// decoder state is wave-uniform; the wave fetches the stream 256 B at a time
-// with the next chunk in flight, and stores 64 decoded atoms at a time) and
-// frames run in parallel, one wave each.  Output: float32 [n][n_atoms][3] Angstrom frames in HBM with
+// decoder state is wave-uniform; the wave holds a 256-B window of the stream
+// in its lanes with the next one in flight, reads any field up to 64 bits
+// with three readlanes and shifts, and stores 64 decoded atoms at a time)
+// and frames run in parallel, one wave each.  Output: float32 [n][n_atoms][3] Angstrom frames in HBM with
 // MDAnalysis' rounding f32(f32(int * f32(1/prec)) * 10), bit-identical to the
 // host decoder.  The selection is applied downstream (the accumulate
 // kernels gather it in-kernel), as for any HBM-resident trajectory.
@@ -80,117 +81,123 @@ constexpr int32_t kOk = 0, kShort = 1, kBadMagic = 2, kBadNatoms = 3, kBadHeader
 
 __host__ __device__ inline uint32_t be32w(uint32_t w) { return __builtin_bswap32(w); }
 
-// MSB-first bit reader: Src supplies the record's words in order, already
-// byte-swapped from XDR's big-endian (word()); `acc` keeps up to 64 bits.  Past the stream's words Src yields
-// zeros, and `left` goes negative: an overrun is checked once per atom.
-template <class Src>
-struct Bits {
-  Src src;
-  uint64_t acc = 0;
-  int n = 0;         // valid bits in the low end of acc
-  int64_t left = 0;  // bits left in the stream (< 0: overrun)
-  __host__ __device__ inline bool bad() const { return left < 0; }
-  __host__ __device__ inline uint32_t get(int k) {  // 0 <= k <= 32
-    left -= k;
-    if (n < k) {
-      acc = (acc << 32) | src.word();
-      n += 32;
-    }
-    n -= k;
-    return (uint32_t)(acc >> n) & (uint32_t)((1ull << k) - 1ull);
-  }
-};
+// ---- bit windows ------------------------------------------------------------
+// A window yields the 64 stream bits at its read position, MSB first
+// (peek64), and advances (skip).  Words past the stream read as 0;
+// consumed() > 8*nbytes flags an overrun, checked once per atom.  Both reads
+// are branch-free: of the 96 bits w0:w1:w2 around the position, bits
+// [sh, sh+64) are (w0:w1 << sh) | ((w1:w2 << sh) >> 32).
+__host__ __device__ inline uint64_t bits64(uint32_t w0, uint32_t w1, uint32_t w2, int sh) {
+  const uint64_t hi = (uint64_t)w0 << 32 | w1, lo = (uint64_t)w1 << 32 | w2;
+  return (hi << sh) | ((lo << sh) >> 32);
+}
 
-// host: the words straight from memory
-struct MemWords {
-  const uint32_t *w, *wend;
-  __host__ __device__ inline void start(const uint32_t *p, int64_t n_words) {
-    w = p;
-    wend = p + n_words;
-  }
-  __host__ __device__ inline uint32_t word() { return w < wend ? be32w(*w++) : 0u; }
-};
-
-// device, one wave per frame: every lane runs the (uniform) decoder; the
-// stream is fetched 64 words (256 B) at a time by the whole wave, lane j
-// holding word j of the chunk, and read back with readlane.  The next chunk
-// is always in flight, so the load latency hides behind ~50 atoms of decode.
-struct WaveWords {
+// host: straight from memory
+struct MemWindow {
   const uint32_t *s;
-  int64_t nw, wi;
+  int64_t nw, pos;
+  __host__ __device__ inline void start(const uint32_t *p, int64_t n_words) {
+    s = p;
+    nw = n_words;
+    pos = 0;
+  }
+  __host__ __device__ inline uint32_t at(int64_t j) const { return j < nw ? be32w(s[j]) : 0u; }
+  __host__ __device__ inline uint64_t peek64() const {
+    const int64_t i = pos >> 5;
+    return bits64(at(i), at(i + 1), at(i + 2), (int)(pos & 31));
+  }
+  __host__ __device__ inline void skip(int k) { pos += k; }
+  __host__ __device__ inline int64_t consumed() const { return pos; }
+};
+
+// device, one wave per frame: every lane runs the (uniform) decoder.  Lane j
+// holds stream word w0+j (cur, byte-swapped) and word w0+60+j (nxt, raw, in
+// flight); reads take words w0+i..w0+i+2 with readlane, i <= 61, and the
+// window slides by 60 words once the position passes word 60 -- so the
+// next chunk's load hides behind ~40 atoms of decode.
+struct WaveWindow {
+  const uint32_t *s;
+  int64_t nw, w0;
   uint32_t cur, nxt;
+  int pos;  // bit offset from word w0, < 1920 between calls
   int lane;
   __device__ inline void start(const uint32_t *p, int64_t n_words) {
     s = p;
     nw = n_words;
-    wi = 0;
+    w0 = 0;
+    pos = 0;
     lane = (int)(threadIdx.x & 63);
     cur = lane < nw ? be32w(p[lane]) : 0u;
-    nxt = 64 + lane < nw ? p[64 + lane] : 0u;  // swapped when it becomes current
+    nxt = 60 + lane < nw ? p[60 + lane] : 0u;
   }
-  __device__ inline uint32_t word() {
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)(wi & 63));
-    ++wi;
-    if ((wi & 63) == 0) {
+  __device__ inline uint32_t word(int i) const { return (uint32_t)__builtin_amdgcn_readlane((int)cur, i); }
+  __device__ inline uint64_t peek64() const {
+    const int i = pos >> 5;
+    return bits64(word(i), word(i + 1), word(i + 2), pos & 31);
+  }
+  __device__ inline void skip(int k) {  // k <= 64
+    pos += k;
+    if (pos >= 60 * 32) {
+      pos -= 60 * 32;
+      w0 += 60;
       cur = be32w(nxt);
-      const int64_t j = wi + 64 + lane;
+      const int64_t j = w0 + 60 + lane;
       nxt = j < nw ? s[j] : 0u;
     }
-    return w;
   }
+  __device__ inline int64_t consumed() const { return 32 * w0 + pos; }
 };
 
-// receiveints' byte order: the packed value's bytes arrive least significant
-// first (8 bits each), the last (1..8 bits) carrying the top.  nbits <= 64.
-template <class B>
-__host__ __device__ inline uint64_t read_packed(B &b, int nbits) {
-  int q = (nbits - 1) >> 3;
-  const int last = nbits - 8 * q;
-  uint64_t v = 0;
-  int sh = 0;
-  while (q >= 4) {
-    v |= (uint64_t)be32w(b.get(32)) << sh;
-    sh += 32;
-    q -= 4;
-  }
-  if (q > 0) {
-    v |= (uint64_t)(be32w(b.get(8 * q)) >> (32 - 8 * q)) << sh;
-    sh += 8 * q;
-  }
-  v |= (uint64_t)b.get(last) << sh;
+template <class W>
+__host__ __device__ inline uint64_t take(W &w, int k) {  // 1 <= k <= 64
+  const uint64_t v = w.peek64() >> (64 - k);
+  w.skip(k);
   return v;
 }
 
-// value = (n0*s1 + n1)*s2 + n2, value < 2^52: exact double arithmetic.
+// receiveints' byte order: the packed value's bytes arrive least significant
+// first (8 bits each), the last (1..8 bits) carrying the top.  One read of
+// all nbits (<= 64), then the q full bytes are reversed.
+__host__ __device__ inline uint64_t unpack(uint64_t x, int nbits) {  // x: the nbits as read, MSB first
+  const int q = (nbits - 1) >> 3, r = nbits - 8 * q;  // q full bytes, r (1..8) top bits
+  const uint64_t top = x & ((1ull << r) - 1ull);
+  const uint64_t low = (__builtin_bswap64(x >> r) >> (63 - 8 * q)) >> 1;
+  return (top << (8 * q)) | low;
+}
+
+template <class W>
+__host__ __device__ inline uint64_t read_packed(W &w, int nbits) {
+  return unpack(take(w, nbits), nbits);
+}
+
+// value = (n0*s1 + n1)*s2 + n2, value < 2^52: exact double arithmetic, the
+// quotient estimate corrected by at most one, without branches.
 __host__ __device__ inline void split_f64(uint64_t v, const unsigned s[3], const double inv[3], int out[3]) {
   double d = (double)v;
   for (int i = 2; i >= 1; --i) {
+    const double si = (double)s[i];
     double q = floor(d * inv[i]);
-    double r = fma(-q, (double)s[i], d);  // exact: |r| < 2 s
-    if (r < 0.0) {
-      q -= 1.0;
-      r += (double)s[i];
-    } else if (r >= (double)s[i]) {
-      q += 1.0;
-      r -= (double)s[i];
-    }
+    double r = fma(-q, si, d);  // exact: |r| < 2 s
+    const double adj = (r >= si ? 1.0 : 0.0) - (r < 0.0 ? 1.0 : 0.0);
+    q += adj;
+    r = fma(-adj, si, r);
     out[i] = (int)r;
     d = q;
   }
-  out[0] = (int)(uint32_t)(uint64_t)d;
+  out[0] = (int)fmin(d, 2147483647.0);  // < s0 <= 2^24 for a valid stream
 }
 
 // the published byte-wise long division, for packed values wider than 52 bits
-template <class B>
-__host__ __device__ inline bool split_bytes(B &b, int nbits, const unsigned s[3], int out[3]) {
+template <class W>
+__host__ __device__ inline bool split_bytes(W &w, int nbits, const unsigned s[3], int out[3]) {
   if (nbits > 96 || s[1] == 0 || s[2] == 0 || s[1] > (1u << 24) || s[2] > (1u << 24)) return false;
   unsigned bytes[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   int nb = 0;
   while (nbits > 8) {
-    bytes[nb++] = b.get(8);
+    bytes[nb++] = (unsigned)take(w, 8);
     nbits -= 8;
   }
-  if (nbits > 0) bytes[nb++] = b.get(nbits);
+  if (nbits > 0) bytes[nb++] = (unsigned)take(w, nbits);
   for (int i = 2; i > 0; --i) {
     unsigned num = 0;
     for (int j = nb - 1; j >= 0; --j) {
@@ -205,14 +212,13 @@ __host__ __device__ inline bool split_bytes(B &b, int nbits, const unsigned s[3]
   return true;
 }
 
-template <class B>
-__host__ __device__ inline bool read_triple(B &b, int nbits, const unsigned s[3], const double inv[3],
-                                            int out[3]) {
+template <class W>
+__host__ __device__ inline bool read_triple(W &w, int nbits, const unsigned s[3], const double inv[3], int out[3]) {
   if (nbits <= 52) {
-    split_f64(read_packed(b, nbits), s, inv, out);
+    split_f64(read_packed(w, nbits), s, inv, out);
     return true;
   }
-  return split_bytes(b, nbits, s, out);
+  return split_bytes(w, nbits, s, out);
 }
 
 __host__ __device__ inline int sizeofint_hd(unsigned size) {
@@ -253,49 +259,6 @@ __host__ __device__ inline int sizeofints_hd(const unsigned sizes[3]) {
 }
 
 __host__ __device__ inline float f32_bits(uint32_t u) { return __builtin_bit_cast(float, u); }
-
-// device, one lane per frame: the lane fetches its own stream 16 B at a
-// time (four dword loads) with the next 16 B already in flight.
-struct LaneWords {
-  const uint32_t *s;
-  int64_t nw, wi;  // wi: next word to fetch
-  uint32_t q0, q1, q2, q3, p0, p1, p2, p3;
-  int cnt;
-  __device__ inline uint32_t at(int64_t j) const { return j < nw ? s[j] : 0u; }
-  __device__ inline void start(const uint32_t *p, int64_t n_words) {
-    s = p;
-    nw = n_words;
-    q0 = at(0);
-    q1 = at(1);
-    q2 = at(2);
-    q3 = at(3);
-    p0 = at(4);
-    p1 = at(5);
-    p2 = at(6);
-    p3 = at(7);
-    wi = 8;
-    cnt = 4;
-  }
-  __device__ inline uint32_t word() {
-    const uint32_t w = q0;
-    q0 = q1;
-    q1 = q2;
-    q2 = q3;
-    if (--cnt == 0) {
-      q0 = p0;
-      q1 = p1;
-      q2 = p2;
-      q3 = p3;
-      p0 = at(wi);
-      p1 = at(wi + 1);
-      p2 = at(wi + 2);
-      p3 = at(wi + 3);
-      wi += 4;
-      cnt = 4;
-    }
-    return w;
-  }
-};
 
 // xdrfile scales to nm in f32; MDAnalysis then multiplies by 10 in f32
 __host__ __device__ inline void to_angstrom(int c0, int c1, int c2, float invp, float &a, float &b, float &c) {
@@ -369,8 +332,8 @@ struct WaveSink {
 
 // Decode one XTC frame record (starting at its magic word, `words` long)
 // into n_atoms Angstrom triples through `sink`.  Mirrors decode_coords() of
-// xtc.cpp.  Src: MemWords (host) or WaveWords (device, one wave per frame).
-template <class Src, class Sink>
+// xtc.cpp.  W: MemWindow (host) or WaveWindow (device, one wave per frame).
+template <class W, class Sink>
 __host__ __device__ int32_t decode_record(const uint32_t *rec, int64_t words, int64_t n_atoms, Sink &sink,
                                           const int *magic, const double *inv_magic) {
 #pragma clang fp contract(off)
@@ -421,21 +384,23 @@ __host__ __device__ int32_t decode_record(const uint32_t *rec, int64_t words, in
   invsmall[0] = invsmall[1] = invsmall[2] = inv_magic[smallidx];
   const float inv_precision = (float)(1.0 / (double)precision);
 
-  Bits<Src> b;
-  const int64_t nw = ((int64_t)nbytes + 3) / 4;
-  b.src.start(p, nw);
-  b.left = 8 * (int64_t)nbytes;
+  W b;
+  b.start(p, ((int64_t)nbytes + 3) / 4);
+  const int64_t nbits = 8 * (int64_t)nbytes;
   int prev[3] = {0, 0, 0};
   int run = 0, i = 0;
   while (i < natoms) {
     int cur[3];
     if (bitsize == 0) {
-      cur[0] = (int)b.get(bitsizeint[0]);
-      cur[1] = (int)b.get(bitsizeint[1]);
-      cur[2] = (int)b.get(bitsizeint[2]);
+      cur[0] = (int)take(b, bitsizeint[0]);
+      cur[1] = (int)take(b, bitsizeint[1]);
+      cur[2] = (int)take(b, bitsizeint[2]);
     } else if (!read_triple(b, bitsize, sizeint, invint, cur)) {
       return kCorrupt;
     }
+    // flag bit, then (flag set) a 5-bit run code: one peek, no branch
+    const uint32_t p6 = (uint32_t)(b.peek64() >> 58);
+    b.skip((p6 >> 5) ? 6 : 1);
     i++;
     cur[0] += minint[0];
     cur[1] += minint[1];
@@ -443,13 +408,10 @@ __host__ __device__ int32_t decode_record(const uint32_t *rec, int64_t words, in
     prev[0] = cur[0];
     prev[1] = cur[1];
     prev[2] = cur[2];
-    int is_smaller = 0;
-    if (b.get(1)) {
-      run = (int)b.get(5);
-      is_smaller = run % 3;
-      run -= is_smaller;
-      is_smaller--;
-    }
+    const bool flag = (p6 >> 5) != 0;
+    const int rc = (int)(p6 & 31), rm = rc % 3;
+    run = flag ? rc - rm : run;
+    const int is_smaller = flag ? rm - 1 : 0;
     if (run > 0) {
       if (i + run / 3 > natoms || sizesmall[0] == 0) return kCorrupt;
       for (int k = 0; k < run; k += 3) {
@@ -491,10 +453,10 @@ __host__ __device__ int32_t decode_record(const uint32_t *rec, int64_t words, in
       sizesmall[0] = sizesmall[1] = sizesmall[2] = magic[smallidx];
       invsmall[0] = invsmall[1] = invsmall[2] = inv_magic[smallidx];
     }
-    if (b.bad()) return kCorrupt;
+    if (b.consumed() > nbits) return kCorrupt;
   }
   sink.flush();
-  return b.bad() ? kCorrupt : kOk;
+  return kOk;
 }
 
 // One wave per frame (grid = n_frames blocks of 64): the decoder state is
@@ -508,37 +470,11 @@ __global__ __launch_bounds__(64) void k_xtc_decode(const uint32_t *__restrict__ 
   const int64_t f = blockIdx.x;
   float *o = out + f * out_stride;
   WaveSink sink{o, 0, 0u, 0u, 0u, 1.0f, false};
-  const int32_t st = decode_record<WaveWords>(words + rec_off[f], rec_len[f], n_atoms, sink, g_magic.v, g_inv.v);
+  const int32_t st = decode_record<WaveWindow>(words + rec_off[f], rec_len[f], n_atoms, sink, g_magic.v, g_inv.v);
   if (st != kOk) {
     for (int64_t k = threadIdx.x; k < 3 * n_atoms; k += 64) o[k] = __builtin_nanf("");
   }
   if (threadIdx.x == 0) status[f] = st;
-}
-
-// One lane per frame, `lpw` frames per wave (the other lanes idle).
-__global__ __launch_bounds__(64) void k_xtc_decode_lanes(const uint32_t *__restrict__ words,
-                                                         const int64_t *__restrict__ rec_off,
-                                                         const int64_t *__restrict__ rec_len, int64_t n_frames,
-                                                         int64_t n_atoms, float *__restrict__ out,
-                                                         int64_t out_stride, int32_t *__restrict__ status,
-                                                         int lpw) {
-  const int lane = threadIdx.x;
-  if (lane >= lpw) return;
-  const int64_t f = (int64_t)blockIdx.x * lpw + lane;
-  if (f >= n_frames) return;
-  float *o = out + f * out_stride;
-  MemSink sink{o};
-  const int32_t st = decode_record<LaneWords>(words + rec_off[f], rec_len[f], n_atoms, sink, g_magic.v, g_inv.v);
-  if (st != kOk) {
-    for (int64_t k = 0; k < 3 * n_atoms; ++k) o[k] = __builtin_nanf("");
-  }
-  status[f] = st;
-}
-
-int simd_count() {
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  return 4 * std::max(1, cus);
 }
 
 const char *status_text(int32_t s) {
@@ -639,26 +575,6 @@ RMSF_EXPORT int rmsf_xtc_decode_records(const void *d_records, const int64_t *d_
   return RMSF_OK;
 }
 
-// benchmarking hook (not in the public header): mode 0 = one wave per frame,
-// mode k >= 1 = one lane per frame with k frames per wave (-1: automatic)
-RMSF_EXPORT int rmsf_internal_xtc_decode_mode(const void *d_records, const int64_t *d_rec_off,
-                                              const int64_t *d_rec_len, int64_t n_frames, int64_t n_atoms,
-                                              float *d_out, int64_t out_stride, int32_t *d_status, int mode,
-                                              void *stream) {
-  if (mode == 0)
-    return rmsf_xtc_decode_records(d_records, d_rec_off, d_rec_len, n_frames, n_atoms, d_out, out_stride, d_status,
-                                   stream);
-  int lpw = mode;
-  if (lpw < 0) lpw = (int)std::max<int64_t>(1, std::min<int64_t>(64, (n_frames + simd_count() - 1) / simd_count()));
-  lpw = std::min(lpw, 64);
-  const int64_t blocks = (n_frames + lpw - 1) / lpw;
-  hipLaunchKernelGGL(k_xtc_decode_lanes, dim3((unsigned)blocks), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
-                     static_cast<const uint32_t *>(d_records), d_rec_off, d_rec_len, n_frames, n_atoms, d_out,
-                     out_stride, d_status, lpw);
-  XD_HIP(hipGetLastError());
-  return RMSF_OK;
-}
-
 RMSF_EXPORT int rmsf_xtc_decode_records_host(const void *h_records, const int64_t *h_rec_off,
                                              const int64_t *h_rec_len, int64_t n_frames, int64_t n_atoms,
                                              float *h_out, int64_t out_stride, int32_t *h_status) {
@@ -668,7 +584,7 @@ RMSF_EXPORT int rmsf_xtc_decode_records_host(const void *h_records, const int64_
   const uint32_t *w = static_cast<const uint32_t *>(h_records);
   for (int64_t f = 0; f < n_frames; ++f) {
     MemSink sink{h_out + f * out_stride};
-    h_status[f] = decode_record<MemWords>(w + h_rec_off[f], h_rec_len[f], n_atoms, sink, h_magic.v, h_inv.v);
+    h_status[f] = decode_record<MemWindow>(w + h_rec_off[f], h_rec_len[f], n_atoms, sink, h_magic.v, h_inv.v);
   }
   return RMSF_OK;
 }

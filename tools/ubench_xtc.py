@@ -1,7 +1,8 @@
-"""GPU XTC decode strategies (not product code): one wave per frame (mode 0)
-vs one lane per frame with k frames per wave (mode k; -1 = automatic), on
-250k-atom frames.  K distinct frames are written once; the record table
-points at them cyclically so N frames decode from device memory.
+"""GPU XTC decode throughput (not product code): rmsf_xtc_decode_records on
+250k-atom frames, one wave per frame.  K distinct frames are written once;
+the record table points at them cyclically so N frames decode from device
+memory.  (Round 1 also measured one LANE per frame, 1-64 frames per wave:
+slower below ~8k frames -- profiles/r01_workloads/ubench_xtc_decode.txt.)
     python tools/ubench_xtc.py [N ...]"""
 import ctypes
 import os
@@ -32,10 +33,9 @@ def water_like(rng, n_atoms, n_frames):
 def main():
     ns = [int(a) for a in sys.argv[1:]] or [400, 4096]
     lib = load()
-    lib.rmsf_internal_xtc_decode_mode.restype = ctypes.c_int
     n_atoms, K = 250_000, 32
     dev = torch.device("cuda")
-    for kind in ("uniform", "water"):
+    for kind in os.environ.get("UB_KINDS", "uniform,water").split(","):
         x = SY.frames(0, n_atoms, 0, K) if kind == "uniform" else water_like(np.random.default_rng(1), n_atoms, K)
         path = os.path.join(tempfile.mkdtemp(), "u.xtc")
         write_xtc(path, x)
@@ -49,13 +49,13 @@ def main():
             out = torch.empty((N, n_atoms, 3), dtype=torch.float32, device=dev)
             st = torch.empty(N, dtype=torch.int32, device=dev)
             ref = None
-            for mode in (0, -1, 1, 4, 16, 64):
+            for mode in (0,):
                 def go():
-                    rc = lib.rmsf_internal_xtc_decode_mode(
+                    rc = lib.rmsf_xtc_decode_records(
                         ctypes.c_void_p(words.data_ptr()), ctypes.c_void_p(off.data_ptr()),
                         ctypes.c_void_p(ln.data_ptr()), ctypes.c_int64(N), ctypes.c_int64(n_atoms),
                         ctypes.c_void_p(out.data_ptr()), ctypes.c_int64(3 * n_atoms), ctypes.c_void_p(st.data_ptr()),
-                        ctypes.c_int(mode), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                        ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
                     assert rc == 0
                 go()
                 torch.cuda.synchronize()
