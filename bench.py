@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--stager-batch", type=int, default=None, help="c5: frames per staged batch")
     ap.add_argument("--xtc-decode", choices=["gpu", "host"], default="gpu",
                     help="c5xtc: decompress the XTC records on the GPU (default) or on host threads")
+    ap.add_argument("--xtc-cache", action="store_true",
+                    help="c5xtc (GPU decode): keep decoded frames in HBM within a step (RMSF.py's second sweep "
+                         "reads them from HBM); dropped before every step, so each step decodes once")
     ap.add_argument("--align", choices=["none", "frame0", "average"], default=None, help="override the workload's")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo only "
                                                      "to rehearse several ranks on one GPU)")
@@ -222,7 +225,7 @@ def main():
             del host
             src = XtcSource(xtc_path, None, batch_frames=a.stager_batch, decode=a.xtc_decode,
                             n_threads=a.stager_threads if a.xtc_decode == "host" else max(a.stager_threads, 16),
-                            n_slots=3)
+                            n_slots=3, cache=a.xtc_cache)
         else:
             src = HostSource(host, None, batch_frames=a.stager_batch, n_threads=a.stager_threads, offset=b0,
                              n_traj=n_total)
@@ -231,6 +234,8 @@ def main():
     fl = FrameList(n_total)
 
     def run(align, timer=None):
+        if hasattr(src, "drop_cache"):
+            src.drop_cache()  # every step streams the file again
         return run_pipeline(eng, src, fl, align=align, block=(b0, b1), ref_owner=0, n_splits=a.splits,
                             max_batch=a.batch_frames, timer=timer)
 
@@ -299,7 +304,8 @@ def main():
                          "threads": a.stager_threads, "batch_frames": src.batch_frames,
                          "host_link_spec_gbs": 63.0}
         if wl.get("xtc"):
-            out["stager"].update(xtc_decode=a.xtc_decode, xtc_bytes=os.path.getsize(xtc_path), xtc_write_s=t_w,
+            out["stager"].update(xtc_decode=a.xtc_decode, xtc_cache=a.xtc_cache,
+                                 xtc_bytes=os.path.getsize(xtc_path), xtc_write_s=t_w,
                                  xtc_frames_per_s=n_local * a.steps / dt,
                                  xtc_gb_per_s_compressed=os.path.getsize(xtc_path) * a.steps / dt / 1e9)
         out["roofline"]["note"] = "C5 is PCIe/host bound; the kernel roofline above is the device-side launch"

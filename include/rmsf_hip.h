@@ -256,6 +256,11 @@ int rmsf_xtcdec_destroy(rmsf_xtcdec *d);
 int rmsf_xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n_frames,
                        int64_t step, void *consumer_stream, int *slot,
                        float **d_frames);
+/* The same into the caller's device buffer: frame k of the batch at
+ * d_out + k*out_stride floats (e.g. a trajectory kept resident in HBM). */
+int rmsf_xtcdec_decode_into(rmsf_xtcdec *d, int64_t f0, int64_t n_frames,
+                            int64_t step, float *d_out, int64_t out_stride,
+                            void *consumer_stream, int *slot);
 /* The slot may be reused once the work queued so far on consumer_stream ends. */
 int rmsf_xtcdec_release(rmsf_xtcdec *d, int slot, void *consumer_stream);
 /* Wait for every outstanding decode; first per-frame error, if any. */

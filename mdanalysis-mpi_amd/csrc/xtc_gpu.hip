@@ -601,7 +601,6 @@ RMSF_EXPORT int rmsf_xtcdec_create(const rmsf_xtc *x, int64_t batch_frames, int 
   d->n_threads = n_threads;
   d->slots.resize(n_slots);
   const size_t raw = (size_t)batch_frames * (size_t)x->max_size;
-  const size_t frames = (size_t)batch_frames * 3 * (size_t)x->n_atoms * sizeof(float);
   for (auto &s : d->slots) {
     s.raw_cap = raw;
     hipError_t e = hipHostMalloc((void **)&s.h_raw, raw, hipHostMallocDefault);
@@ -610,7 +609,6 @@ RMSF_EXPORT int rmsf_xtcdec_create(const rmsf_xtc *x, int64_t batch_frames, int 
     if (e == hipSuccess) e = hipMalloc((void **)&s.d_raw, raw);
     if (e == hipSuccess) e = hipMalloc((void **)&s.d_tab, 2 * batch_frames * sizeof(int64_t));
     if (e == hipSuccess) e = hipMalloc((void **)&s.d_status, batch_frames * sizeof(int32_t));
-    if (e == hipSuccess) e = hipMalloc((void **)&s.d_frames, frames);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.released, hipEventDisableTiming);
@@ -634,11 +632,15 @@ RMSF_EXPORT int rmsf_xtcdec_destroy(rmsf_xtcdec *d) {
   return RMSF_OK;
 }
 
-RMSF_EXPORT int rmsf_xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_t step, void *consumer_stream,
-                                   int *slot, float **d_frames) {
-  if (!d || !slot || !d_frames || n < 1 || n > d->batch || step < 1 || f0 < 0 ||
-      f0 + (n - 1) * step >= (int64_t)d->x->offset.size())
-    return fail(RMSF_EINVAL, "rmsf_xtcdec_decode: bad arguments");
+}  // extern "C"
+
+namespace {
+
+// out == nullptr: into the slot's own frame buffer (allocated on first use),
+// reused once the consumer released the slot; otherwise into the caller's
+// buffer, frame k at out + k*out_stride.
+int xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_t step, float *out, int64_t out_stride,
+                  void *consumer_stream, int *slot, float **d_frames) {
   const int si = d->next;
   d->next = (d->next + 1) % (int)d->slots.size();
   auto &s = d->slots[si];
@@ -680,9 +682,18 @@ RMSF_EXPORT int rmsf_xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_
   }
   XD_HIP(hipMemcpyAsync(s.d_raw, s.h_raw, total, hipMemcpyHostToDevice, s.s));
   XD_HIP(hipMemcpyAsync(s.d_tab, s.h_tab, 2 * d->batch * sizeof(int64_t), hipMemcpyHostToDevice, s.s));
-  XD_HIP(hipStreamWaitEvent(s.s, s.released, 0));  // the consumer is done with the previous frames
-  rc = rmsf_xtc_decode_records(s.d_raw, s.d_tab, s.d_tab + d->batch, n, d->n_atoms, s.d_frames, 3 * d->n_atoms,
-                               s.d_status, s.s);
+  if (!out) {
+    if (!s.d_frames) {
+      const size_t bytes = (size_t)d->batch * 3 * (size_t)d->n_atoms * sizeof(float);
+      hipError_t e = hipMalloc((void **)&s.d_frames, bytes);
+      if (e != hipSuccess) return fail(RMSF_ENOMEM, std::string("rmsf_xtcdec_decode: ") + hipGetErrorString(e));
+    }
+    XD_HIP(hipStreamWaitEvent(s.s, s.released, 0));  // the consumer is done with the previous frames
+    out = s.d_frames;
+    out_stride = 3 * d->n_atoms;
+  }
+  rc = rmsf_xtc_decode_records(s.d_raw, s.d_tab, s.d_tab + d->batch, n, d->n_atoms, out, out_stride, s.d_status,
+                               s.s);
   if (rc) return rc;
   XD_HIP(hipMemcpyAsync(s.h_status, s.d_status, n * sizeof(int32_t), hipMemcpyDeviceToHost, s.s));
   XD_HIP(hipEventRecord(s.done, s.s));
@@ -691,8 +702,28 @@ RMSF_EXPORT int rmsf_xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_
   s.f0 = f0;
   s.step = step;
   *slot = si;
-  *d_frames = s.d_frames;
+  if (d_frames) *d_frames = out;
   return RMSF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+RMSF_EXPORT int rmsf_xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_t step, void *consumer_stream,
+                                   int *slot, float **d_frames) {
+  if (!d || !slot || !d_frames || n < 1 || n > d->batch || step < 1 || f0 < 0 ||
+      f0 + (n - 1) * step >= (int64_t)d->x->offset.size())
+    return fail(RMSF_EINVAL, "rmsf_xtcdec_decode: bad arguments");
+  return xtcdec_decode(d, f0, n, step, nullptr, 0, consumer_stream, slot, d_frames);
+}
+
+RMSF_EXPORT int rmsf_xtcdec_decode_into(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_t step, float *d_out,
+                                        int64_t out_stride, void *consumer_stream, int *slot) {
+  if (!d || !slot || !d_out || out_stride < 3 * d->n_atoms || n < 1 || n > d->batch || step < 1 || f0 < 0 ||
+      f0 + (n - 1) * step >= (int64_t)d->x->offset.size())
+    return fail(RMSF_EINVAL, "rmsf_xtcdec_decode_into: bad arguments");
+  return xtcdec_decode(d, f0, n, step, d_out, out_stride, consumer_stream, slot, nullptr);
 }
 
 RMSF_EXPORT int rmsf_xtcdec_release(rmsf_xtcdec *d, int slot, void *consumer_stream) {

@@ -82,6 +82,7 @@ SIGNATURES = {
     "rmsf_xtcdec_create": (c_int, [P, c_int64, c_int, c_int, POINTER(c_void_p)]),
     "rmsf_xtcdec_destroy": (c_int, [P]),
     "rmsf_xtcdec_decode": (c_int, [P, c_int64, c_int64, c_int64, P, POINTER(c_int), POINTER(c_void_p)]),
+    "rmsf_xtcdec_decode_into": (c_int, [P, c_int64, c_int64, c_int64, P, c_int64, P, POINTER(c_int)]),
     "rmsf_xtcdec_release": (c_int, [P, c_int, P]),
     "rmsf_xtcdec_synchronize": (c_int, [P]),
     "rmsf_xtc_decode_records": (c_int, [P, P, P, c_int64, c_int64, P, c_int64, P, P]),

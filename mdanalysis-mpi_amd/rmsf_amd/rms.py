@@ -124,7 +124,9 @@ class RMSF:
             path = os.fspath(x)
             if not str(path).lower().endswith(".xtc"):
                 raise ValueError(f"only .xtc trajectory files are read natively, got {path!r}")
-            return XtcSource(path, self.select, batch_frames=self.batch_frames), self.masses
+            # RMSF.py's two sweeps read every frame twice: keep the decoded frames in HBM
+            return XtcSource(path, self.select, batch_frames=self.batch_frames,
+                             cache=self.align == "average"), self.masses
         if hasattr(x, "universe") and hasattr(x, "positions"):
             masses = self.masses
             if masses is None and self.align is not None:

@@ -201,6 +201,11 @@ class XtcDecoder:
         call("rmsf_xtcdec_decode", self._h, first, n, step, stream, ctypes.byref(slot), ctypes.byref(dptr))
         return slot.value, dptr.value
 
+    def decode_into(self, first: int, n: int, step: int, out_ptr: int, out_stride: int, stream: int) -> int:
+        slot = ctypes.c_int()
+        call("rmsf_xtcdec_decode_into", self._h, first, n, step, out_ptr, out_stride, stream, ctypes.byref(slot))
+        return slot.value
+
     def release(self, slot: int, stream: int) -> None:
         call("rmsf_xtcdec_release", self._h, slot, stream)
 
@@ -227,10 +232,16 @@ class XtcSource:
     of the consumer (3 slots: one hardware queue each beside the consumer's,
     HIP's default being 4 per process).  ``decode="host"``: frames are decoded frame-parallel on
     ``n_threads`` host threads straight into the stager's pinned slots
-    (selection applied) and DMA'd.  Both give the same float32 frames."""
+    (selection applied) and DMA'd.  Both give the same float32 frames.
+
+    ``cache=True`` (GPU decode): decoded frames stay resident in HBM, so a
+    second sweep over the trajectory -- RMSF.py re-reads every frame for its
+    second loop (RMSF.py:124) -- reads them from HBM instead of decoding
+    again; ignored (with no error) when the trajectory would take more than
+    half of the free device memory."""
 
     def __init__(self, path, sel=None, batch_frames: int | None = None, n_slots: int = 3, n_threads: int = 16,
-                 decode: str = "gpu"):
+                 decode: str = "gpu", cache: bool = False):
         from .xtc import XTCFile
 
         if decode not in ("gpu", "host"):
@@ -246,6 +257,14 @@ class XtcSource:
             if batch_frames is None:  # ~2 GB of decoded frames per slot
                 batch_frames = max(1, min(4096, (2 << 30) // max(1, 12 * self.n_atoms)))
             self.decoder = XtcDecoder(self.xtc, batch_frames, n_slots, n_threads)
+            self.cache = None
+            if cache:
+                need = 12 * self.n_atoms * self.n_traj
+                free, _ = torch.cuda.mem_get_info()
+                if need <= free // 2:
+                    self.cache = torch.empty((self.n_traj, self.n_atoms, 3), dtype=torch.float32,
+                                             device=torch.cuda.current_device())
+                    self._cached = np.zeros(self.n_traj, dtype=bool)
             self.sel_dev = None
             if sel_arr is not None and not np.array_equal(sel_arr, np.arange(self.n_sel)):
                 self.sel_dev = torch.as_tensor(sel_arr.astype(np.int32)).to(torch.cuda.current_device())
@@ -258,7 +277,22 @@ class XtcSource:
     def holds(self, frame: int) -> bool:
         return 0 <= frame < self.n_traj
 
+    def drop_cache(self) -> None:
+        """Forget the HBM-resident frames (the next sweep decodes again)."""
+        if self.decode_on == "gpu" and self.cache is not None:
+            self._cached[:] = False
+
     def _stage(self, first: int, step: int, n: int, stream: int) -> Batch:
+        if self.decode_on == "gpu" and self.cache is not None:
+            fs = 3 * self.n_atoms
+            ptr = self.cache.data_ptr() + 4 * fs * first
+            rows = first + step * np.arange(n)
+            release = None
+            if not self._cached[rows].all():
+                slot = self.decoder.decode_into(first, n, step, ptr, fs * step, stream)
+                self._cached[rows] = True
+                release = lambda: self.decoder.release(slot, stream)  # noqa: E731
+            return Batch(ptr, fs * step, n, self.sel_dev, release)
         if self.decode_on == "gpu":
             slot, ptr = self.decoder.decode(first, n, step, stream)
             return Batch(ptr, 3 * self.n_atoms, n, self.sel_dev, lambda: self.decoder.release(slot, stream))
@@ -270,9 +304,25 @@ class XtcSource:
 
     def _check(self) -> None:
         if self.decode_on == "gpu":
-            self.decoder.synchronize()
+            try:
+                self.decoder.synchronize()
+            except Exception:
+                if self.cache is not None:
+                    self._cached[:] = False  # a corrupt frame left NaN rows: decode again next time
+                raise
 
     def reference(self, frame: int, stream: int) -> Batch:
+        if self.decode_on == "gpu" and self.cache is not None:
+            # a reference frame costs one whole decode latency: decode the
+            # frames after it in the same wait (one batch per slot), so the
+            # sweep that follows finds them resident
+            first = frame
+            for _ in range(self.decoder.n_slots):
+                if first >= self.n_traj:
+                    break
+                n = min(self.batch_frames, self.n_traj - first)
+                self._stage(first, 1, n, stream).done()
+                first += n
         b = self._stage(frame, 1, 1, stream)
         self._check()
         return b

@@ -169,3 +169,49 @@ def test_xtc_decoder_reports_corrupt_frame(tmp_path):
     words.tofile(p)
     with pytest.raises(RmsfError, match="frame 3"):
         RMSF(XtcSource(p, None, batch_frames=2, decode="gpu")).run()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("step", [1, 3])
+def test_hbm_cache_two_sweeps(tmp_path, step):
+    """RMSF.py's two sweeps over a GPU-decoded XTC with the decoded frames kept
+    in HBM: bit-identical to decoding twice, and to host decoding."""
+    from rmsf_amd import RMSF
+    from rmsf_amd.sources import XtcSource
+    from rmsf_amd.xtc import write_xtc
+    x = _protein_like(np.random.default_rng(8), 3341, 31)
+    p = str(tmp_path / "t.xtc")
+    write_xtc(p, x)
+    sel = np.sort(np.random.default_rng(2).choice(3341, 214, replace=False))
+    cached = XtcSource(p, sel, batch_frames=5, cache=True)
+    assert cached.cache is not None
+    a = RMSF(cached, align="average").run(step=step).results
+    assert cached._cached[::step].all()
+    b = RMSF(cached, align="average").run(step=step).results  # all frames served from HBM
+    c = RMSF(XtcSource(p, sel, batch_frames=5), align="average").run(step=step).results
+    d = RMSF(XtcSource(p, sel, batch_frames=5, decode="host"), align="average").run(step=step).results
+    for r in (b, c, d):
+        np.testing.assert_array_equal(a.rmsf, r.rmsf)
+        np.testing.assert_array_equal(a.average, r.average)
+    # the path form caches in average mode (default batch size: another
+    # Chan merge order, so equal to rounding only)
+    e = RMSF(p, select=sel, align="average").run(step=step).results
+    np.testing.assert_allclose(a.rmsf, e.rmsf, rtol=0, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_hbm_cache_forgets_corrupt_frames(tmp_path):
+    from rmsf_amd import RMSF, RmsfError
+    from rmsf_amd.sources import XtcSource
+    from rmsf_amd.xtc import write_xtc
+    x = _protein_like(np.random.default_rng(4), 500, 6)
+    p = str(tmp_path / "t.xtc")
+    write_xtc(p, x)
+    words, off, ln, _ = _records(p)
+    words = words.copy()
+    words[off[3] + 14 + 7] = np.array([200], ">u4").view(np.uint32)[0]
+    words.tofile(p)
+    src = XtcSource(p, None, batch_frames=2, cache=True)
+    with pytest.raises(RmsfError, match="frame 3"):
+        RMSF(src, align="average").run()
+    assert not src._cached.any()
