@@ -343,8 +343,10 @@ int rmsf_set_reference_average(rmsf_ctx *ctx);
  * buffer may be reused when the call returns).                               */
 int rmsf_push_frames(rmsf_ctx *ctx, const float *xyz, int64_t n_frames,
                      int64_t frame_stride, int mode, int is_device_ptr);
-/* Push XTC frames f0, f0+step, ... (n_frames) decoded by the native reader
- * straight into the stager (RMSF.py:92,124 frame source).                    */
+/* Push XTC frames f0, f0+step, ... (n_frames) of an open file (RMSF.py:92,124
+ * frame source): the compressed records are decompressed on the GPU (the
+ * context keeps an rmsf_xtcdec for the file, up to 3 batches in flight).
+ * Synchronises at the end to report corrupt frames.                          */
 int rmsf_push_xtc(rmsf_ctx *ctx, const rmsf_xtc *x, int64_t f0,
                   int64_t n_frames, int64_t step, int mode);
 

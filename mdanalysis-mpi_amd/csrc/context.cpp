@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "rmsf_hip.h"
+#include "xtc_internal.h"
 
 #define RMSF_EXPORT __attribute__((visibility("default")))
 
@@ -159,6 +160,8 @@ struct rmsf_ctx {
   bool ref_set = false;
   Running wel, sum;
   rmsf_stager *stager = nullptr;
+  rmsf_xtcdec *xdec = nullptr;  // GPU XTC decoder, bound to the file of serial xdec_serial
+  uint64_t xdec_serial = 0;
   int64_t stage_batch = 0;  // 0 = auto
   int stage_slots = 2, stage_threads = 4;
   bool stager_dirty = true;
@@ -474,6 +477,7 @@ RMSF_EXPORT int rmsf_ctx_destroy(rmsf_ctx *c) {
     DeviceScope ds(c->dev);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->stager) rmsf_stager_destroy(c->stager);
+    if (c->xdec) rmsf_xtcdec_destroy(c->xdec);
     if (c->comm && rccl().ok) rccl().CommDestroy(c->comm);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;  // DevBufs free on the context's device
@@ -605,19 +609,40 @@ RMSF_EXPORT int rmsf_push_xtc(rmsf_ctx *c, const rmsf_xtc *x, int64_t f0, int64_
   CX_OK(check_mode(mode, "rmsf_push_xtc"));
   if (!x || n_frames < 0 || step < 1 || f0 < 0) return fail(RMSF_EINVAL, "rmsf_push_xtc: bad arguments");
   if (n_frames == 0) return RMSF_OK;
+  if (x->n_atoms != c->n_atoms) return fail(RMSF_EINVAL, "rmsf_push_xtc: the file's atom count differs");
   DeviceScope ds(c->dev);
-  CX_OK(ensure_stager(c));
-  for (int64_t i = 0; i < n_frames; i += c->stage_batch) {
-    const int64_t nf = std::min(c->stage_batch, n_frames - i);
-    int slot = -1;
-    float *d = nullptr;
-    CX_OK(rmsf_stager_stage_xtc(c->stager, x, f0 + i * step, nf, step, c->stream, &slot, &d));
-    int rc = process(c, d, 3 * c->n_sel, nf, nullptr, mode);
-    int rc2 = rmsf_stager_release(c->stager, slot, c->stream);
-    CX_OK(rc);
-    CX_OK(rc2);
+  // the records are decompressed on the GPU (csrc/xtc_gpu.hip) into full
+  // frames; the accumulate kernels gather the selection
+  constexpr int kSlots = 3;
+  if (!c->xdec || c->xdec_serial != x->serial) {
+    if (c->xdec) CX_OK(rmsf_xtcdec_destroy(c->xdec));
+    c->xdec = nullptr;
+    const int64_t batch = std::max<int64_t>(1, std::min<int64_t>(4096, (int64_t(2) << 30) / (12 * c->n_atoms)));
+    CX_OK(rmsf_xtcdec_create(x, batch, kSlots, 16, &c->xdec));
+    c->xdec_serial = x->serial;
   }
-  return RMSF_OK;
+  const int64_t batch = std::max<int64_t>(1, std::min<int64_t>(4096, (int64_t(2) << 30) / (12 * c->n_atoms)));
+  struct Pending {
+    int slot;
+    float *d;
+    int64_t n;
+  };
+  std::vector<Pending> q;  // up to kSlots decodes in flight ahead of the kernels
+  size_t head = 0;
+  auto consume = [&]() -> int {
+    const Pending p = q[head++];
+    const int rc = process(c, p.d, 3 * c->n_atoms, p.n, c->d_sel(), mode);
+    const int rc2 = rmsf_xtcdec_release(c->xdec, p.slot, c->stream);
+    return rc ? rc : rc2;
+  };
+  for (int64_t i = 0; i < n_frames; i += batch) {
+    Pending p{-1, nullptr, std::min(batch, n_frames - i)};
+    CX_OK(rmsf_xtcdec_decode(c->xdec, f0 + i * step, p.n, step, c->stream, &p.slot, &p.d));
+    q.push_back(p);
+    if (q.size() - head >= (size_t)kSlots) CX_OK(consume());
+  }
+  while (head < q.size()) CX_OK(consume());
+  return rmsf_xtcdec_synchronize(c->xdec);
 }
 
 RMSF_EXPORT int rmsf_get_partial(rmsf_ctx *c, int64_t *n, double *h_mean, double *h_m2) {

@@ -566,7 +566,9 @@ RMSF_EXPORT int rmsf_xtc_open(const char *path, rmsf_xtc **out, int64_t *n_atoms
     close(fd);
     return fail(RMSF_EINVAL, "rmsf_xtc_open: stat failed");
   }
+  static std::atomic<uint64_t> next_serial{1};
   auto *x = new rmsf_xtc();
+  x->serial = next_serial.fetch_add(1);
   x->fd = fd;
   const int64_t fsize = st.st_size;
   int64_t off = 0;

@@ -6,6 +6,7 @@
 #include <vector>
 
 struct rmsf_xtc {
+  uint64_t serial = 0;          // unique per open (a freed handle's address may be reused)
   int fd = -1;
   int64_t n_atoms = 0;
   std::vector<int64_t> offset;  // byte offset of each frame record (a multiple of 4)
