@@ -124,9 +124,10 @@ class RMSF:
             path = os.fspath(x)
             if not str(path).lower().endswith(".xtc"):
                 raise ValueError(f"only .xtc trajectory files are read natively, got {path!r}")
-            # RMSF.py's two sweeps read every frame twice: keep the decoded frames in HBM
+            # aligned runs read the reference frame first (and RMSF.py's two sweeps read
+            # every frame twice): keep the decoded frames resident in HBM
             return XtcSource(path, self.select, batch_frames=self.batch_frames,
-                             cache=self.align == "average"), self.masses
+                             cache=self.align is not None), self.masses
         if hasattr(x, "universe") and hasattr(x, "positions"):
             masses = self.masses
             if masses is None and self.align is not None:
