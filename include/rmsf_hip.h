@@ -47,6 +47,9 @@ extern "C" {
 /* Size of one per-frame transform record written by rmsf_superpose():
  * R[9] (row-major, applied as x @ R, RMSF.py:100), mobile COM[3], rmsd, pad[3] */
 #define RMSF_XFORM_DOUBLES 16
+/* longest frame tile one rmsf_accumulate split may hold (Welford
+ * coefficient table); n_splits >= ceil(n_frames / RMSF_MAX_SPLIT_FRAMES)    */
+#define RMSF_MAX_SPLIT_FRAMES 4096
 /* Size of the reference record written by rmsf_reference_setup():
  * [0..15]  ref_com[3], sum_r[3] (= sum of centred ref coords),
  *          G_ref (= sum |r|^2), total mass, n_sel, pad[7]

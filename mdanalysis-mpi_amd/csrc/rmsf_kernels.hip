@@ -67,7 +67,7 @@ constexpr int64_t kStatsBlocks = 16384;  // aim for >= this many (frame-group, c
 // Welford coefficients a_k = k/(k+1), b_k = 1/(k+1) (RMSF.py:137-138), folded
 // at compile time (IEEE division, identical to numpy's) into a constant table
 // read with scalar loads.  A split never exceeds kCoefN frames.
-constexpr int kCoefN = 4096;
+constexpr int kCoefN = RMSF_MAX_SPLIT_FRAMES;
 struct WCoef {
   double a, b;
 };
@@ -1061,7 +1061,7 @@ RMSF_EXPORT int rmsf_accumulate(const float *d_xyz, int64_t fstride, int64_t n_f
   if (n_splits <= 0) n_splits = rmsf_accumulate_splits(n_sel, n_frames, d_xform != nullptr);
   if (n_splits > 65535) return fail(RMSF_EINVAL, "rmsf_accumulate: n_splits > 65535");
   if ((n_frames + n_splits - 1) / n_splits > kCoefN)
-    return fail(RMSF_EINVAL, "rmsf_accumulate: a split exceeds 4096 frames; raise n_splits");
+    return fail(RMSF_EINVAL, "rmsf_accumulate: a split exceeds RMSF_MAX_SPLIT_FRAMES frames; raise n_splits");
   hipStream_t s = S(stream);
   const int64_t n_coord = 3 * n_sel;
   const bool flat_ok = !d_xform && !d_sel && mode == RMSF_MODE_WELFORD && (n_coord % 4 == 0) &&

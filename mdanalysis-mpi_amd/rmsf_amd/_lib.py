@@ -21,6 +21,7 @@ RMSF_EEMPTY = -4
 RMSF_MODE_WELFORD = 0
 RMSF_MODE_SUM = 1
 RMSF_XFORM_DOUBLES = 16
+RMSF_MAX_SPLIT_FRAMES = 4096  # frames per accumulate split (Welford coefficient table)
 RMSF_REFINFO_DOUBLES = 2064  # 16-double record + reduction scratch
 ABI_VERSION = 1
 

@@ -21,7 +21,8 @@ import numpy as np
 import torch
 
 from . import parallel
-from ._lib import RMSF_MODE_SUM, RMSF_MODE_WELFORD, RMSF_REFINFO_DOUBLES, RMSF_XFORM_DOUBLES, RmsfEmptyError
+from ._lib import (RMSF_MAX_SPLIT_FRAMES, RMSF_MODE_SUM, RMSF_MODE_WELFORD, RMSF_REFINFO_DOUBLES, RMSF_XFORM_DOUBLES,
+                   RmsfEmptyError)
 from .engine import Engine
 from .sources import Batch, FrameList
 
@@ -73,7 +74,9 @@ class Accumulator:
         self.timer = timer
         self.n_coord = 3 * n_sel
         self.fixed_splits = n_splits
-        self.s_max = n_splits or eng.splits(n_sel, max_batch, aligned)
+        # a requested split count is raised where a tile would exceed the limit
+        self.s_max = max(n_splits, -(-max_batch // RMSF_MAX_SPLIT_FRAMES)) if n_splits else \
+            eng.splits(n_sel, max_batch, aligned)
         # only slot 0 (the running result) must start at zero: split slots are
         # fully written by the accumulate kernel before they are read
         self.parts0 = eng.empty(1 + self.s_max, self.n_coord)
@@ -86,7 +89,10 @@ class Accumulator:
 
     def add(self, b: Batch, xform: torch.Tensor | None = None, refinfo: torch.Tensor | None = None) -> None:
         eng = self.eng
-        s = self.fixed_splits or min(self.s_max, eng.splits(self.n_sel, b.n_frames, self.aligned))
+        if self.fixed_splits:
+            s = max(self.fixed_splits, -(-b.n_frames // RMSF_MAX_SPLIT_FRAMES))
+        else:
+            s = min(self.s_max, eng.splits(self.n_sel, b.n_frames, self.aligned))
         with _span(self.timer, "accumulate"):
             eng.accumulate(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, xform, refinfo, self.mode, s,
                            self.parts0[1:], None if self.parts1 is None else self.parts1[1:])

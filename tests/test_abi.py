@@ -97,3 +97,15 @@ def test_context_create_fails_cleanly_without_gpu():
         pytest.skip("a GPU is present")
     rc = lib.rmsf_ctx_create(0, 10, 10, None, None, 0, ctypes.byref(h))
     assert rc < 0 and not h.value
+
+
+def test_python_constants_match_header():
+    """Every #define the ctypes layer mirrors has the header's value."""
+    from rmsf_amd import _lib
+    src = open(HEADER).read()
+    defines = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define\s+(RMSF_[A-Z0-9_]+)\s+\(?(-?\d+)\)?", src)}
+    mirrored = [n for n in defines if hasattr(_lib, n)]
+    assert {"RMSF_XFORM_DOUBLES", "RMSF_REFINFO_DOUBLES", "RMSF_MAX_SPLIT_FRAMES", "RMSF_OK", "RMSF_EINVAL",
+            "RMSF_MODE_SUM"} <= set(mirrored)
+    for n in mirrored:
+        assert getattr(_lib, n) == defines[n], n
