@@ -197,7 +197,16 @@ int main() {
   run("welford U=" #U " BS=" #BS " NT=" #NT, S, [&] { hipLaunchKernelGGL((k_wel<U, BS, NT>), dim3((n4 + BS - 1) / BS, S), dim3(BS), 0, 0, x, n4, n4, nf, S, om, oq); })
 #define SP(U, BS, S) \
   run("welford-sp U=" #U " BS=" #BS, S, [&] { hipLaunchKernelGGL((k_wel_sp<U, BS>), dim3((n4 + BS - 1) / BS, S), dim3(BS), 0, 0, x, n4, n4, nf, S, om, oq); })
+  const char *set = getenv("UB_SET");
   for (int rep = 0; rep < 2; ++rep) {
+    if (set && set[0] == 'S') {  // split-count sweep
+      RD(4, 256, 12);
+      RD(4, 256, 56);
+      for (int S : {10, 12, 13, 20, 24, 28, 32, 40}) WL(4, 256, true, S);
+      for (int S : {12, 24, 40}) WL(8, 256, true, S);
+      for (int S : {12, 24}) WL(4, 512, true, S);
+      continue;
+    }
     RD(4, 256, 56);
     for (int S : {8, 12, 16, 56}) WL(4, 256, true, S);
     for (int S : {8, 12, 16, 56}) SP(4, 256, S);
