@@ -120,6 +120,31 @@ int rmsf_accumulate(const float *d_xyz, int64_t frame_stride, int64_t n_frames,
 /* split s of rmsf_accumulate() holds this many frames */
 int64_t rmsf_split_count(int64_t n_frames, int n_splits, int s);
 
+/* ---- balanced streaming accumulator (the default product path) ------------
+ * Same arithmetic as rmsf_accumulate(), different work decomposition: the
+ * batch's (256-lane chunk, frame) space is cut into n_groups equal contiguous
+ * ranges, one per workgroup (n_groups <= 0: a per-kernel multiple of the
+ * CU count -- 3 for the float4 Welford, 2 per atom lane, 32 with the
+ * transform -- fewer for small batches), so every workgroup streams the same
+ * bytes and no tail wave is left.  The partials and a plan header go to d_work
+ * (rmsf_accumulate_balanced_workspace_bytes() bytes, 16-B aligned; the
+ * bound covers every layout and mode for these n_sel/n_frames/n_groups).
+ * rmsf_fold_balanced() then folds them, in frame order, into a running
+ * result that already holds acc_n frames (acc_n = 0: d_acc* are
+ * overwritten): Chan's merge (RMSF.py:36-41) into d_acc0 = mean,
+ * d_acc1 = M2 for WELFORD; d_acc0 += sum for SUM.  n_coord = 3*n_sel.
+ * d_work must not be reused between the two calls.                        */
+size_t rmsf_accumulate_balanced_workspace_bytes(int64_t n_sel, int64_t n_frames,
+                                                int n_groups);
+int rmsf_accumulate_balanced(const float *d_xyz, int64_t frame_stride,
+                             int64_t n_frames, int64_t n_sel,
+                             const int32_t *d_sel, const double *d_xform,
+                             const double *d_refinfo, int mode, int n_groups,
+                             void *d_work, size_t work_bytes, void *stream);
+int rmsf_fold_balanced(const void *d_work, int64_t n_coord, int mode,
+                       int64_t acc_n, double *d_acc0, double *d_acc1,
+                       void *stream);
+
 /* ---- Chan merge: second_order_moments, RMSF.py:36-41 ------------------------
  * Folds n_parts partial (count, mean, M2) sets of n_coord coordinates, in
  * order 0..n_parts-1, with T=n1+n2, mu=(n1 mu1+n2 mu2)/T,

@@ -140,10 +140,9 @@ struct DevBuf {
   double *d() const { return static_cast<double *>(p); }
 };
 
-// Running partial over pushed chunks: slot 0 of parts0/parts1 is the result.
+// Running partial over pushed chunks: parts0/parts1 hold the result (mean/sum, M2).
 struct Running {
   DevBuf parts0, parts1;
-  int slots = 0;  // split slots available after slot 0
   int64_t n = 0;
 };
 
@@ -156,7 +155,7 @@ struct rmsf_ctx {
   bool has_masses = false;
   std::vector<double> h_masses;
   hipStream_t stream = nullptr;
-  DevBuf sel, masses, ref, refinfo, xform, work, frame, avg, rmsf, xa, xb, cnt;
+  DevBuf sel, masses, ref, refinfo, xform, work, accwork, frame, avg, rmsf, xa, xb, cnt;
   bool ref_set = false;
   Running wel, sum;
   rmsf_stager *stager = nullptr;
@@ -190,16 +189,6 @@ int zero_running(rmsf_ctx *c, Running &r, bool two) {
   return RMSF_OK;
 }
 
-// grow the split slots of a running partial to >= s, keeping slot 0
-int ensure_slots(rmsf_ctx *c, Running &r, int s, bool two) {
-  if (s <= r.slots) return RMSF_OK;
-  const size_t need = sizeof(double) * c->n_coord * (size_t)(1 + s);
-  CX_OK(r.parts0.ensure(need, c->stream, true));
-  if (two) CX_OK(r.parts1.ensure(need, c->stream, true));
-  r.slots = s;
-  return RMSF_OK;
-}
-
 // one launch group over n_frames device frames: [superpose] + accumulate + fold
 int process(rmsf_ctx *c, const float *d_xyz, int64_t stride, int64_t n_frames, const int32_t *d_sel, int mode) {
   const bool aligned = mode == RMSF_PUSH_ALIGN_SUM || mode == RMSF_PUSH_ALIGN_WELFORD;
@@ -215,21 +204,15 @@ int process(rmsf_ctx *c, const float *d_xyz, int64_t stride, int64_t n_frames, c
     xf = c->xform.d();
   }
   Running &r = welford ? c->wel : c->sum;
-  const int s = rmsf_accumulate_splits(c->n_sel, n_frames, aligned ? 1 : 0);
-  if (s <= 0) return fail(RMSF_EINVAL, "rmsf_push: no split layout for this chunk");
-  CX_OK(ensure_slots(c, r, s, welford));
-  double *p0 = r.parts0.d(), *p1 = welford ? r.parts1.d() : nullptr;
-  CX_OK(rmsf_accumulate(d_xyz, stride, n_frames, c->n_sel, d_sel, xf, aligned ? c->refinfo.d() : nullptr,
-                        welford ? RMSF_MODE_WELFORD : RMSF_MODE_SUM, s, p0 + c->n_coord,
-                        welford ? p1 + c->n_coord : nullptr, c->stream));
-  if (welford) {
-    std::vector<int64_t> counts(1 + s);
-    counts[0] = r.n;
-    for (int i = 0; i < s; ++i) counts[1 + i] = rmsf_split_count(n_frames, s, i);
-    CX_OK(rmsf_chan_merge(p0, p1, counts.data(), 1 + s, c->n_coord, p0, p1, c->stream));
-  } else {
-    CX_OK(rmsf_sum_splits(p0, 1 + s, c->n_coord, p0, c->stream));
-  }
+  const int mode_k = welford ? RMSF_MODE_WELFORD : RMSF_MODE_SUM;
+  // balanced grid: equal (lane chunk, frame) ranges per workgroup, folded in
+  // frame order into the running slot 0
+  const size_t wb = rmsf_accumulate_balanced_workspace_bytes(c->n_sel, n_frames, 0);
+  CX_OK(c->accwork.ensure(std::max<size_t>(wb, 16), c->stream));
+  CX_OK(rmsf_accumulate_balanced(d_xyz, stride, n_frames, c->n_sel, d_sel, xf, aligned ? c->refinfo.d() : nullptr,
+                                 mode_k, 0, c->accwork.p, c->accwork.bytes, c->stream));
+  CX_OK(rmsf_fold_balanced(c->accwork.p, c->n_coord, mode_k, r.n, r.parts0.d(), welford ? r.parts1.d() : nullptr,
+                           c->stream));
   r.n += n_frames;
   return RMSF_OK;
 }

@@ -19,6 +19,7 @@
 //   * k_synth            counter-based synthetic trajectory generator.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -99,8 +100,51 @@ __device__ __forceinline__ int64_t split_begin(int64_t n_frames, int n_splits, i
 }
 
 // ---------------------------------------------------------------------------
-// k_welford_flat: contiguous selection, no alignment (config C2).
-// grid = (ceil(n4/256), n_splits); lane owns 4 consecutive coordinates.
+// Streaming bodies.  One lane walks `nf` consecutive frames of its column and
+// keeps the statistics in registers; U frames of loads are in flight.
+//
+// wel_flat_run: 4 consecutive coordinates (one float4) per lane, no
+// alignment, contiguous selection (config C2).
+template <int U>
+__device__ __forceinline__ void wel_flat_run(const f32x4 *__restrict__ p, int64_t stride4, int nf, double (&m)[4],
+                                             double (&q)[4]) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) m[c] = q[c] = 0.0;
+  int k = 0;
+  for (; k + U <= nf; k += U) {
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + (int64_t)(k + u) * stride4);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const WCoef c = g_coef.v[k + u];
+      welford(m[0], q[0], (double)v[u].x, c);
+      welford(m[1], q[1], (double)v[u].y, c);
+      welford(m[2], q[2], (double)v[u].z, c);
+      welford(m[3], q[3], (double)v[u].w, c);
+    }
+  }
+  for (; k < nf; ++k) {
+    const f32x4 v = __builtin_nontemporal_load(p + (int64_t)k * stride4);
+    const WCoef c = g_coef.v[k];
+    welford(m[0], q[0], (double)v.x, c);
+    welford(m[1], q[1], (double)v.y, c);
+    welford(m[2], q[2], (double)v.z, c);
+    welford(m[3], q[3], (double)v.w, c);
+  }
+}
+
+__device__ __forceinline__ void store4(double *__restrict__ om, double *__restrict__ oq, const double (&m)[4],
+                                       const double (&q)[4]) {
+  f64x2 *a = reinterpret_cast<f64x2 *>(om);
+  f64x2 *b = reinterpret_cast<f64x2 *>(oq);
+  a[0] = f64x2{m[0], m[1]};
+  a[1] = f64x2{m[2], m[3]};
+  b[0] = f64x2{q[0], q[1]};
+  b[1] = f64x2{q[2], q[3]};
+}
+
+// k_welford_flat (split grid): grid = (ceil(n4/256), n_splits).
 template <int U>
 __global__ __launch_bounds__(kBlock) void k_welford_flat(
     const float *__restrict__ xyz, int64_t stride4, int64_t n4, int64_t n_frames,
@@ -111,37 +155,9 @@ __global__ __launch_bounds__(kBlock) void k_welford_flat(
   const int s = blockIdx.y;
   const int64_t fb = split_begin(n_frames, n_splits, s);
   const int nf = (int)(split_begin(n_frames, n_splits, s + 1) - fb);
-  const f32x4 *p = reinterpret_cast<const f32x4 *>(xyz) + fb * stride4 + i4;
-
-  double m0 = 0, m1 = 0, m2 = 0, m3 = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0;
-  int k = 0;
-  for (; k + U <= nf; k += U) {
-    f32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + (int64_t)(k + u) * stride4);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const WCoef c = g_coef.v[k + u];
-      welford(m0, q0, (double)v[u].x, c);
-      welford(m1, q1, (double)v[u].y, c);
-      welford(m2, q2, (double)v[u].z, c);
-      welford(m3, q3, (double)v[u].w, c);
-    }
-  }
-  for (; k < nf; ++k) {
-    const f32x4 v = __builtin_nontemporal_load(p + (int64_t)k * stride4);
-    const WCoef c = g_coef.v[k];
-    welford(m0, q0, (double)v.x, c);
-    welford(m1, q1, (double)v.y, c);
-    welford(m2, q2, (double)v.z, c);
-    welford(m3, q3, (double)v.w, c);
-  }
-  f64x2 *om = reinterpret_cast<f64x2 *>(out_mean + (int64_t)s * n_coord + 4 * i4);
-  f64x2 *oq = reinterpret_cast<f64x2 *>(out_m2 + (int64_t)s * n_coord + 4 * i4);
-  om[0] = f64x2{m0, m1};
-  om[1] = f64x2{m2, m3};
-  oq[0] = f64x2{q0, q1};
-  oq[1] = f64x2{q2, q3};
+  double m[4], q[4];
+  wel_flat_run<U>(reinterpret_cast<const f32x4 *>(xyz) + fb * stride4 + i4, stride4, nf, m, q);
+  store4(out_mean + (int64_t)s * n_coord + 4 * i4, out_m2 + (int64_t)s * n_coord + 4 * i4, m, q);
 }
 
 // ---------------------------------------------------------------------------
@@ -162,8 +178,61 @@ __device__ __forceinline__ void apply_xform(float &x, float &y, float &z, const 
   z = (float)((double)r2 + rc2);
 }
 
-// k_accum_atoms: one selected atom per lane, frames of split blockIdx.y.
-// MODE 0 = WELFORD (out0 = mean, out1 = M2), 1 = SUM (out0 = sum).
+// accum_atoms_run: one selected atom (12 B) per lane; MODE 0 = WELFORD
+// (m = mean, q = M2), 1 = SUM (m = sum).  xf = the first frame's transform.
+template <int MODE, bool ALIGN, int U>
+__device__ __forceinline__ void accum_atoms_run(const float *__restrict__ p, int64_t fstride, int nf,
+                                                const double *__restrict__ xf, double rc0, double rc1, double rc2,
+                                                double (&m)[3], double (&q)[3]) {
+#pragma unroll
+  for (int c = 0; c < 3; ++c) m[c] = q[c] = 0.0;
+  auto consume = [&](float x, float y, float z, int k) {
+    if (ALIGN) apply_xform(x, y, z, xf + (int64_t)k * kXform, rc0, rc1, rc2);
+    if (MODE == RMSF_MODE_WELFORD) {
+      const WCoef c = g_coef.v[k];
+      welford(m[0], q[0], (double)x, c);
+      welford(m[1], q[1], (double)y, c);
+      welford(m[2], q[2], (double)z, c);
+    } else {
+      m[0] += (double)x;
+      m[1] += (double)y;
+      m[2] += (double)z;
+    }
+  };
+  int k = 0;
+  for (; k + U <= nf; k += U) {
+    float vx[U], vy[U], vz[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float *r = p + (int64_t)(k + u) * fstride;
+      vx[u] = __builtin_nontemporal_load(r);
+      vy[u] = __builtin_nontemporal_load(r + 1);
+      vz[u] = __builtin_nontemporal_load(r + 2);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) consume(vx[u], vy[u], vz[u], k + u);
+  }
+  for (; k < nf; ++k) {
+    const float *r = p + (int64_t)k * fstride;
+    consume(r[0], r[1], r[2], k);
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void store3(double *__restrict__ o0, double *__restrict__ o1, const double (&m)[3],
+                                       const double (&q)[3]) {
+  o0[0] = m[0];
+  o0[1] = m[1];
+  o0[2] = m[2];
+  if (MODE == RMSF_MODE_WELFORD) {
+    o1[0] = q[0];
+    o1[1] = q[1];
+    o1[2] = q[2];
+  }
+}
+
+// k_accum_atoms (split grid): one selected atom per lane, frames of split
+// blockIdx.y.  MODE 0 = WELFORD (out0 = mean, out1 = M2), 1 = SUM (out0 = sum).
 template <int MODE, bool ALIGN, bool GATHER, int U>
 __global__ __launch_bounds__(kBlock) void k_accum_atoms(
     const float *__restrict__ xyz, int64_t fstride, int64_t n_sel, const int32_t *__restrict__ sel,
@@ -175,50 +244,192 @@ __global__ __launch_bounds__(kBlock) void k_accum_atoms(
   const int64_t fb = split_begin(n_frames, n_splits, s);
   const int nf = (int)(split_begin(n_frames, n_splits, s + 1) - fb);
   const int64_t off = GATHER ? 3 * (int64_t)sel[a] : 3 * a;
-  const float *p = xyz + fb * fstride + off;
-  const double *xf = ALIGN ? xform + fb * kXform : nullptr;
   const double rc0 = ALIGN ? refinfo[0] : 0.0, rc1 = ALIGN ? refinfo[1] : 0.0, rc2 = ALIGN ? refinfo[2] : 0.0;
-
-  double m0 = 0, m1 = 0, m2 = 0, q0 = 0, q1 = 0, q2 = 0;
-  auto consume = [&](float x, float y, float z, int k) {
-    if (ALIGN) apply_xform(x, y, z, xf + (int64_t)k * kXform, rc0, rc1, rc2);
-    if (MODE == RMSF_MODE_WELFORD) {
-      const WCoef c = g_coef.v[k];
-      welford(m0, q0, (double)x, c);
-      welford(m1, q1, (double)y, c);
-      welford(m2, q2, (double)z, c);
-    } else {
-      m0 += (double)x;
-      m1 += (double)y;
-      m2 += (double)z;
-    }
-  };
-  int k = 0;
-  for (; k + U <= nf; k += U) {
-    float vx[U], vy[U], vz[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const float *q = p + (int64_t)(k + u) * fstride;
-      vx[u] = __builtin_nontemporal_load(q);
-      vy[u] = __builtin_nontemporal_load(q + 1);
-      vz[u] = __builtin_nontemporal_load(q + 2);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) consume(vx[u], vy[u], vz[u], k + u);
-  }
-  for (; k < nf; ++k) {
-    const float *q = p + (int64_t)k * fstride;
-    consume(q[0], q[1], q[2], k);
-  }
+  double m[3], q[3];
+  accum_atoms_run<MODE, ALIGN, U>(xyz + fb * fstride + off, fstride, nf, ALIGN ? xform + fb * kXform : nullptr,
+                                  rc0, rc1, rc2, m, q);
   const int64_t o = (int64_t)s * 3 * n_sel + 3 * a;
-  out0[o + 0] = m0;
-  out0[o + 1] = m1;
-  out0[o + 2] = m2;
-  if (MODE == RMSF_MODE_WELFORD) {
-    out1[o + 0] = q0;
-    out1[o + 1] = q1;
-    out1[o + 2] = q2;
+  store3<MODE>(out0 + o, out1 + o, m, q);
+}
+
+// ---------------------------------------------------------------------------
+// Balanced ("stream-K") grid.  The batch's (lane chunk, frame) space --
+// chunk c = lanes [256c, 256c+256), frames 0..nf-1 -- is linearised
+// chunk-major and cut into G equal ranges, one per workgroup (G = a multiple
+// of the CU count, kSkPerCu* below), so every workgroup streams the same
+// bytes and no tail wave exists.  A workgroup walks its range as segments:
+// maximal runs inside one chunk, at most kCoefN frames (the coefficient
+// table); each segment writes one partial into slot b*P + j (j = segment
+// index within workgroup b).  Measured on MI355X (tools/ubench_welford.hip,
+// 100k atoms x 20k frames): 3.48 ms at G = 512 vs 3.67-3.75 ms for the best
+// split grid, against a 3.47 ms pure-read ceiling.  The gain varies by box:
+// where the split grid already streams at ~3.67 ms the two tie.
+//
+// Workspace = header (kSkHdr int64) + parts0[G*P][256*cpl] (+ parts1).
+constexpr int kSkHdr = 16;
+constexpr int64_t kSkMinSeg = 32;  // auto grid: ranges of >= this many frames
+struct SkPlan {
+  int64_t lanes, C, nf, T;
+  int G, P, cpl, mode;
+};
+
+__host__ __device__ inline int64_t sk_lo(const SkPlan &p, int64_t b) { return p.T * b / p.G; }
+
+__host__ __device__ inline int64_t sk_seg_len(const SkPlan &p, int64_t lo, int64_t hi, int64_t *c, int64_t *f0) {
+  *c = lo / p.nf;
+  *f0 = lo - *c * p.nf;
+  int64_t len = hi - lo;
+  if (p.nf - *f0 < len) len = p.nf - *f0;
+  if (len > kCoefN) len = kCoefN;
+  return len;
+}
+
+// The segment walk is wave-uniform, but 64-bit division runs on the VALU:
+// pin the results to SGPRs so the per-frame transform records and the
+// coefficient table keep arriving by scalar loads.
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ void sk_write_header(int64_t *hdr, const SkPlan &p) {
+  hdr[0] = p.lanes;
+  hdr[1] = p.C;
+  hdr[2] = p.nf;
+  hdr[3] = p.T;
+  hdr[4] = p.G;
+  hdr[5] = p.P;
+  hdr[6] = p.cpl;
+  hdr[7] = p.mode;
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_welford_flat_sk(const float *__restrict__ xyz, int64_t stride4,
+                                                            SkPlan pl, int64_t *__restrict__ hdr,
+                                                            double *__restrict__ parts0,
+                                                            double *__restrict__ parts1) {
+  const int b = blockIdx.x;
+  if (b == 0 && threadIdx.x == 0) sk_write_header(hdr, pl);
+  int64_t lo = sk_lo(pl, b);
+  const int64_t hi = sk_lo(pl, b + 1);
+  int64_t slot = (int64_t)b * pl.P;
+  while (lo < hi) {
+    int64_t c, f0;
+    const int len = (int)sk_seg_len(pl, lo, hi, &c, &f0);
+    const int64_t i4 = c * kBlock + threadIdx.x;
+    if (i4 < pl.lanes) {
+      double m[4], q[4];
+      wel_flat_run<U>(reinterpret_cast<const f32x4 *>(xyz) + f0 * stride4 + i4, stride4, len, m, q);
+      const int64_t o = slot * (kBlock * 4) + 4 * threadIdx.x;
+      store4(parts0 + o, parts1 + o, m, q);
+    }
+    lo += len;
+    ++slot;
   }
+}
+
+template <int MODE, bool ALIGN, bool GATHER, int U>
+__global__ __launch_bounds__(kBlock) void k_accum_atoms_sk(const float *__restrict__ xyz, int64_t fstride,
+                                                           const int32_t *__restrict__ sel,
+                                                           const double *__restrict__ xform,
+                                                           const double *__restrict__ refinfo, SkPlan pl,
+                                                           int64_t *__restrict__ hdr, double *__restrict__ parts0,
+                                                           double *__restrict__ parts1) {
+  const int b = blockIdx.x;
+  if (b == 0 && threadIdx.x == 0) sk_write_header(hdr, pl);
+  const double rc0 = ALIGN ? refinfo[0] : 0.0, rc1 = ALIGN ? refinfo[1] : 0.0, rc2 = ALIGN ? refinfo[2] : 0.0;
+  int64_t lo = uni64(sk_lo(pl, b));
+  const int64_t hi = uni64(sk_lo(pl, b + 1));
+  int64_t slot = (int64_t)b * pl.P;
+  while (lo < hi) {
+    int64_t c, f0;
+    const int len = __builtin_amdgcn_readfirstlane((int)sk_seg_len(pl, lo, hi, &c, &f0));
+    c = uni64(c);
+    f0 = uni64(f0);
+    const int64_t a = c * kBlock + threadIdx.x;
+    if (a < pl.lanes) {
+      const int64_t off = GATHER ? 3 * (int64_t)sel[a] : 3 * a;
+      double m[3], q[3];
+      accum_atoms_run<MODE, ALIGN, U>(xyz + f0 * fstride + off, fstride, len, ALIGN ? xform + f0 * kXform : nullptr,
+                                      rc0, rc1, rc2, m, q);
+      const int64_t o = slot * (kBlock * 3) + 3 * threadIdx.x;
+      store3<MODE>(parts0 + o, parts1 + o, m, q);
+    }
+    lo += len;
+    ++slot;
+  }
+}
+
+// Fold the balanced partials of one batch, in frame order, into the running
+// result (acc_n frames already in acc0/acc1; 0 = overwrite): Chan's merge
+// (second_order_moments, RMSF.py:36-41) for WELFORD, a sum for SUM.  One
+// thread per coordinate; it replays the segment walk of the workgroups that
+// cover its chunk (fixed order: bitwise reproducible).
+__global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ hdr,
+                                                    const double *__restrict__ parts0, int64_t n_coord,
+                                                    double acc_n, double *__restrict__ acc0,
+                                                    double *__restrict__ acc1) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n_coord) return;
+  SkPlan pl;
+  pl.lanes = hdr[0];
+  pl.C = hdr[1];
+  pl.nf = hdr[2];
+  pl.T = hdr[3];
+  pl.G = (int)hdr[4];
+  pl.P = (int)hdr[5];
+  pl.cpl = (int)hdr[6];
+  pl.mode = (int)hdr[7];
+  const int64_t lane = j / pl.cpl;
+  const int64_t c = lane / kBlock;
+  const int64_t slot_d = (int64_t)kBlock * pl.cpl;
+  const int64_t off = j - c * slot_d;
+  const int64_t clo = c * pl.nf, chi = clo + pl.nf;
+  const double *__restrict__ parts1 = parts0 + (int64_t)pl.G * pl.P * slot_d;
+  // first workgroup whose range ends after the chunk starts
+  int64_t b = clo * pl.G / pl.T;
+  while (b > 0 && sk_lo(pl, b) > clo) --b;
+  while (sk_lo(pl, b + 1) <= clo) ++b;
+  const bool wel = pl.mode == RMSF_MODE_WELFORD;
+  double n1 = acc_n, mu = 0.0, M = 0.0;
+  if (acc_n > 0) {
+    mu = acc0[j];
+    if (wel) M = acc1[j];
+  }
+  for (; b < pl.G; ++b) {
+    int64_t lo = sk_lo(pl, b);
+    if (lo >= chi) break;
+    const int64_t hi = sk_lo(pl, b + 1);
+    int64_t slot = b * pl.P;
+    while (lo < hi) {
+      int64_t cc, f0;
+      const int64_t len = sk_seg_len(pl, lo, hi, &cc, &f0);
+      if (cc > c) break;
+      if (cc == c) {
+        const int64_t o = slot * slot_d + off;
+        if (!wel) {
+          mu += parts0[o];
+        } else if (n1 <= 0) {
+          n1 = (double)len;
+          mu = parts0[o];
+          M = parts1[o];
+        } else {
+          const double n2 = (double)len, mu2 = parts0[o], M2 = parts1[o];
+          const double T = n1 + n2;
+          const double d = mu2 - mu;
+          const double mun = (n1 * mu + n2 * mu2) / T;
+          M = M + M2 + (n1 * n2 / T) * (d * d);
+          mu = mun;
+          n1 = T;
+        }
+      }
+      lo += len;
+      ++slot;
+    }
+  }
+  acc0[j] = mu;
+  if (wel) acc1[j] = M;
 }
 
 // ---------------------------------------------------------------------------
@@ -1092,6 +1303,133 @@ RMSF_EXPORT int rmsf_accumulate(const float *d_xyz, int64_t fstride, int64_t n_f
   }
 #undef AC_LAUNCH
   return after_launch("k_accum_atoms");
+}
+
+}  // extern "C"
+
+namespace {
+
+int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  const int slot = dev < 64 ? dev : 63;
+  if (cached[slot] > 0) return cached[slot];
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  cached[slot] = n;
+  return n;
+}
+
+// Auto workgroups per CU of the balanced grid, by kernel (tools/tune_groups.py,
+// 100k atoms x 20k frames, same-process sweeps on MI355X): the float4 Welford
+// streams best with 2-3 resident workgroups per CU (3.58 ms at 3/CU vs 3.75 ms
+// split grid on the same box); one atom per lane without the transform at 1-2;
+// the aligned (transform) kernels are VALU-heavy (~48 fp64 ops per
+// atom-frame, 99 VGPRs) and want many short ranges: 3.90 vs 4.06 ms (Welford),
+// 3.73 vs 3.77 ms (sum) at 32/CU.
+constexpr int kSkPerCuFlat = 3, kSkPerCuAtoms = 2, kSkPerCuAligned = 32;
+
+// Balanced-grid plan for `lanes` lanes (cpl coordinates each) over nf frames.
+SkPlan sk_plan(int64_t lanes, int cpl, int64_t nf, int n_groups, int mode, int per_cu) {
+  SkPlan p{};
+  p.lanes = lanes;
+  p.C = (lanes + kBlock - 1) / kBlock;
+  p.nf = nf;
+  p.T = p.C * nf;
+  p.cpl = cpl;
+  p.mode = mode;
+  int64_t G = n_groups > 0 ? n_groups : (int64_t)per_cu * cu_count();
+  if (n_groups <= 0) G = std::min<int64_t>(G, std::max<int64_t>(1, p.T / kSkMinSeg));
+  G = std::max<int64_t>(1, std::min<int64_t>({G, p.T, (int64_t)INT32_MAX}));
+  p.G = (int)G;
+  // segments per workgroup: a range of W frames meets at most (W-1)/nf + 2
+  // chunks and each chunk piece adds at most one cut at kCoefN
+  const int64_t W = (p.T + G - 1) / G;
+  p.P = (int)((W + kCoefN - 1) / kCoefN + (W - 1) / nf + 2);
+  return p;
+}
+
+size_t sk_bytes(const SkPlan &p, bool two) {
+  const size_t part = (size_t)p.G * (size_t)p.P * kBlock * (size_t)p.cpl * sizeof(double);
+  return kSkHdr * sizeof(int64_t) + part * (two ? 2 : 1);
+}
+
+bool flat_layout(const float *d_xyz, int64_t fstride, int64_t n_sel, const int32_t *d_sel, const double *d_xform,
+                 int mode) {
+  return !d_xform && !d_sel && mode == RMSF_MODE_WELFORD && (3 * n_sel) % 4 == 0 && fstride % 4 == 0 &&
+         reinterpret_cast<uintptr_t>(d_xyz) % 16 == 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+RMSF_EXPORT size_t rmsf_accumulate_balanced_workspace_bytes(int64_t n_sel, int64_t n_frames, int n_groups) {
+  if (n_sel < 1 || n_frames < 1) return 0;
+  // the larger of the two layouts (float4 columns / one atom per lane), WELFORD
+  size_t m = 0;
+  for (int per_cu : {kSkPerCuFlat, kSkPerCuAtoms, kSkPerCuAligned}) {
+    m = std::max(m, sk_bytes(sk_plan((3 * n_sel + 3) / 4, 4, n_frames, n_groups, RMSF_MODE_WELFORD, per_cu), true));
+    m = std::max(m, sk_bytes(sk_plan(n_sel, 3, n_frames, n_groups, RMSF_MODE_WELFORD, per_cu), true));
+  }
+  return m;
+}
+
+RMSF_EXPORT int rmsf_accumulate_balanced(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
+                                         const int32_t *d_sel, const double *d_xform, const double *d_refinfo,
+                                         int mode, int n_groups, void *d_work, size_t work_bytes, void *stream) {
+  if (mode != RMSF_MODE_WELFORD && mode != RMSF_MODE_SUM)
+    return fail(RMSF_EINVAL, "rmsf_accumulate_balanced: bad mode");
+  if (!d_xyz || !d_work || n_sel < 1 || n_frames < 1 || fstride < (d_sel ? 3 : 3 * n_sel) ||
+      reinterpret_cast<uintptr_t>(d_work) % 16 != 0)
+    return fail(RMSF_EINVAL, "rmsf_accumulate_balanced: bad arguments");
+  if (d_xform && !d_refinfo) return fail(RMSF_EINVAL, "rmsf_accumulate_balanced: aligned mode needs d_refinfo");
+  hipStream_t s = S(stream);
+  const bool two = mode == RMSF_MODE_WELFORD;
+  int64_t *hdr = static_cast<int64_t *>(d_work);
+  if (flat_layout(d_xyz, fstride, n_sel, d_sel, d_xform, mode)) {
+    const SkPlan pl = sk_plan(3 * n_sel / 4, 4, n_frames, n_groups, mode, kSkPerCuFlat);
+    if (work_bytes < sk_bytes(pl, two)) return fail(RMSF_ENOMEM, "rmsf_accumulate_balanced: workspace too small");
+    double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
+    double *p1 = p0 + (size_t)pl.G * pl.P * kBlock * 4;
+    hipLaunchKernelGGL((k_welford_flat_sk<4>), dim3(pl.G), dim3(kBlock), 0, s, d_xyz, fstride / 4, pl, hdr, p0, p1);
+    return after_launch("k_welford_flat_sk");
+  }
+  const SkPlan pl = sk_plan(n_sel, 3, n_frames, n_groups, mode, d_xform ? kSkPerCuAligned : kSkPerCuAtoms);
+  if (work_bytes < sk_bytes(pl, two)) return fail(RMSF_ENOMEM, "rmsf_accumulate_balanced: workspace too small");
+  double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
+  double *p1 = two ? p0 + (size_t)pl.G * pl.P * kBlock * 3 : nullptr;
+  const bool g = d_sel != nullptr, al = d_xform != nullptr;
+#define SK_LAUNCH(M_, A_, G_) \
+  hipLaunchKernelGGL((k_accum_atoms_sk<M_, A_, G_, 4>), dim3(pl.G), dim3(kBlock), 0, s, d_xyz, fstride, d_sel, d_xform, d_refinfo, pl, hdr, p0, p1)
+  if (two) {
+    if (al && g) SK_LAUNCH(0, true, true);
+    else if (al) SK_LAUNCH(0, true, false);
+    else if (g) SK_LAUNCH(0, false, true);
+    else SK_LAUNCH(0, false, false);
+  } else {
+    if (al && g) SK_LAUNCH(1, true, true);
+    else if (al) SK_LAUNCH(1, true, false);
+    else if (g) SK_LAUNCH(1, false, true);
+    else SK_LAUNCH(1, false, false);
+  }
+#undef SK_LAUNCH
+  return after_launch("k_accum_atoms_sk");
+}
+
+RMSF_EXPORT int rmsf_fold_balanced(const void *d_work, int64_t n_coord, int mode, int64_t acc_n, double *d_acc0,
+                                   double *d_acc1, void *stream) {
+  if (mode != RMSF_MODE_WELFORD && mode != RMSF_MODE_SUM) return fail(RMSF_EINVAL, "rmsf_fold_balanced: bad mode");
+  if (!d_work || !d_acc0 || (mode == RMSF_MODE_WELFORD && !d_acc1) || n_coord < 1 || acc_n < 0)
+    return fail(RMSF_EINVAL, "rmsf_fold_balanced: bad arguments");
+  const int64_t *hdr = static_cast<const int64_t *>(d_work);
+  const double *p0 = reinterpret_cast<const double *>(hdr + kSkHdr);
+  // the plan (and where parts1 starts) is read from the header the
+  // accumulate kernel wrote
+  hipLaunchKernelGGL(k_fold_sk, dim3(grid1(n_coord)), dim3(kBlock), 0, S(stream), hdr, p0, n_coord, (double)acc_n,
+                     d_acc0, d_acc1);
+  return after_launch("k_fold_sk");
 }
 
 RMSF_EXPORT int rmsf_chan_merge(const double *d_mean_parts, const double *d_m2_parts, const int64_t *h_counts,

@@ -84,6 +84,22 @@ class Engine:
         call("rmsf_accumulate", xyz_ptr, fstride, n_frames, n_sel, _ptr(sel), _ptr(xform), _ptr(refinfo), mode,
              n_splits, out0.data_ptr(), _ptr(out1), self.stream)
 
+    def balanced_workspace_bytes(self, n_sel: int, n_frames: int, n_groups: int = 0) -> int:
+        return int(self.lib.rmsf_accumulate_balanced_workspace_bytes(n_sel, n_frames, n_groups))
+
+    def accumulate_balanced(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, sel, xform, refinfo,
+                            mode: int, work: torch.Tensor, n_groups: int = 0) -> None:
+        """RMSF.py:99-103 (SUM) / 133-138 (WELFORD) on the balanced grid (one equal
+        (lane chunk, frame) range per workgroup); partials go to ``work``."""
+        call("rmsf_accumulate_balanced", xyz_ptr, fstride, n_frames, n_sel, _ptr(sel), _ptr(xform), _ptr(refinfo),
+             mode, n_groups, work.data_ptr(), work.numel() * work.element_size(), self.stream)
+
+    def fold_balanced(self, work: torch.Tensor, n_coord: int, mode: int, acc_n: int, acc0: torch.Tensor,
+                      acc1: torch.Tensor | None) -> None:
+        """Fold the balanced partials in frame order into the running result
+        (Chan's merge, RMSF.py:36-41, or a sum)."""
+        call("rmsf_fold_balanced", work.data_ptr(), n_coord, mode, acc_n, acc0.data_ptr(), _ptr(acc1), self.stream)
+
     def chan_merge(self, mean_parts: torch.Tensor, m2_parts: torch.Tensor, counts, n_coord: int,
                    mean_out: torch.Tensor, m2_out: torch.Tensor) -> None:
         """second_order_moments (RMSF.py:36-41) folded over the partials in order."""

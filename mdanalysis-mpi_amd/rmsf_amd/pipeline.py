@@ -64,9 +64,13 @@ def _span(timer, name):
 class Accumulator:
     """Running Welford (or f64 sum) over streamed batches, on device.
 
-    Layout: ``parts0/parts1`` are [1 + S_max, 3*n_sel] f64; slot 0 holds the
-    running result, slots 1..S the current batch's split partials, folded into
-    slot 0 by the Chan-merge kernel (or the split-sum kernel)."""
+    Default (``n_splits=None``): the balanced grid -- one equal (lane chunk,
+    frame) range per workgroup, partials in ``work``, folded in frame order
+    into ``parts0[0]``/``parts1[0]`` (the running result) by
+    ``rmsf_fold_balanced``.  With a fixed ``n_splits`` the split grid is used:
+    ``parts0/parts1`` are [1 + S_max, 3*n_sel] f64, slots 1..S hold the
+    batch's split partials, folded into slot 0 by the Chan-merge kernel (or
+    the split-sum kernel)."""
 
     def __init__(self, eng: Engine, n_sel: int, mode: int, max_batch: int, aligned: bool,
                  n_splits: int | None = None, timer: KernelTimer | None = None):
@@ -74,9 +78,15 @@ class Accumulator:
         self.timer = timer
         self.n_coord = 3 * n_sel
         self.fixed_splits = n_splits
-        # a requested split count is raised where a tile would exceed the limit
-        self.s_max = max(n_splits, -(-max_batch // RMSF_MAX_SPLIT_FRAMES)) if n_splits else \
-            eng.splits(n_sel, max_batch, aligned)
+        self.work = None
+        if n_splits:
+            # a requested split count is raised where a tile would exceed the limit
+            self.s_max = max(n_splits, -(-max_batch // RMSF_MAX_SPLIT_FRAMES))
+        else:
+            self.s_max = 0
+            # the bound grows with the batch, so size it for the largest one
+            nbytes = eng.balanced_workspace_bytes(n_sel, max_batch)
+            self.work = eng.empty(max(2, (nbytes + 7) // 8))
         # only slot 0 (the running result) must start at zero: split slots are
         # fully written by the accumulate kernel before they are read
         self.parts0 = eng.empty(1 + self.s_max, self.n_coord)
@@ -89,10 +99,18 @@ class Accumulator:
 
     def add(self, b: Batch, xform: torch.Tensor | None = None, refinfo: torch.Tensor | None = None) -> None:
         eng = self.eng
-        if self.fixed_splits:
-            s = max(self.fixed_splits, -(-b.n_frames // RMSF_MAX_SPLIT_FRAMES))
-        else:
-            s = min(self.s_max, eng.splits(self.n_sel, b.n_frames, self.aligned))
+        p1 = None if self.parts1 is None else self.parts1[0]
+        if not self.fixed_splits:
+            need = eng.balanced_workspace_bytes(self.n_sel, b.n_frames)
+            if need > self.work.numel() * 8:  # the bound is not monotone in the batch size
+                self.work = eng.empty((need + 7) // 8)
+            with _span(self.timer, "accumulate"):
+                eng.accumulate_balanced(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, xform, refinfo, self.mode,
+                                        self.work)
+            eng.fold_balanced(self.work, self.n_coord, self.mode, self.n, self.parts0[0], p1)
+            self.n += b.n_frames
+            return
+        s = max(self.fixed_splits, -(-b.n_frames // RMSF_MAX_SPLIT_FRAMES))
         with _span(self.timer, "accumulate"):
             eng.accumulate(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, xform, refinfo, self.mode, s,
                            self.parts0[1:], None if self.parts1 is None else self.parts1[1:])

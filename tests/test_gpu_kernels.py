@@ -153,6 +153,57 @@ def test_welford_noalign(eng, n_sel, nf, splits):
         np.testing.assert_allclose(rmsf.cpu().numpy(), d["rmsf_P1"], rtol=0, atol=1e-9)
 
 
+@pytest.mark.parametrize("n_sel,nf,groups,gather", [
+    (4096, 1000, 0, False), (4096, 1000, 1, False), (4096, 1000, 3, False), (1001, 333, 0, False),
+    (1001, 333, 7, True), (3, 5, 0, False), (3, 5, 2, True), (300, 9000, 1, False), (300, 9000, 5, True),
+    (2048, 700, 3000, False), (100_000, 64, 0, False), (257, 4097, 2, False)])
+def test_balanced_welford_and_sum(eng, n_sel, nf, groups, gather):
+    """Balanced grid (rmsf_accumulate_balanced + rmsf_fold_balanced): float4
+    and atom-per-lane layouts, forced workgroup counts (1 = one workgroup
+    walks every chunk; 9000 frames cut segments at RMSF_MAX_SPLIT_FRAMES;
+    3000 > the chunk-frame count clamps), and a running fold over two
+    batches, against the f64 two-pass variance and the f64 sum."""
+    from rmsf_amd.synth import generate
+    from rmsf_amd._lib import RMSF_MODE_SUM, RMSF_MODE_WELFORD
+    n_atoms = n_sel + 17 if gather else n_sel
+    traj = generate(eng, n_atoms, 0, nf, seed=22)
+    sel = np.sort(np.random.default_rng(3).choice(n_atoms, n_sel, replace=False)) if gather else None
+    sdev = torch.tensor(sel.astype(np.int32), device=eng.device) if gather else None
+    host = traj.cpu().numpy()
+    x = (host[:, sel] if gather else host).astype(np.float64)
+    cut = nf // 3
+    mean, m2, s = eng.empty(3 * n_sel), eng.empty(3 * n_sel), eng.empty(3 * n_sel)
+    acc = 0
+    for f0, f1 in ((0, cut), (cut, nf)):
+        if f1 <= f0:
+            continue
+        n = f1 - f0
+        work = eng.empty(eng.balanced_workspace_bytes(n_sel, n, groups) // 8 + 2)
+        ptr = traj.data_ptr() + f0 * 3 * n_atoms * 4
+        eng.accumulate_balanced(ptr, 3 * n_atoms, n, n_sel, sdev, None, None, RMSF_MODE_WELFORD, work, groups)
+        eng.fold_balanced(work, 3 * n_sel, RMSF_MODE_WELFORD, acc, mean, m2)
+        eng.accumulate_balanced(ptr, 3 * n_atoms, n, n_sel, sdev, None, None, RMSF_MODE_SUM, work, groups)
+        eng.fold_balanced(work, 3 * n_sel, RMSF_MODE_SUM, acc, s, None)
+        acc += n
+    rmsf = eng.empty(n_sel)
+    eng.finalize(m2, n_sel, nf, rmsf)
+    _sync()
+    np.testing.assert_allclose(mean.cpu().numpy().reshape(-1, 3), x.mean(0), rtol=0, atol=1e-10)
+    np.testing.assert_allclose(s.cpu().numpy().reshape(-1, 3), x.sum(0), rtol=1e-13, atol=1e-9)
+    np.testing.assert_allclose(rmsf.cpu().numpy(), O.rmsf_two_pass(x), rtol=0, atol=1e-9)
+
+
+def test_balanced_bad_arguments(eng):
+    from rmsf_amd import RmsfError
+    from rmsf_amd._lib import RMSF_MODE_WELFORD
+    x = eng.empty(10, 3, dtype=torch.float32)
+    small = eng.empty(4)
+    with pytest.raises(RmsfError, match="workspace too small"):
+        eng.accumulate_balanced(x.data_ptr(), 3, 10, 1, None, None, None, RMSF_MODE_WELFORD, small)
+    with pytest.raises(RmsfError, match="bad arguments"):
+        eng.accumulate_balanced(x.data_ptr(), 3, 0, 1, None, None, None, RMSF_MODE_WELFORD, small)
+
+
 def test_chan_merge_kernel_many_groups(eng):
     """>128 partials exercise the grouped launches; counts with empties."""
     rng = np.random.default_rng(0)
@@ -197,5 +248,5 @@ def test_error_paths(eng):
     out = eng.empty(30)
     with pytest.raises(RmsfError, match="bad arguments"):
         eng.accumulate(x.data_ptr(), 3, 10, 0, None, None, None, RMSF_MODE_WELFORD, 1, out, out)
-    with pytest.raises(RmsfError, match="4096"):
+    with pytest.raises(RmsfError, match="RMSF_MAX_SPLIT_FRAMES"):
         eng.accumulate(x.data_ptr(), 30, 10000, 10, None, None, None, RMSF_MODE_WELFORD, 1, out, out)

@@ -17,7 +17,7 @@
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int kCoefN = 4096;
+constexpr int kCoefN = 16384;
 struct WCoef {
   double a, b;
 };
@@ -163,6 +163,73 @@ __global__ __launch_bounds__(BS) void k_wel_sp(const f4 *__restrict__ x, int64_t
   oq[o + 3] = q3;
 }
 
+// balanced ("stream-K") decomposition: the (column chunk, frame) space is
+// linearised chunk-major and cut into G equal ranges, one per workgroup, so
+// every workgroup streams the same number of bytes and the grid has no tail
+// wave.  A range spans at most a few chunks; each (chunk, range) segment
+// writes one partial (slot 2b + j).
+template <int U, int BS, bool READ_ONLY>
+__global__ __launch_bounds__(BS) void k_wel_sk(const f4 *__restrict__ x, int64_t stride4, int64_t n4, int64_t nf,
+                                               int G, double *__restrict__ om, double *__restrict__ oq) {
+  const int64_t C = (n4 + BS - 1) / BS;
+  const int64_t T = C * nf;
+  const int b = blockIdx.x;
+  int64_t lo = T * b / G;
+  const int64_t hi = T * (b + 1) / G;
+  int j = 0;
+  while (lo < hi) {
+    const int64_t c = lo / nf, f0 = lo % nf;
+    const int64_t f1 = f0 + (hi - lo) < nf ? f0 + (hi - lo) : nf;
+    const int nfl = (int)(f1 - f0);
+    const int64_t i = c * BS + threadIdx.x;
+    if (i < n4) {
+      const f4 *p = x + f0 * stride4 + i;
+      double m0 = 0, m1 = 0, m2 = 0, m3 = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+      f4 acc = {0, 0, 0, 0};
+      int k = 0;
+      for (; k + U <= nfl; k += U) {
+        f4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + (int64_t)(k + u) * stride4);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (READ_ONLY) {
+            acc += v[u];
+          } else {
+            const WCoef cf = g_coef.v[k + u];
+            welford(m0, q0, (double)v[u].x, cf);
+            welford(m1, q1, (double)v[u].y, cf);
+            welford(m2, q2, (double)v[u].z, cf);
+            welford(m3, q3, (double)v[u].w, cf);
+          }
+        }
+      }
+      for (; k < nfl; ++k) {
+        const f4 v = __builtin_nontemporal_load(p + (int64_t)k * stride4);
+        const WCoef cf = g_coef.v[k];
+        welford(m0, q0, (double)v.x, cf);
+        welford(m1, q1, (double)v.y, cf);
+        welford(m2, q2, (double)v.z, cf);
+        welford(m3, q3, (double)v.w, cf);
+      }
+      if (READ_ONLY) m0 = acc.x + acc.y + acc.z + acc.w;
+      const int64_t o = ((int64_t)(2 * b + j) * BS + threadIdx.x) * 4;
+      if (!READ_ONLY || m0 == 1234.5) {
+        om[o] = m0;
+        om[o + 1] = m1;
+        om[o + 2] = m2;
+        om[o + 3] = m3;
+        oq[o] = q0;
+        oq[o + 1] = q1;
+        oq[o + 2] = q2;
+        oq[o + 3] = q3;
+      }
+    }
+    lo += nfl;
+    j = j < 1 ? j + 1 : 1;
+  }
+}
+
 int main() {
   const int64_t n = 100000, nf = 20000, n4 = 3 * n / 4;
   const size_t bytes = sizeof(float) * 3 * n * nf;
@@ -199,6 +266,18 @@ int main() {
   run("welford-sp U=" #U " BS=" #BS, S, [&] { hipLaunchKernelGGL((k_wel_sp<U, BS>), dim3((n4 + BS - 1) / BS, S), dim3(BS), 0, 0, x, n4, n4, nf, S, om, oq); })
   const char *set = getenv("UB_SET");
   for (int rep = 0; rep < 2; ++rep) {
+    if (set && set[0] == 'K') {  // balanced (stream-K) grid vs the split grid
+#define SK(U, BS, RO, G) \
+  run("sk U=" #U " BS=" #BS " RO=" #RO, G, [&] { hipLaunchKernelGGL((k_wel_sk<U, BS, RO>), dim3(G), dim3(BS), 0, 0, x, n4, n4, nf, G, om, oq); })
+      RD(4, 256, 56);
+      WL(4, 256, true, 12);
+      for (int G : {512, 1024}) SK(4, 256, true, G);
+      for (int G : {384, 512, 640, 768, 896, 1024, 1280, 1536}) SK(4, 256, false, G);
+      for (int G : {512, 768, 1024}) SK(8, 256, false, G);
+      for (int G : {256, 384, 512}) SK(4, 512, false, G);
+      for (int G : {128, 256, 512}) SK(4, 1024, false, G);
+      continue;
+    }
     if (set && set[0] == 'S') {  // split-count sweep
       RD(4, 256, 12);
       RD(4, 256, 56);
