@@ -17,7 +17,8 @@ At N=1 the aligned configurations are measured too and reported under
 "modes" (C3 = QCP alignment to frame 0; RMSF.py's own two-sweep "average").
 
 Rank 0 prints ONE JSON line.  ``roofline`` is measured live with HIP events
-around the dominant kernel (k_welford_flat) on its launch stream;
+around the dominant kernel (k_welford_flat_sk, the balanced-grid Welford
+stream; k_welford_flat with --splits) on its launch stream;
 ``cpu_baseline`` is the oracle's numpy restatement of RMSF.py's per-rank loop
 timed on this host's cores (run before the GPU is touched).
 """
@@ -280,7 +281,8 @@ def main():
         "config": {"workload": wl["name"], "n_atoms": n_atoms, "n_frames_per_gpu": per_gpu,
                    "n_frames_total": n_total, "selection": "all atoms", "align": wl["align"],
                    "parallelism": f"frame-sharded x{world} (RMSF.py:65-69 blocks), RCCL Chan merge"},
-        "roofline": {"bound": "hbm", "kernel": "k_accum_atoms" if wl["align"] else "k_welford_flat",
+        "roofline": {"bound": "hbm", "kernel": ("k_accum_atoms" if wl["align"] else "k_welford_flat")
+                     + ("" if a.splits else "_sk"),
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": f"profiles/pmc_{a.workload}.json" if traffic else None,
                      "algorithmic_bytes_per_launch": bytes_launch,
