@@ -260,6 +260,7 @@ long decode_coords(const unsigned char *p0, size_t avail, int natoms, float *xyz
   for (int i = 0; i < 3; ++i) maxint[i] = rd_i(p);
   unsigned sizeint[3], bitsizeint[3] = {0, 0, 0};
   for (int i = 0; i < 3; ++i) sizeint[i] = (unsigned)(maxint[i] - minint[i]) + 1u;
+  if (!sizeint[0] || !sizeint[1] || !sizeint[2]) return -1;  // a wrapped range: corrupt header
   int bitsize = 0;
   if ((sizeint[0] | sizeint[1] | sizeint[2]) > 0xffffff) {
     for (int i = 0; i < 3; ++i) bitsizeint[i] = sizeofint(sizeint[i]);
@@ -305,7 +306,7 @@ long decode_coords(const unsigned char *p0, size_t avail, int natoms, float *xyz
       is_smaller--;
     }
     if (run > 0) {
-      if (i + run / 3 > lsize) return -1;
+      if (i + run / 3 > lsize || sizesmall[0] == 0) return -1;  // smallidx below the magicints table
       for (int k = 0; k < run; k += 3) {
         int t[3];
         br.ints(smallidx, sizesmall, t);

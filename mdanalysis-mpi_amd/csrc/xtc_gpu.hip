@@ -5,15 +5,15 @@
 // it is bound by host cores (~2k frames/s of 250k atoms on 16 threads).  Here
 // the compressed frame records themselves are streamed: read from the file
 // into a pinned slot (pread, host threads), copied to HBM (about 1/6 of the
-// decoded bytes), and decompressed on the device -- the xdr3dfcoord stream of
-// one frame is strictly sequential, so a frame is one wave's work (the
-// decoder state is wave-uniform; the wave holds a 256-B window of the stream
-// in its lanes with the next one in flight, reads any field up to 64 bits
-// with three readlanes and shifts, and stores 64 decoded atoms at a time)
-// and frames run in parallel, one wave each.  Output: float32 [n][n_atoms][3] Angstrom frames in HBM with
-// MDAnalysis' rounding f32(f32(int * f32(1/prec)) * 10), bit-identical to the
-// host decoder.  The selection is applied downstream (the accumulate
-// kernels gather it in-kernel), as for any HBM-resident trajectory.
+// decoded bytes), and decompressed on the device, one wave per frame, frames
+// in parallel.  A frame's xdr3dfcoord stream is sequential only in its bit
+// offsets, so the decode is two passes (see "two-pass frame decode" below):
+// a wave-uniform walk that reads just the 1-6 flag bits per atom group, and
+// a lane-parallel decode of 64 recorded groups at a time.  Output: float32
+// [n][n_atoms][3] Angstrom frames in HBM with MDAnalysis' rounding
+// f32(f32(int * f32(1/prec)) * 10), bit-identical to the host decoder.  The
+// selection is applied downstream (the accumulate kernels gather it
+// in-kernel), as for any HBM-resident trajectory.
 //
 // Packed triples of <= 52 bits are split with two exact double-precision
 // divisions (quotient estimate by reciprocal, one correction step); wider
@@ -107,45 +107,11 @@ struct MemWindow {
     return bits64(at(i), at(i + 1), at(i + 2), (int)(pos & 31));
   }
   __host__ __device__ inline void skip(int k) { pos += k; }
+  __host__ __device__ inline void advance(int64_t k) { pos += k; }
+  __host__ __device__ inline void skip64(int64_t k) { pos += k; }
   __host__ __device__ inline int64_t consumed() const { return pos; }
-};
-
-// device, one wave per frame: every lane runs the (uniform) decoder.  Lane j
-// holds stream word w0+j (cur, byte-swapped) and word w0+60+j (nxt, raw, in
-// flight); reads take words w0+i..w0+i+2 with readlane, i <= 61, and the
-// window slides by 60 words once the position passes word 60 -- so the
-// next chunk's load hides behind ~40 atoms of decode.
-struct WaveWindow {
-  const uint32_t *s;
-  int64_t nw, w0;
-  uint32_t cur, nxt;
-  int pos;  // bit offset from word w0, < 1920 between calls
-  int lane;
-  __device__ inline void start(const uint32_t *p, int64_t n_words) {
-    s = p;
-    nw = n_words;
-    w0 = 0;
-    pos = 0;
-    lane = (int)(threadIdx.x & 63);
-    cur = lane < nw ? be32w(p[lane]) : 0u;
-    nxt = 60 + lane < nw ? p[60 + lane] : 0u;
-  }
-  __device__ inline uint32_t word(int i) const { return (uint32_t)__builtin_amdgcn_readlane((int)cur, i); }
-  __device__ inline uint64_t peek64() const {
-    const int i = pos >> 5;
-    return bits64(word(i), word(i + 1), word(i + 2), pos & 31);
-  }
-  __device__ inline void skip(int k) {  // k <= 64
-    pos += k;
-    if (pos >= 60 * 32) {
-      pos -= 60 * 32;
-      w0 += 60;
-      cur = be32w(nxt);
-      const int64_t j = w0 + 60 + lane;
-      nxt = j < nw ? s[j] : 0u;
-    }
-  }
-  __device__ inline int64_t consumed() const { return 32 * w0 + pos; }
+  __host__ __device__ static inline int uni(int v) { return v; }
+  __host__ __device__ inline void uniformize() {}
 };
 
 template <class W>
@@ -163,11 +129,6 @@ __host__ __device__ inline uint64_t unpack(uint64_t x, int nbits) {  // x: the n
   const uint64_t top = x & ((1ull << r) - 1ull);
   const uint64_t low = (__builtin_bswap64(x >> r) >> (63 - 8 * q)) >> 1;
   return (top << (8 * q)) | low;
-}
-
-template <class W>
-__host__ __device__ inline uint64_t read_packed(W &w, int nbits) {
-  return unpack(take(w, nbits), nbits);
 }
 
 // value = (n0*s1 + n1)*s2 + n2, value < 2^52: exact double arithmetic, the
@@ -210,15 +171,6 @@ __host__ __device__ inline bool split_bytes(W &w, int nbits, const unsigned s[3]
   }
   out[0] = (int)(bytes[0] | bytes[1] << 8 | bytes[2] << 16 | bytes[3] << 24);
   return true;
-}
-
-template <class W>
-__host__ __device__ inline bool read_triple(W &w, int nbits, const unsigned s[3], const double inv[3], int out[3]) {
-  if (nbits <= 52) {
-    split_f64(read_packed(w, nbits), s, inv, out);
-    return true;
-  }
-  return split_bytes(w, nbits, s, out);
 }
 
 __host__ __device__ inline int sizeofint_hd(unsigned size) {
@@ -269,74 +221,136 @@ __host__ __device__ inline void to_angstrom(int c0, int c1, int c2, float invp, 
   c = z * 10.0f;
 }
 
-// host: atoms written in order
-struct MemSink {
-  float *o;
-  __host__ __device__ inline void put_f(float a, float b, float c) {
-    o[0] = a;
-    o[1] = b;
-    o[2] = c;
-    o += 3;
-  }
-  __host__ __device__ inline void put(int c0, int c1, int c2, float invp) {
-    float a, b, c;
-    to_angstrom(c0, c1, c2, invp, a, b, c);
-    put_f(a, b, c);
-  }
-  __host__ __device__ inline void flush() {}
+// ---- two-pass frame decode ---------------------------------------------------
+// The stream is a sequence of groups: one "large" atom (an absolute packed
+// triple) followed by the run of small triples its flag announced (run/3
+// atoms, each relative to the previous one).  Only the bit offsets are
+// sequential: a group's length is fixed by the header (large triple), its
+// flag/run code and the current small-integer index.  Pass 1 walks the
+// stream reading nothing but the 1-6 flag bits per group and records each
+// group's (bit offset, atom index, small index, run); pass 2 decodes the
+// recorded groups independently -- on the device one group per lane, 64 at a
+// time -- reading the triples straight from memory.  Groups are independent
+// because smallnum == magicints[smallidx]/2 in every state a run can use and a
+// large atom resets `prev`.  Corruption is detected in pass 1, in the order
+// of the sequential algorithm, so the status is identical.
+struct XtcFrame {
+  const uint32_t *s;  // compressed stream (big-endian words)
+  int64_t nw, nbits;
+  int natoms, bitsize, large_bits, smallidx0;
+  unsigned bitsizeint[3], sizeint[3];
+  double invint[3];
+  int minint[3];
+  float inv_precision;
 };
 
-// device: atom k of a group of 64 goes to lane k's registers;
-// a full group is stored by the whole wave, 768 contiguous bytes.
-struct WaveSink {
-  float *o;  // next group's first atom
-  int k;
-  uint32_t vx, vy, vz;  // lane j: atom j of the group (integers, or f32 bits)
-  float invp;
-  bool raw;
-  __device__ inline void put(int c0, int c1, int c2, float inv_precision) {
-    invp = inv_precision;
-    keep((uint32_t)c0, (uint32_t)c1, (uint32_t)c2);
+struct XtcGroup {
+  int64_t pos;   // bit offset of the large triple
+  int32_t idx;   // index of the group's first output atom
+  uint32_t meta; // small-integer index (bits per small triple) | run/3 << 8 | flag bits (1 or 6) << 16
+  __host__ __device__ inline int sidx() const { return (int)(meta & 0xff); }
+  __host__ __device__ inline int nsmall() const { return (int)((meta >> 8) & 0xff); }
+  __host__ __device__ inline int fbits() const { return (int)(meta >> 16); }
+};
+
+__host__ __device__ inline uint32_t stream_word(const uint32_t *s, int64_t nw, int64_t j) {
+  return j < nw ? be32w(s[j]) : 0u;
+}
+
+__host__ __device__ inline bool split_bytes_ok(int nbits, const unsigned s[3]) {
+  return !(nbits > 96 || s[1] == 0 || s[2] == 0 || s[1] > (1u << 24) || s[2] > (1u << 24));
+}
+
+// stream words for pass 2: straight from memory (host) ...
+struct MemSrc {
+  const uint32_t *s;
+  int64_t nw;
+  __host__ __device__ inline uint32_t at(int64_t j) const { return stream_word(s, nw, j); }
+};
+
+// ... or from the wave's LDS ring (device): the last kRing words the window
+// passed, byte-swapped, zero past the stream
+constexpr int kRing = 2048;
+struct LdsSrc {
+  const uint32_t *ring;
+  __device__ inline uint32_t at(int64_t j) const { return ring[j & (kRing - 1)]; }
+};
+
+template <class Src>
+__host__ __device__ inline void triple_at(const XtcFrame &F, const Src &src, int64_t pos, int nbits,
+                                          const unsigned s[3], const double inv[3], int out[3]) {
+  if (nbits <= 52) {
+    const int64_t i = pos >> 5;
+    const uint64_t v = bits64(src.at(i), src.at(i + 1), src.at(i + 2), (int)(pos & 31)) >> (64 - nbits);
+    split_f64(unpack(v, nbits), s, inv, out);
+  } else {
+    MemWindow w;
+    w.start(F.s, F.nw);
+    w.skip64(pos);
+    (void)split_bytes(w, nbits, s, out);  // the widths were validated (header / pass 1)
   }
-  __device__ inline void put_f(float a, float b, float c) {
-    raw = true;
-    keep(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, c));
-  }
-  __device__ inline void keep(uint32_t a, uint32_t b, uint32_t c) {
-    const bool mine = (int)(threadIdx.x & 63) == k;
-    vx = mine ? a : vx;
-    vy = mine ? b : vy;
-    vz = mine ? c : vz;
-    if (++k == 64) flush();
-  }
-  // the group's integer -> Angstrom conversions run lane-parallel here
-  __device__ inline void flush() {
-    const int lane = (int)(threadIdx.x & 63);
-    if (lane < k) {
-      float a, b, c;
-      if (raw) {
-        a = __builtin_bit_cast(float, vx);
-        b = __builtin_bit_cast(float, vy);
-        c = __builtin_bit_cast(float, vz);
-      } else {
-        to_angstrom((int)vx, (int)vy, (int)vz, invp, a, b, c);
-      }
-      o[3 * lane] = a;
-      o[3 * lane + 1] = b;
-      o[3 * lane + 2] = c;
+}
+
+__host__ __device__ inline void put_atom(float *o, int64_t idx, int c0, int c1, int c2, float invp) {
+  float a, b, c;
+  to_angstrom(c0, c1, c2, invp, a, b, c);
+  o[3 * idx] = a;
+  o[3 * idx + 1] = b;
+  o[3 * idx + 2] = c;
+}
+
+// pass 2: one group
+template <class Src>
+__host__ __device__ inline void decode_group(const XtcFrame &F, const XtcGroup &g, const int *magic,
+                                             const double *inv_magic, float *o, const Src &src) {
+  int cur[3];
+  if (F.bitsize == 0) {
+    int64_t p = g.pos;
+    for (int c = 0; c < 3; ++c) {
+      const int64_t i = p >> 5;
+      cur[c] = (int)(bits64(src.at(i), src.at(i + 1), src.at(i + 2), (int)(p & 31)) >> (64 - F.bitsizeint[c]));
+      p += F.bitsizeint[c];
     }
-    o += 3 * k;
-    k = 0;
+  } else {
+    triple_at(F, src, g.pos, F.bitsize, F.sizeint, F.invint, cur);
   }
-};
+  for (int c = 0; c < 3; ++c) cur[c] += F.minint[c];
+  const int nsmall = g.nsmall(), sidx = g.sidx();
+  if (nsmall == 0) {
+    put_atom(o, g.idx, cur[0], cur[1], cur[2], F.inv_precision);
+    return;
+  }
+  const unsigned m = (unsigned)magic[sidx];
+  const unsigned ss[3] = {m, m, m};
+  const double iv = inv_magic[sidx];
+  const double is[3] = {iv, iv, iv};
+  const int smallnum = magic[sidx] / 2;
+  int prev[3] = {cur[0], cur[1], cur[2]};
+  int64_t p = g.pos + F.large_bits + g.fbits();
+  for (int k = 0; k < nsmall; ++k) {
+    int t[3];
+    triple_at(F, src, p, sidx, ss, is, t);
+    p += sidx;
+    for (int c = 0; c < 3; ++c) t[c] += prev[c] - smallnum;
+    if (k == 0) {  // the writer swapped the first two atoms (water)
+      put_atom(o, g.idx, t[0], t[1], t[2], F.inv_precision);
+      put_atom(o, g.idx + 1, prev[0], prev[1], prev[2], F.inv_precision);
+    } else {
+      put_atom(o, g.idx + 1 + k, t[0], t[1], t[2], F.inv_precision);
+    }
+    prev[0] = t[0];
+    prev[1] = t[1];
+    prev[2] = t[2];
+  }
+}
 
-// Decode one XTC frame record (starting at its magic word, `words` long)
-// into n_atoms Angstrom triples through `sink`.  Mirrors decode_coords() of
-// xtc.cpp.  W: MemWindow (host) or WaveWindow (device, one wave per frame).
-template <class W, class Sink>
-__host__ __device__ int32_t decode_record(const uint32_t *rec, int64_t words, int64_t n_atoms, Sink &sink,
-                                          const int *magic, const double *inv_magic) {
+// Frame header of one XTC record (starting at its magic word, `words`
+// long): the raw form (<= 9 atoms) is decoded here (*raw = true); otherwise
+// F describes the compressed stream.  Mirrors decode_coords() of xtc.cpp.
+__host__ __device__ inline int32_t parse_header(const uint32_t *rec, int64_t words, int64_t n_atoms, float *o,
+                                                XtcFrame &F, bool *raw) {
 #pragma clang fp contract(off)
+  *raw = false;
   if (words < 14) return kShort;
   if ((int)be32w(rec[0]) != kMagic) return kBadMagic;
   const int natoms = (int)be32w(rec[1]);
@@ -346,131 +360,220 @@ __host__ __device__ int32_t decode_record(const uint32_t *rec, int64_t words, in
   if (natoms <= 9) {
     if (left < 3 * natoms) return kShort;
     for (int a = 0; a < natoms; ++a)  // raw floats (nm) x 10, as MDAnalysis
-      sink.put_f(f32_bits(be32w(p[3 * a])) * 10.0f, f32_bits(be32w(p[3 * a + 1])) * 10.0f,
-                 f32_bits(be32w(p[3 * a + 2])) * 10.0f);
-    sink.flush();
+      for (int c = 0; c < 3; ++c) o[3 * a + c] = f32_bits(be32w(p[3 * a + c])) * 10.0f;
+    *raw = true;
     return kOk;
   }
   if (left < 9) return kShort;
+  F.natoms = natoms;
   const float precision = f32_bits(be32w(p[0]));
-  int minint[3], maxint[3];
+  int maxint[3];
   for (int c = 0; c < 3; ++c) {
-    minint[c] = (int)be32w(p[1 + c]);
+    F.minint[c] = (int)be32w(p[1 + c]);
     maxint[c] = (int)be32w(p[4 + c]);
   }
-  int smallidx = (int)be32w(p[7]);
+  const int smallidx = (int)be32w(p[7]);
   const int nbytes = (int)be32w(p[8]);
   p += 9;
   left -= 9;
   if (smallidx < kFirstIdx || smallidx >= kLastIdx || nbytes < 0 || ((int64_t)nbytes + 3) / 4 > left)
     return kBadHeader;
-  unsigned sizeint[3], bitsizeint[3] = {0, 0, 0};
-  double invint[3];
   for (int c = 0; c < 3; ++c) {
-    sizeint[c] = (unsigned)(maxint[c] - minint[c]) + 1u;
-    invint[c] = 1.0 / (double)sizeint[c];
+    F.sizeint[c] = (unsigned)(maxint[c] - F.minint[c]) + 1u;
+    if (F.sizeint[c] == 0) return kBadHeader;  // a wrapped range
+    F.invint[c] = 1.0 / (double)F.sizeint[c];
+    F.bitsizeint[c] = 0;
   }
-  int bitsize = 0;
-  if ((sizeint[0] | sizeint[1] | sizeint[2]) > 0xffffff) {
-    for (int c = 0; c < 3; ++c) bitsizeint[c] = sizeofint_hd(sizeint[c]);
+  F.bitsize = 0;
+  if ((F.sizeint[0] | F.sizeint[1] | F.sizeint[2]) > 0xffffff) {
+    for (int c = 0; c < 3; ++c) F.bitsizeint[c] = sizeofint_hd(F.sizeint[c]);
+    F.large_bits = (int)(F.bitsizeint[0] + F.bitsizeint[1] + F.bitsizeint[2]);
   } else {
-    bitsize = sizeofints_hd(sizeint);
+    F.bitsize = sizeofints_hd(F.sizeint);
+    F.large_bits = F.bitsize;
+    // the sequential decoder fails on its first large triple
+    if (F.bitsize > 52 && !split_bytes_ok(F.bitsize, F.sizeint)) return kCorrupt;
   }
-  int smaller = magic[smallidx - 1 > kFirstIdx ? smallidx - 1 : kFirstIdx] / 2;
-  int smallnum = magic[smallidx] / 2;
-  unsigned sizesmall[3];
-  double invsmall[3];
-  sizesmall[0] = sizesmall[1] = sizesmall[2] = magic[smallidx];
-  invsmall[0] = invsmall[1] = invsmall[2] = inv_magic[smallidx];
-  const float inv_precision = (float)(1.0 / (double)precision);
-
-  W b;
-  b.start(p, ((int64_t)nbytes + 3) / 4);
-  const int64_t nbits = 8 * (int64_t)nbytes;
-  int prev[3] = {0, 0, 0};
-  int run = 0, i = 0;
-  while (i < natoms) {
-    int cur[3];
-    if (bitsize == 0) {
-      cur[0] = (int)take(b, bitsizeint[0]);
-      cur[1] = (int)take(b, bitsizeint[1]);
-      cur[2] = (int)take(b, bitsizeint[2]);
-    } else if (!read_triple(b, bitsize, sizeint, invint, cur)) {
-      return kCorrupt;
-    }
-    // flag bit, then (flag set) a 5-bit run code: one peek, no branch
-    const uint32_t p6 = (uint32_t)(b.peek64() >> 58);
-    b.skip((p6 >> 5) ? 6 : 1);
-    i++;
-    cur[0] += minint[0];
-    cur[1] += minint[1];
-    cur[2] += minint[2];
-    prev[0] = cur[0];
-    prev[1] = cur[1];
-    prev[2] = cur[2];
-    const bool flag = (p6 >> 5) != 0;
-    const int rc = (int)(p6 & 31), rm = rc % 3;
-    run = flag ? rc - rm : run;
-    const int is_smaller = flag ? rm - 1 : 0;
-    if (run > 0) {
-      if (i + run / 3 > natoms || sizesmall[0] == 0) return kCorrupt;
-      for (int k = 0; k < run; k += 3) {
-        int t[3];
-        if (!read_triple(b, smallidx, sizesmall, invsmall, t)) return kCorrupt;
-        i++;
-        t[0] += prev[0] - smallnum;
-        t[1] += prev[1] - smallnum;
-        t[2] += prev[2] - smallnum;
-        if (k == 0) {  // the writer swapped the first two atoms (water)
-          const int s0 = t[0], s1 = t[1], s2 = t[2];
-          t[0] = prev[0];
-          t[1] = prev[1];
-          t[2] = prev[2];
-          prev[0] = s0;
-          prev[1] = s1;
-          prev[2] = s2;
-          sink.put(prev[0], prev[1], prev[2], inv_precision);
-        } else {
-          prev[0] = t[0];
-          prev[1] = t[1];
-          prev[2] = t[2];
-        }
-        sink.put(t[0], t[1], t[2], inv_precision);
-      }
-    } else {
-      sink.put(cur[0], cur[1], cur[2], inv_precision);
-    }
-    smallidx += is_smaller;
-    if (smallidx < kFirstIdx - 1 || smallidx >= kLastIdx) return kCorrupt;
-    if (is_smaller != 0) {
-      if (is_smaller < 0) {
-        smallnum = smaller;
-        smaller = smallidx > kFirstIdx ? magic[smallidx - 1] / 2 : 0;
-      } else {
-        smaller = smallnum;
-        smallnum = magic[smallidx] / 2;
-      }
-      sizesmall[0] = sizesmall[1] = sizesmall[2] = magic[smallidx];
-      invsmall[0] = invsmall[1] = invsmall[2] = inv_magic[smallidx];
-    }
-    if (b.consumed() > nbits) return kCorrupt;
-  }
-  sink.flush();
+  F.inv_precision = (float)(1.0 / (double)precision);
+  F.s = p;
+  F.nw = ((int64_t)nbytes + 3) / 4;
+  F.nbits = 8 * (int64_t)nbytes;
+  F.smallidx0 = smallidx;
   return kOk;
 }
 
-// One wave per frame (grid = n_frames blocks of 64): the decoder state is
-// wave-uniform; the stream is fetched by the whole wave (WaveWords) and the
-// output stored by it (WaveSink).
+// one step of pass 1, shared by host and device: from the group's flag
+// peek (p6 = the 6 bits after its large triple) to its record.  Returns
+// false on a corrupt stream (the sequential algorithm's checks, in order).
+__host__ __device__ inline bool group_step(const XtcFrame &F, const int *magic, uint32_t p6, int &i, int &run,
+                                           int &sidx, int &adv, uint32_t &meta) {
+  const bool flag = (p6 >> 5) != 0;
+  const int rc = (int)(p6 & 31), rm = rc % 3;
+  run = flag ? rc - rm : run;
+  const int is_smaller = flag ? rm - 1 : 0;
+  ++i;
+  int nsmall = 0;
+  adv = flag ? 6 : 1;
+  if (run > 0) {
+    nsmall = run / 3;
+    if (i + nsmall > F.natoms || magic[sidx] == 0) return false;
+    adv += nsmall * sidx;
+    i += nsmall;
+  }
+  meta = (uint32_t)sidx | (uint32_t)nsmall << 8 | (flag ? 6u : 1u) << 16;
+  sidx += is_smaller;
+  return !(sidx < kFirstIdx - 1 || sidx >= kLastIdx);
+}
+
+// host: pass 1 and pass 2 interleaved group by group
+inline int32_t scan_host(const XtcFrame &F, const int *magic, const double *inv, float *o) {
+  const MemSrc src{F.s, F.nw};
+  MemWindow b;
+  b.start(F.s, F.nw);
+  int i = 0, run = 0, sidx = F.smallidx0;
+  while (i < F.natoms) {
+    XtcGroup g;
+    g.pos = b.consumed();
+    g.idx = i;
+    b.advance(F.large_bits);
+    const uint32_t p6 = (uint32_t)(b.peek64() >> 58);
+    int adv;
+    if (!group_step(F, magic, p6, i, run, sidx, adv, g.meta)) return kCorrupt;
+    b.advance(adv);
+    if (b.consumed() > F.nbits) return kCorrupt;
+    decode_group(F, g, magic, inv, o, src);
+  }
+  return kOk;
+}
+
+// v_writelane_b32 (the LLVM intrinsic; this clang has no builtin for it):
+// lane `lane` of `old` := the uniform `value`
+extern "C" __device__ int llvm_amdgcn_writelane(int value, int lane, int old) __asm("llvm.amdgcn.writelane");
+__device__ inline uint32_t writelane(uint32_t old, uint32_t value, int lane) {
+  return (uint32_t)llvm_amdgcn_writelane((int)value, lane, (int)old);
+}
+__device__ inline int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Prefetch of the next window words.  Issued by inline asm so the compiler
+// does not track them: every copy of an in-flight register (the phi moves
+// its register allocator inserts around the slide) would otherwise wait on
+// vmcnt(0) -- once per group.  The slide waits for them explicitly.  The
+// address is clamped into the record; words past the stream read as 0.
+__device__ inline uint32_t ld_async(const uint32_t *s, int64_t nw, int64_t j) {
+  const int64_t jj = nw > 0 ? (j < nw ? j : nw - 1) : -1;  // s[-1]: the last header word
+  uint32_t v;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(s + jj) : "memory");
+  return v;
+}
+
+// device: one wave per frame.  Pass 1 is wave-uniform (SGPR state): the
+// stream window is 128 words held in two VGPRs (lane j = word w0+j, w0+64+j)
+// read with readlane, the next 128 words in flight one slide ahead, and
+// every window is also copied to an LDS ring that pass 2 reads.  Group k of
+// a batch of 64 goes to lane k (writelane); a full batch is decoded
+// lane-parallel.
+__device__ int32_t scan_wave(const XtcFrame &F, const int *magic, const double *inv, float *o,
+                             uint32_t *ring) {
+  const int lane = (int)(threadIdx.x & 63);
+  const uint32_t *s = F.s;
+  const int64_t nw = F.nw;
+  int64_t w0 = 0;
+  uint32_t c0 = be32w(lane < nw ? s[lane] : 0u), c1 = be32w(64 + lane < nw ? s[64 + lane] : 0u);
+  uint32_t n0 = ld_async(s, nw, 120 + lane), n1 = ld_async(s, nw, 184 + lane);
+  ring[lane] = c0;
+  ring[64 + lane] = c1;
+  const LdsSrc src{ring};
+  uint32_t r_lo = 0, r_hi = 0, r_idx = 0, r_meta = 0;
+  auto flush = [&](int n) {
+    if (lane < n) {
+      XtcGroup g;
+      g.pos = (int64_t)((uint64_t)r_hi << 32 | r_lo);
+      g.idx = (int32_t)r_idx;
+      g.meta = r_meta;
+      decode_group(F, g, magic, inv, o, src);
+    }
+  };
+  int pos = 0, i = 0, run = 0, sidx = F.smallidx0, n = 0;
+  const int natoms = F.natoms, lb = F.large_bits;
+  // bits of the stream past the window start (the overrun check compares
+  // pos with it; clamped to int, the window start is < nbits while decoding)
+  auto room = [&]() { return (int)min((int64_t)0x7fffffff, F.nbits - 32 * w0); };
+  int lim = room();
+  int32_t st = kOk;
+  // The group step of group_step(), restated branch-free for the wave (the
+  // host runs group_step itself; the device kernel is checked against it
+  // bit for bit, statuses included): run = 0 or a multiple of 3, so
+  // run / 3 is the count of small triples in either case; magicints[k] == 0
+  // only for k = 8 (kFirstIdx - 1).
+  while (i < natoms) {
+    pos = uni(pos);
+    const int64_t gpos = w0 * 32 + pos;
+    const int q = pos + lb;  // pos < 3840, lb <= 96: the flag bits lie within words <= 123
+    const int k = q >> 5, k1 = k + 1;
+    const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)c0, k & 63);
+    const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)c1, k & 63);
+    const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)c0, k1 & 63);
+    const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)c1, k1 & 63);
+    const uint32_t a = k < 64 ? a0 : a1, b = k1 < 64 ? b0 : b1;
+    const uint32_t p6 = (uint32_t)((((uint64_t)a << 32 | b) << (q & 31)) >> 58);
+    const uint32_t flag = p6 >> 5, rc = p6 & 31, rm = rc - 3 * ((rc * 0x56u) >> 8);
+    run = flag ? (int)(rc - rm) : run;
+    const int is_smaller = flag ? (int)rm - 1 : 0;
+    const int nsmall = (int)(((uint32_t)run * 0x56u) >> 8);
+    const int idx = i;
+    i += 1 + nsmall;
+    const uint32_t meta = (uint32_t)sidx | (uint32_t)nsmall << 8 | (flag ? 6u : 1u) << 16;
+    pos = q + (flag ? 6 : 1) + nsmall * sidx;
+    const bool bad = i > natoms || (nsmall > 0 && sidx <= kFirstIdx - 1);
+    sidx += is_smaller;
+    if (bad || (unsigned)(sidx - (kFirstIdx - 1)) > (unsigned)(kLastIdx - kFirstIdx)) {
+      st = kCorrupt;
+      break;
+    }
+    while (pos >= 120 * 32) {  // slide by 120 words
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1) : : "memory");
+      pos -= 120 * 32;
+      w0 += 120;
+      c0 = be32w(w0 + lane < nw ? n0 : 0u);
+      c1 = be32w(w0 + 64 + lane < nw ? n1 : 0u);
+      n0 = ld_async(s, nw, w0 + 120 + lane);
+      n1 = ld_async(s, nw, w0 + 184 + lane);
+      ring[(w0 + lane) & (kRing - 1)] = c0;
+      ring[(w0 + 64 + lane) & (kRing - 1)] = c1;
+      lim = room();
+    }
+    if (pos > lim) {
+      st = kCorrupt;
+      break;
+    }
+    n = uni(n);
+    r_lo = writelane(r_lo, (uint32_t)uni((int)(uint32_t)gpos), n);
+    r_hi = writelane(r_hi, (uint32_t)uni((int)(uint32_t)((uint64_t)gpos >> 32)), n);
+    r_idx = writelane(r_idx, (uint32_t)uni(idx), n);
+    r_meta = writelane(r_meta, (uint32_t)uni((int)meta), n);
+    if (++n == 64) {
+      flush(64);
+      n = 0;
+    }
+  }
+  if (st == kOk) flush(n);
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1) : : "memory");  // no load outlives the wave
+  return st;
+}
+
+// One wave per frame (grid = n_frames blocks of 64).
 __global__ __launch_bounds__(64) void k_xtc_decode(const uint32_t *__restrict__ words,
                                                    const int64_t *__restrict__ rec_off,
                                                    const int64_t *__restrict__ rec_len, int64_t n_atoms,
                                                    float *__restrict__ out, int64_t out_stride,
                                                    int32_t *__restrict__ status) {
+  __shared__ uint32_t ring[kRing];
   const int64_t f = blockIdx.x;
   float *o = out + f * out_stride;
-  WaveSink sink{o, 0, 0u, 0u, 0u, 1.0f, false};
-  const int32_t st = decode_record<WaveWindow>(words + rec_off[f], rec_len[f], n_atoms, sink, g_magic.v, g_inv.v);
+  XtcFrame F;
+  bool raw;
+  int32_t st = parse_header(words + rec_off[f], rec_len[f], n_atoms, o, F, &raw);
+  if (st == kOk && !raw) st = scan_wave(F, g_magic.v, g_inv.v, o, ring);
   if (st != kOk) {
     for (int64_t k = threadIdx.x; k < 3 * n_atoms; k += 64) o[k] = __builtin_nanf("");
   }
@@ -583,8 +686,12 @@ RMSF_EXPORT int rmsf_xtc_decode_records_host(const void *h_records, const int64_
     return fail(RMSF_EINVAL, "rmsf_xtc_decode_records_host: bad arguments");
   const uint32_t *w = static_cast<const uint32_t *>(h_records);
   for (int64_t f = 0; f < n_frames; ++f) {
-    MemSink sink{h_out + f * out_stride};
-    h_status[f] = decode_record<MemWindow>(w + h_rec_off[f], h_rec_len[f], n_atoms, sink, h_magic.v, h_inv.v);
+    float *o = h_out + f * out_stride;
+    XtcFrame F;
+    bool raw;
+    int32_t st = parse_header(w + h_rec_off[f], h_rec_len[f], n_atoms, o, F, &raw);
+    if (st == kOk && !raw) st = scan_host(F, h_magic.v, h_inv.v, o);
+    h_status[f] = st;
   }
   return RMSF_OK;
 }

@@ -80,13 +80,29 @@ def test_corrupt_records_are_rejected(tmp_path):
     ln2[2] = 30                                       # frame 2: truncated record
     _, st = _host_decode(bad, off, ln2, n_atoms)
     assert st[0] != 0 and st[1] != 0 and st[2] != 0
-    # garbage compressed bytes never crash the decoder and are flagged or decoded in bounds
+    # garbage compressed bytes never crash the decoder, and it accepts exactly
+    # what the host codec (xtc.cpp, sequential) accepts, with the same atoms
+    from rmsf_amd import RmsfError
+    from rmsf_amd.xtc import XTCFile
     rng = np.random.default_rng(0)
-    for _ in range(20):
+    n_ok = 0
+    for t in range(60):
         g = words.copy()
-        lo = off[0] + 24
+        lo = off[0] + 24 + (t % 5) * 40  # corrupt from a few depths into the stream
         g[lo:off[0] + ln[0]] = rng.integers(0, 2**32, off[0] + ln[0] - lo, dtype=np.uint64).astype(np.uint32)
-        _host_decode(g, off[:1], ln[:1], n_atoms)
+        got, st = _host_decode(g, off[:1], ln[:1], n_atoms)
+        pg = str(tmp_path / f"g{t}.xtc")
+        g.tofile(pg)
+        try:
+            with XTCFile(pg) as f:
+                ref = f.read(0, 1)
+        except RmsfError:
+            ref = None
+        assert (st[0] == 0) == (ref is not None), t
+        if ref is not None:
+            n_ok += 1
+            np.testing.assert_array_equal(got[0], ref[0])
+    assert 0 < n_ok < 60  # both outcomes exercised
 
 
 # -- GPU tier ------------------------------------------------------------------
