@@ -268,9 +268,9 @@ struct MemSrc {
   __host__ __device__ inline uint32_t at(int64_t j) const { return stream_word(s, nw, j); }
 };
 
-// ... or from the wave's LDS ring (device): the last kRing words the window
-// passed, byte-swapped, zero past the stream
-constexpr int kRing = 2048;
+// ... or from the wave's LDS ring (device): kRing words of the stream up
+// to the fill point, byte-swapped, zero past the stream
+constexpr int kRing = 4096;
 struct LdsSrc {
   const uint32_t *ring;
   __device__ inline uint32_t at(int64_t j) const { return ring[j & (kRing - 1)]; }
@@ -454,34 +454,52 @@ __device__ inline uint32_t writelane(uint32_t old, uint32_t value, int lane) {
 }
 __device__ inline int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// Prefetch of the next window words.  Issued by inline asm so the compiler
-// does not track them: every copy of an in-flight register (the phi moves
-// its register allocator inserts around the slide) would otherwise wait on
-// vmcnt(0) -- once per group.  The slide waits for them explicitly.  The
-// address is clamped into the record; words past the stream read as 0.
-__device__ inline uint32_t ld_async(const uint32_t *s, int64_t nw, int64_t j) {
-  const int64_t jj = nw > 0 ? (j < nw ? j : nw - 1) : -1;  // s[-1]: the last header word
-  uint32_t v;
-  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(s + jj) : "memory");
-  return v;
-}
+// Stream words for the device passes come from an LDS ring filled in stages
+// of 512 words (8 per lane), one stage in flight ahead of the fill point.
+// (Loads hidden from the compiler with inline asm were measured wrong: its
+// register allocator copies the destination registers before the data
+// lands.)
+__device__ inline uint32_t ld_word(const uint32_t *s, int64_t nw, int64_t j) { return j < nw ? s[j] : 0u; }
 
-// device: one wave per frame.  Pass 1 is wave-uniform (SGPR state): the
-// stream window is 128 words held in two VGPRs (lane j = word w0+j, w0+64+j)
-// read with readlane, the next 128 words in flight one slide ahead, and
-// every window is also copied to an LDS ring that pass 2 reads.  Group k of
-// a batch of 64 goes to lane k (writelane); a full batch is decoded
-// lane-parallel.
+constexpr int kStage = 512;
+struct RingFill {
+  const uint32_t *s;
+  int64_t nw;
+  uint32_t *ring;
+  int lane;
+  int64_t hi;       // the ring holds stream words [hi - kRing, hi)
+  uint32_t st[8];   // in flight: words hi + 64 v + lane
+  __device__ inline void issue() {
+#pragma unroll
+    for (int v = 0; v < 8; ++v) st[v] = ld_word(s, nw, hi + 64 * v + lane);
+  }
+  __device__ inline void advance() {
+#pragma unroll
+    for (int v = 0; v < 8; ++v) ring[(hi + 64 * v + lane) & (kRing - 1)] = be32w(st[v]);
+    hi += kStage;
+    issue();
+  }
+  __device__ inline void ensure(int64_t word) {  // word < hi afterwards (uniform)
+    while (word >= hi) advance();
+  }
+};
+
+// device: one wave per frame.  Pass 1 (wave-uniform, SGPR state) alternates
+// two steps.  (a) A lane-parallel scan: while the flag bit is 0 a group's
+// length is constant (D = large bits + 1 + run/3 * smallidx), so lane m tests
+// the flag bit of group m at pos + m*D + large bits, and a ballot gives the
+// count K of clean groups ahead (flag 0, inside the stream, the atom count
+// and the ring); their records are written lane-parallel.  (b) For the
+// group the scan stopped at (a set flag, the frame's end, or a corrupt
+// stream) the sequential step: a 6-bit peek and group_step(), exactly as on
+// the host.  Group k of a batch of 64 lives in lane k; a full batch is
+// decoded lane-parallel (pass 2) from the LDS ring.
 __device__ int32_t scan_wave(const XtcFrame &F, const int *magic, const double *inv, float *o,
                              uint32_t *ring) {
   const int lane = (int)(threadIdx.x & 63);
-  const uint32_t *s = F.s;
-  const int64_t nw = F.nw;
-  int64_t w0 = 0;
-  uint32_t c0 = be32w(lane < nw ? s[lane] : 0u), c1 = be32w(64 + lane < nw ? s[64 + lane] : 0u);
-  uint32_t n0 = ld_async(s, nw, 120 + lane), n1 = ld_async(s, nw, 184 + lane);
-  ring[lane] = c0;
-  ring[64 + lane] = c1;
+  RingFill rf{F.s, F.nw, ring, lane, 0, {}};
+  rf.issue();
+  rf.advance();  // words [0, 512) in the ring, [512, 1024) in flight
   const LdsSrc src{ring};
   uint32_t r_lo = 0, r_hi = 0, r_idx = 0, r_meta = 0;
   auto flush = [&](int n) {
@@ -493,60 +511,71 @@ __device__ int32_t scan_wave(const XtcFrame &F, const int *magic, const double *
       decode_group(F, g, magic, inv, o, src);
     }
   };
-  int pos = 0, i = 0, run = 0, sidx = F.smallidx0, n = 0;
+  auto rd = [&](int64_t j) { return (uint32_t)uni((int)ring[j & (kRing - 1)]); };
+  int64_t pos = 0;
+  int i = 0, run = 0, sidx = F.smallidx0, n = 0;
   const int natoms = F.natoms, lb = F.large_bits;
-  // bits of the stream past the window start (the overrun check compares
-  // pos with it; clamped to int, the window start is < nbits while decoding)
-  auto room = [&]() { return (int)min((int64_t)0x7fffffff, F.nbits - 32 * w0); };
-  int lim = room();
+  const int64_t nbits = F.nbits;
   int32_t st = kOk;
-  // The group step of group_step(), restated branch-free for the wave (the
-  // host runs group_step itself; the device kernel is checked against it
-  // bit for bit, statuses included): run = 0 or a multiple of 3, so
-  // run / 3 is the count of small triples in either case; magicints[k] == 0
-  // only for k = 8 (kFirstIdx - 1).
   while (i < natoms) {
-    pos = uni(pos);
-    const int64_t gpos = w0 * 32 + pos;
-    const int q = pos + lb;  // pos < 3840, lb <= 96: the flag bits lie within words <= 123
-    const int k = q >> 5, k1 = k + 1;
-    const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)c0, k & 63);
-    const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)c1, k & 63);
-    const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)c0, k1 & 63);
-    const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)c1, k1 & 63);
-    const uint32_t a = k < 64 ? a0 : a1, b = k1 < 64 ? b0 : b1;
-    const uint32_t p6 = (uint32_t)((((uint64_t)a << 32 | b) << (q & 31)) >> 58);
-    const uint32_t flag = p6 >> 5, rc = p6 & 31, rm = rc - 3 * ((rc * 0x56u) >> 8);
-    run = flag ? (int)(rc - rm) : run;
-    const int is_smaller = flag ? (int)rm - 1 : 0;
-    const int nsmall = (int)(((uint32_t)run * 0x56u) >> 8);
-    const int idx = i;
-    i += 1 + nsmall;
-    const uint32_t meta = (uint32_t)sidx | (uint32_t)nsmall << 8 | (flag ? 6u : 1u) << 16;
-    pos = q + (flag ? 6 : 1) + nsmall * sidx;
-    const bool bad = i > natoms || (nsmall > 0 && sidx <= kFirstIdx - 1);
-    sidx += is_smaller;
-    if (bad || (unsigned)(sidx - (kFirstIdx - 1)) > (unsigned)(kLastIdx - kFirstIdx)) {
-      st = kCorrupt;
-      break;
-    }
-    while (pos >= 120 * 32) {  // slide by 120 words
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1) : : "memory");
-      pos -= 120 * 32;
-      w0 += 120;
-      c0 = be32w(w0 + lane < nw ? n0 : 0u);
-      c1 = be32w(w0 + 64 + lane < nw ? n1 : 0u);
-      n0 = ld_async(s, nw, w0 + 120 + lane);
-      n1 = ld_async(s, nw, w0 + 184 + lane);
-      ring[(w0 + lane) & (kRing - 1)] = c0;
-      ring[(w0 + 64 + lane) & (kRing - 1)] = c1;
-      lim = room();
-    }
-    if (pos > lim) {
-      st = kCorrupt;
-      break;
-    }
+    i = uni(i);
+    run = uni(run);
+    sidx = uni(sidx);
     n = uni(n);
+    // (a) scan of clean (flag 0) groups; run is 0 or a multiple of 3
+    const int ns = (int)(((uint32_t)run * 0x56u) >> 8);
+    const int D = lb + 1 + ns * sidx;
+    int K = 0;
+    if (!(ns > 0 && sidx <= kFirstIdx - 1)) {  // magicints[8] == 0: a run there is corrupt
+      rf.ensure((pos >> 5) + 192);
+      const int64_t P = pos + (int64_t)lane * D + lb;                // flag bit of group `lane`
+      const int64_t endb = P + 1 + (int64_t)ns * sidx;                // end of its small triples
+      const int64_t im = (int64_t)i + (int64_t)lane * (1 + ns);      // its first atom
+      bool stop = im + 1 + ns > natoms || endb > nbits || ((endb + 95) >> 5) >= rf.hi;
+      if (!stop) stop = ((ring[(P >> 5) & (kRing - 1)] >> (31 - (int)(P & 31))) & 1u) != 0;
+      const uint64_t m = __ballot(stop);
+      K = uni(m ? (int)__builtin_ctzll(m) : 64);
+    }
+    if (K > 0) {
+      const uint32_t meta0 = (uint32_t)sidx | (uint32_t)ns << 8 | 1u << 16;
+      for (int done = 0; done < K;) {
+        const int take = min(K - done, 64 - n);
+        if (lane >= n && lane < n + take) {
+          const int mm = done + (lane - n);
+          const int64_t gp = pos + (int64_t)mm * D;
+          r_lo = (uint32_t)gp;
+          r_hi = (uint32_t)((uint64_t)gp >> 32);
+          r_idx = (uint32_t)(i + mm * (1 + ns));
+          r_meta = meta0;
+        }
+        n += take;
+        done += take;
+        if (n == 64) {
+          flush(64);
+          n = 0;
+        }
+      }
+      pos += (int64_t)K * D;
+      i += K * (1 + ns);
+      continue;
+    }
+    // (b) sequential step for the group at pos
+    const int64_t q = pos + lb;
+    rf.ensure(((q + 6 + 720 + 95) >> 5) + 1);  // flag bits and up to 10 small triples of <= 72 bits
+    const uint32_t p6 = (uint32_t)((((uint64_t)rd(q >> 5) << 32 | rd((q >> 5) + 1)) << (q & 31)) >> 58);
+    int adv;
+    uint32_t meta;
+    const int idx = i;
+    if (!group_step(F, magic, p6, i, run, sidx, adv, meta)) {
+      st = kCorrupt;
+      break;
+    }
+    const int64_t gpos = pos;
+    pos = q + adv;
+    if (pos > nbits) {
+      st = kCorrupt;
+      break;
+    }
     r_lo = writelane(r_lo, (uint32_t)uni((int)(uint32_t)gpos), n);
     r_hi = writelane(r_hi, (uint32_t)uni((int)(uint32_t)((uint64_t)gpos >> 32)), n);
     r_idx = writelane(r_idx, (uint32_t)uni(idx), n);
@@ -557,7 +586,6 @@ __device__ int32_t scan_wave(const XtcFrame &F, const int *magic, const double *
     }
   }
   if (st == kOk) flush(n);
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(n0), "+v"(n1) : : "memory");  // no load outlives the wave
   return st;
 }
 

@@ -30,13 +30,23 @@ def water_like(rng, n_atoms, n_frames):
     return np.stack([base + rng.normal(0, 0.3, base.shape) for _ in range(n_frames)]).astype(np.float32)
 
 
+def protein_like(rng, n_atoms, n_frames):
+    """Chains of bonded atoms (1.5 A steps): frequent runs and flag bits,
+    the hard case for the decoder's clean-group scan (~18 % flagged groups)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_xtc import _protein_like
+    return _protein_like(rng, n_atoms, n_frames)
+
+
 def main():
     ns = [int(a) for a in sys.argv[1:]] or [400, 4096]
     lib = load()
     n_atoms, K = 250_000, 32
     dev = torch.device("cuda")
-    for kind in os.environ.get("UB_KINDS", "uniform,water").split(","):
-        x = SY.frames(0, n_atoms, 0, K) if kind == "uniform" else water_like(np.random.default_rng(1), n_atoms, K)
+    for kind in os.environ.get("UB_KINDS", "uniform,water,protein").split(","):
+        rng = np.random.default_rng(1)
+        x = (SY.frames(0, n_atoms, 0, K) if kind == "uniform" else
+             water_like(rng, n_atoms, K) if kind == "water" else protein_like(rng, n_atoms, K))
         path = os.path.join(tempfile.mkdtemp(), "u.xtc")
         write_xtc(path, x)
         with XTCFile(path) as f:
