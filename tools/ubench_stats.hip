@@ -219,7 +219,7 @@ __global__ __launch_bounds__(B) void k_lanes_frames(const float *__restrict__ xy
 // reads, ds_write_b128 staging); next tile prefetched into registers while the
 // current one is consumed; ref wave-uniform -> scalar loads, one 4-atom group
 // per iteration (bounded SGPR use).
-template <int TA2>
+template <int TA2, bool NOMATH = false>
 __global__ __launch_bounds__(B) void k_lanes_frames2(const float *__restrict__ xyz, int64_t fstride, int64_t n_frames, int64_t n,
                                                    int64_t chunk, const double *__restrict__ ref, double *__restrict__ out) {
   constexpr int P2 = 3 * TA2 + 4;
@@ -258,6 +258,10 @@ __global__ __launch_bounds__(B) void k_lanes_frames2(const float *__restrict__ x
     __syncthreads();
     if (t0 + TA2 < a_end) gload(t0 + TA2);
     const f4 *my = reinterpret_cast<const f4 *>(tile + lane * P2 + w * 3 * APW);
+    if (NOMATH) {  // staging floor: keep one LDS read so the tile is consumed
+      acc[0] += my[0].x;
+      continue;
+    }
 #pragma unroll 1
     for (int g = 0; g < APW / 4; ++g) {
       const f4 q0 = my[3 * g], q1 = my[3 * g + 1], q2 = my[3 * g + 2];
@@ -288,8 +292,21 @@ __global__ __launch_bounds__(B) void k_lanes_frames2(const float *__restrict__ x
   if (t == 12345.678) out[f] = t;
 }
 
+// pseudo-random coordinates in [0, 100): real-looking bit patterns (the
+// memset pattern toggles few bits -- HBM/DVFS behaviour may depend on it)
+__global__ void k_fill_random(float *x, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    x[i] = (float)(h & 0xffffff) * (100.0f / 16777216.0f);
+  }
+}
+
 int main() {
-  const int64_t n = 100352, nf = 2000, fs = 3 * n;  // n: multiple of the 64-atom tile (no tail handling in V4)
+  const bool occ = getenv("UB_SET") && getenv("UB_SET")[0] == 'O';
+  const int64_t n = getenv("UB_N") ? atoll(getenv("UB_N")) : 100352, nf = occ ? 20000 : 2000, fs = 3 * n;  // n: multiple of the 64-atom tile (no tail handling in V4)
   float *x;
   double *ref, *out;
   CK(hipMalloc(&x, sizeof(float) * fs * nf));
@@ -314,6 +331,45 @@ int main() {
     ms /= R;
     printf("%-44s %8.3f ms  %7.0f GB/s (12 B/atom-frame)\n", name, ms, bytes / ms / 1e6);
   };
+  if (occ) {  // full C3 size: occupancy (blocks per CU via dynamic LDS) x chunk
+    int lds_max = 0;
+    CK(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, 0));
+    const int stat = 64 * (3 * 32 + 4) * 4;
+    for (int rep = 0; rep < 2; ++rep)
+      for (int64_t chunk : {1024, 1888, 2048}) {
+        if (rep == 1 && chunk == 1024) {
+          hipLaunchKernelGGL(k_fill_random, dim3(8192), dim3(256), 0, 0, x, fs * nf);
+          CK(hipDeviceSynchronize());
+          printf("-- random coordinates from here on --\n");
+        }
+        const int64_t nchunk = (n + chunk - 1) / chunk;
+        for (int k : {0, 2, 3, 4}) {
+          const int dyn = k ? lds_max / k - stat - 512 : 0;
+          char nm[80];
+          snprintf(nm, sizeof nm, "V11 TA=32 chunk=%lld blocks/CU<=%d", (long long)chunk, k ? k : 6);
+          run(nm, [&] {
+            hipLaunchKernelGGL((k_lanes_frames2<32>), dim3((nf + TF - 1) / TF, nchunk), dim3(B), dyn, 0, x, fs, nf, n, chunk, ref, out);
+          });
+        }
+        {
+          char nm2[80];
+          snprintf(nm2, sizeof nm2, "V10 TA=64 chunk=%lld", (long long)chunk);
+          run(nm2, [&] {
+            hipLaunchKernelGGL((k_lanes_frames2<64>), dim3((nf + TF - 1) / TF, nchunk), dim3(B), 0, 0, x, fs, nf, n, chunk, ref, out);
+          });
+          snprintf(nm2, sizeof nm2, "V12 TA=16 chunk=%lld", (long long)chunk);
+          run(nm2, [&] {
+            hipLaunchKernelGGL((k_lanes_frames2<16>), dim3((nf + TF - 1) / TF, nchunk), dim3(B), 0, 0, x, fs, nf, n, chunk, ref, out);
+          });
+        }
+        char nm[80];
+        snprintf(nm, sizeof nm, "V11 staging only chunk=%lld", (long long)chunk);
+        run(nm, [&] {
+          hipLaunchKernelGGL((k_lanes_frames2<32, true>), dim3((nf + TF - 1) / TF, nchunk), dim3(B), 0, 0, x, fs, nf, n, chunk, ref, out);
+        });
+      }
+    return 0;
+  }
   run("V0 rowwise full (nt frame + ref)", [&] { hipLaunchKernelGGL(k_rowwise<0>, dim3(nf), dim3(B), 0, 0, x, fs, n, ref, out); });
   run("V1 rowwise, no ref loads", [&] { hipLaunchKernelGGL(k_rowwise<1>, dim3(nf), dim3(B), 0, 0, x, fs, n, ref, out); });
   run("V2 rowwise, ref, 3 sums", [&] { hipLaunchKernelGGL(k_rowwise<2>, dim3(nf), dim3(B), 0, 0, x, fs, n, ref, out); });
