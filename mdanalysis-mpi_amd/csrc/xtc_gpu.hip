@@ -619,6 +619,8 @@ const char *status_text(int32_t s) {
   }
 }
 
+constexpr size_t kReadPiece = 128u << 20;  // bytes read (and then copied) at a time
+
 // Parallel pread of [off, off+n) into dst (n_threads chunks).
 bool pread_par(int fd, unsigned char *dst, size_t n, int64_t off, int n_threads) {
   const size_t chunk = std::max<size_t>(1 << 20, (n + n_threads - 1) / std::max(1, n_threads));
@@ -785,11 +787,21 @@ int xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_t step, float *ou
   const rmsf_xtc *x = d->x;
   int64_t *off = s.h_tab, *len = s.h_tab + d->batch;
   size_t total = 0;
+  bool copied = false;
   if (step == 1) {
     const int64_t a = x->offset[f0], e = x->offset[f0 + n - 1] + x->size[f0 + n - 1];
     total = (size_t)(e - a);
     if (total > s.raw_cap) return fail(RMSF_EINVAL, "rmsf_xtcdec_decode: batch larger than the slot");
-    if (!pread_par(x->fd, s.h_raw, total, a, d->n_threads)) return fail(RMSF_EINVAL, "xtc: read failed");
+    // read in pieces, each copied as soon as it is in the pinned slot: the
+    // host->device DMA of piece k overlaps the file read of piece k+1
+    for (size_t done = 0; done < total;) {
+      const size_t len = std::min(kReadPiece, total - done);
+      if (!pread_par(x->fd, s.h_raw + done, len, a + (int64_t)done, d->n_threads))
+        return fail(RMSF_EINVAL, "xtc: read failed");
+      XD_HIP(hipMemcpyAsync(s.d_raw + done, s.h_raw + done, len, hipMemcpyHostToDevice, s.s));
+      done += len;
+    }
+    copied = true;
     for (int64_t k = 0; k < n; ++k) {
       off[k] = (x->offset[f0 + k] - a) / 4;
       len[k] = x->size[f0 + k] / 4;
@@ -815,7 +827,7 @@ int xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_t step, float *ou
     for (char c : ok)
       if (!c) return fail(RMSF_EINVAL, "xtc: read failed");
   }
-  XD_HIP(hipMemcpyAsync(s.d_raw, s.h_raw, total, hipMemcpyHostToDevice, s.s));
+  if (!copied) XD_HIP(hipMemcpyAsync(s.d_raw, s.h_raw, total, hipMemcpyHostToDevice, s.s));
   XD_HIP(hipMemcpyAsync(s.d_tab, s.h_tab, 2 * d->batch * sizeof(int64_t), hipMemcpyHostToDevice, s.s));
   if (!out) {
     if (!s.d_frames) {
