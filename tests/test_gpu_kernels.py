@@ -156,13 +156,15 @@ def test_welford_noalign(eng, n_sel, nf, splits):
 @pytest.mark.parametrize("n_sel,nf,groups,gather", [
     (4096, 1000, 0, False), (4096, 1000, 1, False), (4096, 1000, 3, False), (1001, 333, 0, False),
     (1001, 333, 7, True), (3, 5, 0, False), (3, 5, 2, True), (300, 9000, 1, False), (300, 9000, 5, True),
-    (2048, 700, 3000, False), (100_000, 64, 0, False), (257, 4097, 2, False)])
+    (2048, 700, 3000, False), (100_000, 64, 0, False), (257, 4097, 2, False),
+    (300_000, 64, 0, False), (300_000, 33, 0, False), (250_000, 50, 0, True)])
 def test_balanced_welford_and_sum(eng, n_sel, nf, groups, gather):
     """Balanced grid (rmsf_accumulate_balanced + rmsf_fold_balanced): float4
     and atom-per-lane layouts, forced workgroup counts (1 = one workgroup
     walks every chunk; 9000 frames cut segments at RMSF_MAX_SPLIT_FRAMES;
-    3000 > the chunk-frame count clamps), and a running fold over two
-    batches, against the f64 two-pass variance and the f64 sum."""
+    3000 > the chunk-frame count clamps; 250k-300k atoms: more chunks than
+    workgroups, chunk-aligned ranges), and a running fold over two batches,
+    against the f64 two-pass variance and the f64 sum."""
     from rmsf_amd.synth import generate
     from rmsf_amd._lib import RMSF_MODE_SUM, RMSF_MODE_WELFORD
     n_atoms = n_sel + 17 if gather else n_sel
