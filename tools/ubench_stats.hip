@@ -10,6 +10,7 @@
 //      tile staged through LDS; ref via scalar loads; no cross-lane reduce
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -309,7 +310,20 @@ int main() {
   const int64_t n = getenv("UB_N") ? atoll(getenv("UB_N")) : 100352, nf = occ ? 20000 : 2000, fs = 3 * n;  // n: multiple of the 64-atom tile (no tail handling in V4)
   float *x;
   double *ref, *out;
-  CK(hipMalloc(&x, sizeof(float) * fs * nf));
+  // UB_ALIGN=<bytes>: over-allocate and start the trajectory at that
+  // virtual-address alignment (placement probe); UB_SHIFT=<bytes>: plus an offset
+  const size_t ub_align = getenv("UB_ALIGN") ? strtoull(getenv("UB_ALIGN"), nullptr, 0) : 0;
+  const size_t ub_shift = getenv("UB_SHIFT") ? strtoull(getenv("UB_SHIFT"), nullptr, 0) : 0;
+  {
+    char *raw;
+    CK(hipMalloc(&raw, sizeof(float) * fs * nf + ub_align + ub_shift));
+    uintptr_t p = (uintptr_t)raw;
+    if (ub_align) p = (p + ub_align - 1) / ub_align * ub_align;
+    p += ub_shift;
+    x = (float *)p;
+    printf("trajectory base %p (raw %p) mod 1 GiB = %zu MiB\n", (void *)x, (void *)raw,
+           (size_t)(((uintptr_t)x) % (1ull << 30)) >> 20);
+  }
   CK(hipMalloc(&ref, sizeof(double) * 3 * n));
   CK(hipMalloc(&out, sizeof(double) * nf));
   CK(hipMemset(x, 0x3f, sizeof(float) * fs * nf));  // non-zero operands (DVFS)
