@@ -25,6 +25,10 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <mutex>
+#include <memory>
+#include <functional>
+#include <condition_variable>
 #include <string>
 #include <thread>
 #include <vector>
@@ -621,17 +625,70 @@ const char *status_text(int32_t s) {
 
 constexpr size_t kReadPiece = 128u << 20;  // bytes read (and then copied) at a time
 
-// Parallel pread of [off, off+n) into dst (n_threads chunks).
-bool pread_par(int fd, unsigned char *dst, size_t n, int64_t off, int n_threads) {
-  const size_t chunk = std::max<size_t>(1 << 20, (n + n_threads - 1) / std::max(1, n_threads));
-  std::vector<std::thread> th;
-  std::vector<char> ok((n + chunk - 1) / chunk + 1, 1);
-  size_t k = 0;
-  for (size_t s = 0; s < n; s += chunk, ++k) {
-    const size_t len = std::min(chunk, n - s);
-    th.emplace_back([&, s, len, k] { ok[k] = rmsf_internal_pread_all(fd, dst + s, len, off + (int64_t)s); });
+// Persistent worker threads for the file reads (a batch is read in several
+// pieces; spawning threads per piece cost ~0.2 ms each).  run(n, fn) calls
+// fn(0..n-1) on the workers and returns when all are done.
+class ReadPool {
+ public:
+  explicit ReadPool(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
   }
-  for (auto &t : th) t.join();
+  ~ReadPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+  }
+  void run(int64_t n, const std::function<void(int64_t)> &fn) {
+    std::unique_lock<std::mutex> g(m_);
+    fn_ = &fn;
+    next_ = 0;
+    total_ = n;
+    left_ = n;
+    ++gen_;
+    cv_.notify_all();
+    done_.wait(g, [this] { return left_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> g(m_);
+    for (;;) {
+      cv_.wait(g, [&] { return stop_ || (gen_ != seen && next_ < total_); });
+      if (stop_) return;
+      while (next_ < total_) {
+        const int64_t i = next_++;
+        const std::function<void(int64_t)> *fn = fn_;
+        g.unlock();
+        (*fn)(i);
+        g.lock();
+        if (--left_ == 0) done_.notify_all();
+      }
+      seen = gen_;
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int64_t)> *fn_ = nullptr;
+  int64_t next_ = 0, total_ = 0, left_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+// Parallel pread of [off, off+n) into dst: pieces of >= 1 MiB over the pool.
+bool pread_par(ReadPool &pool, int n_threads, int fd, unsigned char *dst, size_t n, int64_t off) {
+  const size_t chunk = std::max<size_t>(1 << 20, (n + n_threads - 1) / std::max(1, n_threads));
+  const int64_t pieces = (int64_t)((n + chunk - 1) / chunk);
+  std::vector<char> ok(pieces, 1);
+  pool.run(pieces, [&](int64_t k) {
+    const size_t s = (size_t)k * chunk, len = std::min(chunk, n - s);
+    ok[k] = rmsf_internal_pread_all(fd, dst + s, len, off + (int64_t)s);
+  });
   return std::all_of(ok.begin(), ok.end(), [](char c) { return c != 0; });
 }
 
@@ -641,6 +698,7 @@ struct rmsf_xtcdec {
   const rmsf_xtc *x = nullptr;
   int64_t batch = 0, n_atoms = 0;
   int n_threads = 1;
+  std::unique_ptr<ReadPool> pool;
   struct Slot {
     unsigned char *h_raw = nullptr;
     int64_t *h_tab = nullptr;  // [2][batch]: record offset (words), record length (words)
@@ -736,6 +794,7 @@ RMSF_EXPORT int rmsf_xtcdec_create(const rmsf_xtc *x, int64_t batch_frames, int 
   d->batch = batch_frames;
   d->n_atoms = x->n_atoms;
   d->n_threads = n_threads;
+  d->pool = std::make_unique<ReadPool>(n_threads);
   d->slots.resize(n_slots);
   const size_t raw = (size_t)batch_frames * (size_t)x->max_size;
   for (auto &s : d->slots) {
@@ -796,7 +855,7 @@ int xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_t step, float *ou
     // host->device DMA of piece k overlaps the file read of piece k+1
     for (size_t done = 0; done < total;) {
       const size_t len = std::min(kReadPiece, total - done);
-      if (!pread_par(x->fd, s.h_raw + done, len, a + (int64_t)done, d->n_threads))
+      if (!pread_par(*d->pool, d->n_threads, x->fd, s.h_raw + done, len, a + (int64_t)done))
         return fail(RMSF_EINVAL, "xtc: read failed");
       XD_HIP(hipMemcpyAsync(s.d_raw + done, s.h_raw + done, len, hipMemcpyHostToDevice, s.s));
       done += len;
@@ -814,16 +873,11 @@ int xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_t step, float *ou
       total += (size_t)x->size[f];
     }
     if (total > s.raw_cap) return fail(RMSF_EINVAL, "rmsf_xtcdec_decode: batch larger than the slot");
-    std::vector<std::thread> th;
-    std::vector<char> ok(d->n_threads, 1);
-    for (int t = 0; t < d->n_threads; ++t)
-      th.emplace_back([&, t] {
-        for (int64_t k = t; k < n; k += d->n_threads) {
-          const int64_t f = f0 + k * step;
-          if (!rmsf_internal_pread_all(x->fd, s.h_raw + 4 * off[k], (size_t)x->size[f], x->offset[f])) ok[t] = 0;
-        }
-      });
-    for (auto &t : th) t.join();
+    std::vector<char> ok(n, 1);
+    d->pool->run(n, [&](int64_t k) {
+      const int64_t f = f0 + k * step;
+      ok[k] = rmsf_internal_pread_all(x->fd, s.h_raw + 4 * off[k], (size_t)x->size[f], x->offset[f]);
+    });
     for (char c : ok)
       if (!c) return fail(RMSF_EINVAL, "xtc: read failed");
   }
