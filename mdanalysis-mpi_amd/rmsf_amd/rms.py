@@ -122,8 +122,16 @@ class RMSF:
         if isinstance(x, (str, bytes)) or hasattr(x, "__fspath__"):
             import os
             path = os.fspath(x)
+            if str(path).lower().endswith(".dcd"):
+                # DCD frames are raw float32 planes: read the selected rows on the host,
+                # stream them through the pinned stager
+                from .dcd import DCDFile
+
+                with DCDFile(path) as f:
+                    frames = f.read(sel=self.select)
+                return HostSource(frames, None, batch_frames=self.batch_frames), self.masses
             if not str(path).lower().endswith(".xtc"):
-                raise ValueError(f"only .xtc trajectory files are read natively, got {path!r}")
+                raise ValueError(f"only .xtc and .dcd trajectory files are read natively, got {path!r}")
             # aligned runs read the reference frame first (and RMSF.py's two sweeps read
             # every frame twice): keep the decoded frames resident in HBM
             return XtcSource(path, self.select, batch_frames=self.batch_frames,

@@ -1,13 +1,14 @@
-"""Minimal GRO topology + selection fallback.
+"""Minimal GRO / PSF topologies + selection fallback.
 
 RMSF.py builds ``mda.Universe(GRO, XTC)`` (RMSF.py:34,56) and selects
-``"protein and name CA"`` (RMSF.py:77,116,120,126).  When MDAnalysis is not
-installed, this module reads the GRO file itself and evaluates a subset of
-the MDAnalysis selection language, so the whole script runs natively:
+``"protein and name CA"`` (RMSF.py:77,116,120,126); BASELINE config C1 names
+the PSF/DCD pair of the same adk system.  When MDAnalysis is not installed,
+this module reads the GRO or PSF file itself and evaluates a subset of the
+MDAnalysis selection language, so the whole script runs natively:
 
-    top = GroTopology("adk.gro")
+    top = GroTopology("adk.gro")                   # or PsfTopology("adk.psf")
     sel = top.select("protein and name CA")        # sorted atom indices
-    RMSF("adk.xtc", select=sel, align="average").run()
+    RMSF("adk.xtc", select=sel, align="average").run()   # or "adk.dcd"
 
 Supported selection grammar (MDAnalysis keywords and precedence: ``not`` >
 ``and`` > ``or``, parentheses): ``all``, ``none``, ``protein``, ``backbone``
@@ -40,7 +41,71 @@ CME ASF
 BACKBONE_NAMES = frozenset(["N", "CA", "C", "O"])
 
 
-class GroTopology:
+class Topology:
+    """Per-atom resids, resnames, names (and masses when the file has them)."""
+
+    resids: np.ndarray
+    resnames: np.ndarray
+    names: np.ndarray
+    masses: np.ndarray | None = None
+    n_atoms: int
+
+    def select(self, selection: str) -> np.ndarray:
+        """Sorted unique atom indices (MDAnalysis ordering) matching ``selection``."""
+        mask = _Parser(selection, self).parse()
+        return np.flatnonzero(mask)
+
+
+class PsfTopology(Topology):
+    """The atoms of a CHARMM/NAMD/X-PLOR .psf file (the ``!NATOM`` section:
+    id, segid, resid, resname, name, type, charge, mass, ...), as MDAnalysis'
+    PSFParser reads them: standard and EXT layouts are both whitespace
+    separated; resids keep their leading integer (insertion codes dropped);
+    masses are float64 (MDAnalysis keeps them as read)."""
+
+    def __init__(self, path: str):
+        self.path = path
+        lines = open(path).read().splitlines()
+        if not lines or not lines[0].startswith("PSF"):
+            raise ValueError(f"{path}: not a PSF file (first line must start with 'PSF')")
+        for k, line in enumerate(lines):
+            if "!NATOM" in line:
+                n = int(line.split()[0])
+                body = lines[k + 1:k + 1 + n]
+                break
+        else:
+            raise ValueError(f"{path}: no !NATOM section")
+        if len(body) < n:
+            raise ValueError(f"{path}: !NATOM announces {n} atoms, {len(body)} lines follow")
+        resids, resnames, names, masses = [], [], [], []
+        for line in body:
+            f = line.split()
+            if len(f) < 8:
+                raise ValueError(f"{path}: short atom line {line!r}")
+            m = re.match(r"-?\d+", f[2])
+            resids.append(int(m.group(0)) if m else 0)
+            resnames.append(f[3])
+            names.append(f[4])
+            masses.append(float(f[7]))
+        self.resids = np.array(resids, dtype=np.int64)
+        self.resnames = np.array(resnames, dtype=object)
+        self.names = np.array(names, dtype=object)
+        self.masses = np.array(masses, dtype=np.float64)
+        self.n_atoms = n
+
+
+def write_psf(path: str, resids, resnames, names, masses=None, segid="PROT", title="rmsf_amd"):
+    """Write a minimal standard-layout .psf (atoms only; tests/tools)."""
+    masses = np.full(len(names), 12.011) if masses is None else np.asarray(masses, dtype=np.float64)
+    with open(path, "w") as fh:
+        fh.write(f"PSF\n\n{1:8d} !NTITLE\n* {title}\n\n{len(names):8d} !NATOM\n")
+        for k, (ri, rn, an, m) in enumerate(zip(resids, resnames, names, masses)):
+            fh.write(f"{k + 1:8d} {segid:<4s} {int(ri):<4d} {rn:<4s} {an:<4s} {an[:4]:<4s} {0.0:10.6f} "
+                     f"{m:13.4f} {0:11d}\n")
+        fh.write(f"\n{0:8d} !NBOND: bonds\n\n")
+
+
+class GroTopology(Topology):
     """Atoms (resid, resname, name) and the frames of a .gro file.
 
     ``positions`` follow MDAnalysis' GROReader rounding: the text is parsed
@@ -92,11 +157,6 @@ class GroTopology:
             raise ValueError(f"{path}: no complete GRO frame")
         return frames, atoms
 
-    def select(self, selection: str) -> np.ndarray:
-        """Sorted unique atom indices (MDAnalysis ordering) matching ``selection``."""
-        mask = _Parser(selection, self).parse()
-        return np.flatnonzero(mask)
-
 
 # ---------------------------------------------------------------------------
 _TOKEN = re.compile(r"\(|\)|[^\s()]+")
@@ -109,7 +169,7 @@ class _Parser:
     KEYWORDS = {"and", "or", "not", "(", ")"}
     SELECTORS = {"all", "none", "protein", "backbone", "name", "resname", "resid", "index", "bynum"}
 
-    def __init__(self, text: str, top: GroTopology):
+    def __init__(self, text: str, top: Topology):
         self.tok = _TOKEN.findall(text)
         self.i = 0
         self.top = top

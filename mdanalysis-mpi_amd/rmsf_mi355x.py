@@ -9,9 +9,10 @@
     # without MDAnalysis: a synthetic trajectory generated in HBM
     python rmsf_mi355x.py --synthetic 100000 2000 --align frame0
 
-Without MDAnalysis, a .gro topology and an .xtc (or multi-frame .gro)
-trajectory are read natively (rmsf_amd.topology / rmsf_amd.xtc) and the
-selection is evaluated by the native subset of the selection language.
+Without MDAnalysis, a .gro or .psf topology and an .xtc, .dcd (or
+multi-frame .gro) trajectory are read natively (rmsf_amd.topology /
+rmsf_amd.xtc / rmsf_amd.dcd) and the selection is evaluated by the native
+subset of the selection language (BASELINE C1: adk PSF/DCD).
 
 Defaults mirror RMSF.py: selection "protein and name CA" (RMSF.py:77),
 ref_frame 0 (RMSF.py:63), the two-sweep average alignment (RMSF.py:89-140),
@@ -80,15 +81,21 @@ def main(argv=None) -> int:
             ag = u.select_atoms(a.select)
             rmsf = RMSF(ag, align=align, ref_frame=a.ref_frame, verbose=True).run().results.rmsf
         else:
-            # native fallback: GRO topology + selection subset, XTC (or multi-frame GRO) trajectory
-            from rmsf_amd.topology import GroTopology
+            # native fallback: GRO or PSF topology + selection subset; XTC, DCD (or
+            # multi-frame GRO) trajectory.  PSF masses feed the mass-weighted
+            # centre of mass RMSF.py uses (RMSF.py:84,94,117,127).
+            from rmsf_amd.topology import GroTopology, PsfTopology
 
-            if not a.topology.lower().endswith(".gro"):
-                ap.error("without MDAnalysis only .gro topologies are read natively")
-            top = GroTopology(a.topology)
+            ext = a.topology.lower().rsplit(".", 1)[-1]
+            if ext not in ("gro", "psf"):
+                ap.error("without MDAnalysis only .gro and .psf topologies are read natively")
+            top = GroTopology(a.topology) if ext == "gro" else PsfTopology(a.topology)
             sel = top.select(a.select)
-            traj = a.trajectory if a.trajectory.lower().endswith(".xtc") else GroTopology(a.trajectory).frames
-            rmsf = RMSF(traj, select=sel, align=align, ref_frame=a.ref_frame, verbose=True).run().results.rmsf
+            masses = None if top.masses is None else top.masses[sel]
+            traj = (a.trajectory if a.trajectory.lower().endswith((".xtc", ".dcd"))
+                    else GroTopology(a.trajectory).frames)
+            rmsf = RMSF(traj, select=sel, align=align, masses=masses, ref_frame=a.ref_frame,
+                        verbose=True).run().results.rmsf
     if rank == 0:
         print(f"RMSF over {len(rmsf)} atoms: mean {rmsf.mean():.6f} A, max {rmsf.max():.6f} A", flush=True)
         if a.out:

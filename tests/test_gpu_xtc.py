@@ -67,3 +67,43 @@ def test_script_mode_gro_xtc_native(tmp_path):
         dec = f.read()
     exp = O.rmsf_script(dec, sel, None, size=1, align="average")["rmsf"]
     np.testing.assert_allclose(np.load(out), exp, rtol=0, atol=1e-6)
+
+
+def test_script_mode_psf_dcd_native(tmp_path):
+    """BASELINE config C1's file pair: the adk shape (3341 atoms, 214 CA, 98
+    frames) as PSF + DCD, RMSF.py's defaults (protein and name CA, mass-
+    weighted COM from the PSF masses, two-sweep average), without MDAnalysis;
+    and RMSF() reading the .dcd directly, with a frame slice."""
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+    from oracle import synth as SY
+    from rmsf_amd import RMSF
+    from rmsf_amd.dcd import write_dcd
+    from rmsf_amd.synth import motion_table
+    from rmsf_amd.topology import PsfTopology, write_psf
+    n_res, n_atoms, nf = 214, 3341, 98
+    per = (n_atoms - 400) // n_res  # protein atoms per residue; the rest is solvent
+    resids = np.concatenate([np.repeat(np.arange(1, n_res + 1), per),
+                             np.arange(n_res + 1, n_res + 1 + n_atoms - per * n_res)])
+    resnames = np.concatenate([np.array(["MET", "ARG", "ILE", "HSD", "GLY"])[np.repeat(np.arange(n_res), per) % 5],
+                               ["TIP3"] * (n_atoms - per * n_res)])
+    base = ["N", "CA", "C", "O", "CB", "CG", "CD", "NE", "CZ", "NH1", "NH2", "HA", "HB1"]
+    names = np.concatenate([np.tile(base[:per], n_res), ["OH2"] * (n_atoms - per * n_res)])
+    masses = np.array([{"N": 14.007, "O": 15.999, "OH2": 15.999}.get(a, 12.011) for a in names])
+    x = SY.frames(31, n_atoms, 0, nf, motion_table(32, nf))
+    psf, dcd, out = str(tmp_path / "adk.psf"), str(tmp_path / "adk.dcd"), str(tmp_path / "rmsf.npy")
+    write_psf(psf, resids, resnames, names, masses)
+    write_dcd(dcd, x, box=(60.0, 90.0, 60.0, 90.0, 90.0, 60.0))
+    r = subprocess.run([sys.executable, f"{ROOT}/mdanalysis-mpi_amd/rmsf_mi355x.py", "--topology", psf,
+                        "--trajectory", dcd, "--out", out], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    top = PsfTopology(psf)
+    sel = top.select("protein and name CA")
+    assert len(sel) == n_res
+    exp = O.rmsf_script(x, sel, top.masses[sel], size=1, align="average")["rmsf"]
+    np.testing.assert_allclose(np.load(out), exp, rtol=0, atol=1e-6)
+    got = RMSF(dcd, select=sel, masses=top.masses[sel], align="frame0").run(start=3, stop=90, step=2)
+    exp = O.rmsf_script(x, sel, top.masses[sel], size=1, align="frame0", start=3, stop=90, step=2)["rmsf"]
+    np.testing.assert_allclose(got.results.rmsf, exp, rtol=0, atol=1e-6)
