@@ -1,0 +1,193 @@
+"""One process, several GPUs: ``RMSF(..., gpus=N).run()`` without a launcher.
+
+RMSF.py runs one MPI rank per frame block (RMSF.py:59-72) and merges with
+``Allreduce`` (RMSF.py:110) and a pickle ``comm.reduce`` (RMSF.py:143).  Here
+one Python process drives one context of the C ABI (``rmsf_ctx``, csrc/
+context.cpp) per device, each owning the RMSF.py:65-69 block of its index;
+the per-device work runs on one host thread per context (the ctypes calls
+release the GIL), and the two exchange steps run over RCCL communicators made
+by ``ncclCommInitAll`` (``rmsf_multi_init_all``) -- or, when a device appears
+twice in ``gpus`` (one GPU hosting several blocks), over the contexts'
+in-process fold, which performs the same arithmetic.
+
+Per context, RMSF.py's rank loop in context-ABI terms:
+
+    set_reference_frame(frame ref_frame)                 RMSF.py:80-87
+    push(block, ALIGN_SUM)                               RMSF.py:89-105
+    multi_allreduce_sum(all)                             RMSF.py:107-110
+    set_reference_average()                              RMSF.py:111-118
+    push(block, ALIGN_WELFORD)                           RMSF.py:120-138
+    multi_chan_merge(all)                                RMSF.py:140-143
+    get_rmsf                                             RMSF.py:145-146
+
+(``align=None``: one Welford push; ``"frame0"``: reference + aligned Welford.)
+"""
+from __future__ import annotations
+
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from . import parallel
+from .context import PUSH_ALIGN_SUM, PUSH_ALIGN_WELFORD, PUSH_WELFORD, Context
+from ._lib import RmsfEmptyError
+from .sources import FrameList
+
+
+def device_list(gpus) -> list[int]:
+    """``gpus``: a count (devices 0..N-1) or an explicit list of device ids."""
+    if isinstance(gpus, (int, np.integer)):
+        if gpus < 1:
+            raise ValueError("gpus must be >= 1")
+        return list(range(int(gpus)))
+    devs = [int(d) for d in gpus]
+    if not devs or min(devs) < 0:
+        raise ValueError("gpus: a non-empty list of device ids expected")
+    return devs
+
+
+class _HostFrames:
+    """A float32 [F, n_atoms, 3] host trajectory; the contexts gather the selection."""
+
+    def __init__(self, arr: np.ndarray, sel):
+        if arr.dtype != np.float32 or arr.ndim != 3 or arr.shape[2] != 3:
+            raise ValueError("host trajectory must be float32 [n_frames, n_atoms, 3]")
+        self.arr = np.ascontiguousarray(arr)
+        self.n_traj, self.n_atoms = self.arr.shape[0], self.arr.shape[1]
+        self.sel = None if sel is None else np.ascontiguousarray(sel, dtype=np.int64)
+        if self.sel is not None and self.sel.size and (self.sel.min() < 0 or self.sel.max() >= self.n_atoms):
+            raise IndexError("selection index out of range")
+
+    def reference(self, frame: int) -> np.ndarray:
+        return self.arr[frame]
+
+    def push(self, ctx: Context, rows: range, mode: int) -> None:
+        if len(rows):
+            # rows is an arithmetic range: a strided view, pushed with its step
+            ctx.push(self.arr[rows.start:rows[-1] + 1], mode, step=rows.step)
+
+
+class _XtcFrames:
+    """A GROMACS XTC file: each context decompresses its block on its GPU."""
+
+    def __init__(self, path: str, sel):
+        from .xtc import XTCFile
+
+        self.xtc = XTCFile(path)
+        self.n_traj, self.n_atoms = self.xtc.n_frames, self.xtc.n_atoms
+        self.sel = None if sel is None else np.ascontiguousarray(sel, dtype=np.int64)
+        if self.sel is not None and self.sel.size and (self.sel.min() < 0 or self.sel.max() >= self.n_atoms):
+            raise IndexError("selection index out of range")
+
+    def reference(self, frame: int) -> np.ndarray:
+        return self.xtc.read(frame, 1)[0]
+
+    def push(self, ctx: Context, rows: range, mode: int) -> None:
+        if len(rows):
+            ctx.push_xtc(self.xtc, rows.start, rows[-1] + 1, rows.step, mode)
+
+
+class _AtomGroupFrames:
+    """An MDAnalysis AtomGroup: ``ag.positions`` per Timestep (RMSF.py:95,128),
+    gathered on this thread (readers are not thread-safe) in batches."""
+
+    serial = True
+
+    def __init__(self, ag, batch_frames: int | None):
+        self.ag, self.traj = ag, ag.universe.trajectory
+        self.n_traj, self.n_atoms, self.sel = len(self.traj), len(ag), None
+        self.batch = batch_frames or max(1, min(1024, (32 << 20) // max(1, 12 * self.n_atoms)))
+
+    def reference(self, frame: int) -> np.ndarray:
+        cur = self.traj.ts.frame
+        try:
+            self.traj[frame]
+            return np.array(self.ag.positions, dtype=np.float32)
+        finally:
+            self.traj[cur]
+
+    def push(self, ctx: Context, rows: range, mode: int) -> None:
+        buf = np.empty((min(self.batch, max(1, len(rows))), self.n_atoms, 3), np.float32)
+        for i in range(0, len(rows), self.batch):
+            part = rows[i:i + self.batch]
+            for j, f in enumerate(part):
+                self.traj[f]
+                buf[j] = self.ag.positions
+            ctx.push(buf[:len(part)], mode)
+
+
+def _frames_of(inp, sel, batch_frames):
+    import os
+
+    if isinstance(inp, np.ndarray):
+        return _HostFrames(inp, sel)
+    if isinstance(inp, (str, bytes)) or hasattr(inp, "__fspath__"):
+        path = os.fspath(inp)
+        if str(path).lower().endswith(".xtc"):
+            return _XtcFrames(path, sel)
+        if str(path).lower().endswith(".dcd"):
+            from .dcd import DCDFile
+
+            with DCDFile(path) as f:
+                return _HostFrames(f.read(sel=sel), None)
+        raise ValueError(f"only .xtc and .dcd trajectory files are read natively, got {path!r}")
+    if hasattr(inp, "universe") and hasattr(inp, "positions"):
+        return _AtomGroupFrames(inp, batch_frames)
+    raise TypeError(f"gpus=: unsupported input {type(inp)!r} (numpy array, .xtc/.dcd path or AtomGroup; "
+                    "an HBM tensor lives on one device -- use torch.distributed, one process per GPU)")
+
+
+def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int = 0, start=None, stop=None,
+              step=None, batch_frames: int | None = None) -> dict:
+    """RMSF.py's computation over the devices ``gpus`` from one process.
+    Returns the ``results`` fields (rmsf, mean, sumsquares, n_frames, ...)."""
+    if align not in (None, "frame0", "average"):
+        raise ValueError(f"align must be one of (None, 'frame0', 'average'), got {align!r}")
+    if parallel.world()[1] > 1:
+        raise ValueError("gpus= drives several devices from one process; under torch.distributed "
+                         "(one process per GPU) leave it unset")
+    devs = device_list(gpus)
+    src = _frames_of(inp, select, batch_frames)
+    fl = FrameList(src.n_traj, start, stop, step)
+    if len(fl) == 0:
+        raise RmsfEmptyError(-4, "RMSF.run", "no frames selected")
+    if align is not None and not 0 <= ref_frame < src.n_traj:
+        raise IndexError(f"ref_frame {ref_frame} outside the trajectory ({src.n_traj} frames)")
+    if masses is None and align is not None and isinstance(src, _AtomGroupFrames):
+        masses = np.asarray(src.ag.masses, dtype=np.float64)
+    ctxs = [Context(src.n_atoms, sel=src.sel, masses=masses, device=d) for d in devs]
+    try:
+        if len(set(devs)) == len(devs) and len(devs) > 1:
+            Context.init_all(ctxs)  # ncclCommInitAll: one communicator per device
+        blocks = [range(fl.r[b0], fl.r[b1 - 1] + 1, fl.step) if b1 > b0 else range(0)
+                  for b0, b1 in parallel.blocks(len(fl), len(devs))]
+
+        def each(fn):
+            if getattr(src, "serial", False) or len(ctxs) == 1:
+                for c, r in zip(ctxs, blocks):
+                    fn(c, r)
+                return
+            with ThreadPoolExecutor(len(ctxs)) as ex:
+                for f in [ex.submit(fn, c, r) for c, r in zip(ctxs, blocks)]:
+                    f.result()
+
+        out = {}
+        if align is not None:
+            ref = src.reference(ref_frame)
+            for c in ctxs:  # every rank reads the reference frame (RMSF.py:80-87)
+                c.set_reference_frame(ref)
+        if align == "average":
+            each(lambda c, r: src.push(c, r, PUSH_ALIGN_SUM))
+            Context.multi_allreduce_sum(ctxs)
+            for c in ctxs:
+                c.set_reference_average()
+            out["average"] = ctxs[0].average().reshape(-1)  # flat, as the pipeline returns it
+        each(lambda c, r: src.push(c, r, PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD))
+        Context.multi_chan_merge(ctxs)
+        n, mean, m2 = ctxs[0].partial()
+        out.update(rmsf=ctxs[0].rmsf(), mean=mean, sumsquares=m2, n_frames=n,
+                   blocks=[(b0, b1) for b0, b1 in parallel.blocks(len(fl), len(devs))], devices=devs)
+        return out
+    finally:
+        for c in ctxs:
+            c.close()

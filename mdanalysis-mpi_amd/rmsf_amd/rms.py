@@ -58,11 +58,16 @@ class RMSF:
         masses are used.
     ref_frame : int
         Trajectory frame of the first reference (RMSF.py:63).
+    gpus : int | list of int, optional
+        Drive this many devices (or these device ids) from one process: each
+        takes the RMSF.py:65-69 block of its index and the blocks merge over
+        RCCL (``ncclCommInitAll``).  Inputs: host array, ``.xtc``/``.dcd``
+        path or AtomGroup.  Leave unset under ``torch.distributed``.
     """
 
     def __init__(self, atomgroup, *, select=None, align=None, masses=None, ref_frame: int = 0,
                  device=None, batch_frames: int | None = None, n_splits: int | None = None,
-                 collect_rmsd: bool = False, verbose: bool = False, **kwargs):
+                 collect_rmsd: bool = False, verbose: bool = False, gpus=None, **kwargs):
         self._input = atomgroup
         self.select = select
         self.align = align
@@ -73,6 +78,7 @@ class RMSF:
         self.n_splits = n_splits
         self.collect_rmsd = collect_rmsd
         self.verbose = verbose
+        self.gpus = gpus
         self.results = Results()
         self._source = None
 
@@ -80,6 +86,8 @@ class RMSF:
     def run(self, start=None, stop=None, step=None, frames=None, verbose=None, **kwargs):
         if frames is not None:
             raise NotImplementedError("explicit frame lists are not supported; use start/stop/step")
+        if self.gpus is not None:
+            return self._run_multi(start, stop, step)
         eng = Engine(self.device)
         src, masses = self._make_source(eng)
         fl = FrameList(src.n_traj, start, stop, step)
@@ -94,6 +102,7 @@ class RMSF:
         r.rmsf = res.rmsf.cpu().numpy()
         r.mean = res.mean.cpu().numpy()
         r.sumsquares = res.m2.cpu().numpy()
+        r.m2 = r.sumsquares
         r.n_frames = res.n_frames
         r.n_local = res.n_local
         r.block = res.block
@@ -102,6 +111,23 @@ class RMSF:
         if res.rmsd is not None:
             r.rmsd = res.rmsd.cpu().numpy()
         self.n_frames = res.n_frames
+        return self
+
+    def _run_multi(self, start, stop, step):
+        """``gpus=N`` (or a list of device ids): one process drives N devices
+        through the context ABI, RCCL communicators from ncclCommInitAll
+        (rmsf_amd.multi)."""
+        from .multi import run_multi
+
+        if self.collect_rmsd:
+            raise NotImplementedError("collect_rmsd is not available with gpus=; use torch.distributed ranks")
+        out = run_multi(self._input, self.gpus, select=self.select, align=self.align, masses=self.masses,
+                        ref_frame=self.ref_frame, start=start, stop=stop, step=step,
+                        batch_frames=self.batch_frames)
+        r = self.results
+        r.update(out)
+        r.m2 = r.sumsquares
+        self.n_frames = r.n_frames
         return self
 
     @property

@@ -109,3 +109,24 @@ def test_python_constants_match_header():
             "RMSF_MODE_SUM"} <= set(mirrored)
     for n in mirrored:
         assert getattr(_lib, n) == defines[n], n
+
+
+def test_multi_device_list_and_input_errors():
+    """rmsf_amd.multi host logic (no device touched): ``gpus=`` parsing and
+    the inputs a one-process multi-device run refuses before any context."""
+    import numpy as np
+    import torch
+    from rmsf_amd import multi
+    assert multi.device_list(3) == [0, 1, 2]
+    assert multi.device_list([2, 0, 0]) == [2, 0, 0]
+    for bad in (0, [], [-1]):
+        with pytest.raises(ValueError):
+            multi.device_list(bad)
+    with pytest.raises(TypeError):
+        multi._frames_of(torch.zeros(2, 3, 3), None, None)
+    with pytest.raises(ValueError):
+        multi._frames_of("traj.nc", None, None)
+    with pytest.raises(ValueError):
+        multi._frames_of(np.zeros((2, 3, 3), np.float64), None, None)
+    with pytest.raises(IndexError):
+        multi._frames_of(np.zeros((2, 3, 3), np.float32), [0, 3], None)
