@@ -1,4 +1,5 @@
-// Times the library's C2 Welford accumulate and C3 superposition sums from a
+// Times the library's C2 Welford accumulate, C3 superposition sums and the
+// aligned accumulators (Welford, sum) from a
 // plain C++ process (no torch), HIP events, 100k atoms x 20k frames -- to
 // compare with the same entry points driven from Python (tools/tune_stats.py,
 // bench.py).  Not product code.
@@ -53,22 +54,26 @@ int main() {
   hipEventCreate(&a);
   hipEventCreate(&b);
   for (int rep = 0; rep < 3; ++rep) {
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < 4; ++k) {
       float ms[5];
       for (int i = 0; i < 5; ++i) {
         hipEventRecord(a, nullptr);
         if (k == 0)
           OK(rmsf_superpose(x, 3 * n, nf, n, nullptr, nullptr, ref, info, xf, work, wb, nullptr));
-        else
+        else if (k == 1)
           OK(rmsf_accumulate_balanced(x, 3 * n, nf, n, nullptr, nullptr, nullptr, RMSF_MODE_WELFORD, 0, acc, ab,
                                       nullptr));
+        else  // aligned (C3 / RMSF.py sweep 2, sweep 1): transform records from the superposition above
+          OK(rmsf_accumulate_balanced(x, 3 * n, nf, n, nullptr, xf, info, k == 2 ? RMSF_MODE_WELFORD : RMSF_MODE_SUM,
+                                      0, acc, ab, nullptr));
         hipEventRecord(b, nullptr);
         hipEventSynchronize(b);
         hipEventElapsedTime(&ms[i], a, b);
       }
       std::sort(ms, ms + 5);
-      printf("%-28s median %.3f ms  min %.3f ms\n", k == 0 ? "rmsf_superpose" : "rmsf_accumulate_balanced", ms[2],
-             ms[0]);
+      static const char *name[4] = {"rmsf_superpose", "accumulate_balanced", "accumulate_balanced align",
+                                     "accumulate_balanced align sum"};
+      printf("%-30s median %.3f ms  min %.3f ms\n", name[k], ms[2], ms[0]);
       fflush(stdout);
     }
   }
