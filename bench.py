@@ -195,6 +195,15 @@ def main():
     from rmsf_amd.synth import generate, motion_table
 
     eng = Engine(torch.device("cuda", local))
+    if world > 1:
+        # RCCL sets its connections up at the first collective: do that once,
+        # untimed, at the merge's message size, so it is not charged to a step
+        # even when --warmup 0
+        _t = torch.zeros(3 * n_atoms, dtype=torch.float64, device=eng.device)
+        dist.all_reduce(_t)
+        dist.barrier()
+        torch.cuda.synchronize()
+        del _t
     n_total = per_gpu * world
     b0, b1 = parallel.blocks(n_total, world)[rank]
     n_local = b1 - b0

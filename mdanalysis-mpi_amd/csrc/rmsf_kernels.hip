@@ -29,6 +29,9 @@
 #include "rmsf_hip.h"
 
 #define RMSF_EXPORT __attribute__((visibility("default")))
+#ifndef RMSF_SHIFTED_SUMS
+#define RMSF_SHIFTED_SUMS 1  // per-frame statistics as shifted sums (0: Welford updates, for A/B)
+#endif
 
 namespace {
 
@@ -88,11 +91,19 @@ __constant__ WCoefTable g_coef = make_coef_table();
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ void welford(double &m, double &q, double x, const WCoef c) {
+[[maybe_unused]] __device__ __forceinline__ void welford(double &m, double &q, double x, const WCoef c) {
   // M2 += k/(k+1) (x-mean)^2 ; mean = (k mean + x)/(k+1) == mean + (x-mean)/(k+1)
   const double d = x - m;
   q = fma(c.a * d, d, q);
   m = fma(c.b, d, m);
+}
+
+// (S1, S2) of n values shifted by sh -> (mean, M2); inv = 1/n.  M2 is
+// clamped at 0 (S2 - S1^2/n can round below it only when M2 ~ 0).
+[[maybe_unused]] __device__ __forceinline__ void shifted_to_moments(double &s1, double &s2, double sh, double inv) {
+  const double d = s1 * inv;
+  s2 = fmax(0.0, fma(-s1, d, s2));
+  s1 = sh + d;
 }
 
 __device__ __forceinline__ int64_t split_begin(int64_t n_frames, int n_splits, int s) {
@@ -108,6 +119,43 @@ __device__ __forceinline__ int64_t split_begin(int64_t n_frames, int n_splits, i
 template <int U>
 __device__ __forceinline__ void wel_flat_run(const f32x4 *__restrict__ p, int64_t stride4, int nf, double (&m)[4],
                                              double (&q)[4]) {
+#if RMSF_SHIFTED_SUMS
+  // Shifted sums: S1 = sum d, S2 = sum d^2 with d = x - x_first (the
+  // segment's first frame), converted to (mean, M2) at the end -- 3 VALU ops
+  // per coordinate against Welford's 4, and no per-frame coefficients.  Same
+  // statistics as RMSF.py:137-138's Welford to f64 rounding (the shift keeps
+  // S1 small, so M2 = S2 - S1^2/n does not cancel).
+  double sh[4];
+  if (nf <= 0) {  // an empty split: nothing to read
+#pragma unroll
+    for (int c = 0; c < 4; ++c) m[c] = q[c] = 0.0;
+    return;
+  }
+  {
+    const f32x4 v0 = p[0];
+    sh[0] = (double)v0.x, sh[1] = (double)v0.y, sh[2] = (double)v0.z, sh[3] = (double)v0.w;
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) m[c] = q[c] = 0.0;
+  auto acc = [&](const f32x4 v) {
+    const double d0 = (double)v.x - sh[0], d1 = (double)v.y - sh[1];
+    const double d2 = (double)v.z - sh[2], d3 = (double)v.w - sh[3];
+    m[0] += d0, m[1] += d1, m[2] += d2, m[3] += d3;
+    q[0] = fma(d0, d0, q[0]), q[1] = fma(d1, d1, q[1]), q[2] = fma(d2, d2, q[2]), q[3] = fma(d3, d3, q[3]);
+  };
+  int k = 0;
+  for (; k + U <= nf; k += U) {
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + (int64_t)(k + u) * stride4);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc(v[u]);
+  }
+  for (; k < nf; ++k) acc(__builtin_nontemporal_load(p + (int64_t)k * stride4));
+  const double inv = g_coef.v[nf - 1].b;  // 1/nf
+#pragma unroll
+  for (int c = 0; c < 4; ++c) shifted_to_moments(m[c], q[c], sh[c], inv);
+#else
 #pragma unroll
   for (int c = 0; c < 4; ++c) m[c] = q[c] = 0.0;
   int k = 0;
@@ -132,6 +180,7 @@ __device__ __forceinline__ void wel_flat_run(const f32x4 *__restrict__ p, int64_
     welford(m[2], q[2], (double)v.z, c);
     welford(m[3], q[3], (double)v.w, c);
   }
+#endif
 }
 
 __device__ __forceinline__ void store4(double *__restrict__ om, double *__restrict__ oq, const double (&m)[4],
@@ -186,13 +235,29 @@ __device__ __forceinline__ void accum_atoms_run(const float *__restrict__ p, int
                                                 double (&m)[3], double (&q)[3]) {
 #pragma unroll
   for (int c = 0; c < 3; ++c) m[c] = q[c] = 0.0;
+#if RMSF_SHIFTED_SUMS
+  // WELFORD as shifted sums (see wel_flat_run): the shift is the segment's
+  // first frame after the transform
+  double sh[3] = {0.0, 0.0, 0.0};
+  if (MODE == RMSF_MODE_WELFORD && nf > 0) {
+    float x = p[0], y = p[1], z = p[2];
+    if (ALIGN) apply_xform(x, y, z, xf, rc0, rc1, rc2);
+    sh[0] = (double)x, sh[1] = (double)y, sh[2] = (double)z;
+  }
+#endif
   auto consume = [&](float x, float y, float z, int k) {
     if (ALIGN) apply_xform(x, y, z, xf + (int64_t)k * kXform, rc0, rc1, rc2);
     if (MODE == RMSF_MODE_WELFORD) {
+#if RMSF_SHIFTED_SUMS
+      const double d0 = (double)x - sh[0], d1 = (double)y - sh[1], d2 = (double)z - sh[2];
+      m[0] += d0, m[1] += d1, m[2] += d2;
+      q[0] = fma(d0, d0, q[0]), q[1] = fma(d1, d1, q[1]), q[2] = fma(d2, d2, q[2]);
+#else
       const WCoef c = g_coef.v[k];
       welford(m[0], q[0], (double)x, c);
       welford(m[1], q[1], (double)y, c);
       welford(m[2], q[2], (double)z, c);
+#endif
     } else {
       m[0] += (double)x;
       m[1] += (double)y;
@@ -216,6 +281,13 @@ __device__ __forceinline__ void accum_atoms_run(const float *__restrict__ p, int
     const float *r = p + (int64_t)k * fstride;
     consume(r[0], r[1], r[2], k);
   }
+#if RMSF_SHIFTED_SUMS
+  if (MODE == RMSF_MODE_WELFORD && nf > 0) {
+    const double inv = g_coef.v[nf - 1].b;  // 1/nf
+#pragma unroll
+    for (int c = 0; c < 3; ++c) shifted_to_moments(m[c], q[c], sh[c], inv);
+  }
+#endif
 }
 
 template <int MODE>
