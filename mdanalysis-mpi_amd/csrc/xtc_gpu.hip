@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -623,17 +624,19 @@ const char *status_text(int32_t s) {
   }
 }
 
-constexpr size_t kReadPiece = 128u << 20;  // bytes read (and then copied) at a time
+constexpr size_t kReadSub = 4u << 20;     // bytes per pread task (read contiguous batches)
+constexpr size_t kCopyMin = 64u << 20;    // host->device copies of at least this many bytes
 
-// Persistent worker threads for the file reads (a batch is read in several
-// pieces; spawning threads per piece cost ~0.2 ms each).  run(n, fn) calls
-// fn(0..n-1) on the workers and returns when all are done.
+// Persistent worker threads for the file reads (spawning threads per read
+// cost ~0.2 ms each).  launch(n, fn) hands fn(0..n-1) to the workers (in
+// increasing k) and returns; wait() returns when all are done; run() = both.
 class ReadPool {
  public:
   explicit ReadPool(int n) {
     for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
   }
   ~ReadPool() {
+    wait();
     {
       std::lock_guard<std::mutex> g(m_);
       stop_ = true;
@@ -641,16 +644,23 @@ class ReadPool {
     cv_.notify_all();
     for (auto &t : th_) t.join();
   }
-  void run(int64_t n, const std::function<void(int64_t)> &fn) {
+  void launch(int64_t n, std::function<void(int64_t)> fn) {
     std::unique_lock<std::mutex> g(m_);
-    fn_ = &fn;
+    done_.wait(g, [this] { return left_ == 0; });
+    fn_ = std::move(fn);
     next_ = 0;
     total_ = n;
     left_ = n;
     ++gen_;
     cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> g(m_);
     done_.wait(g, [this] { return left_ == 0; });
-    fn_ = nullptr;
+  }
+  void run(int64_t n, std::function<void(int64_t)> fn) {
+    launch(n, std::move(fn));
+    wait();
   }
 
  private:
@@ -662,7 +672,7 @@ class ReadPool {
       if (stop_) return;
       while (next_ < total_) {
         const int64_t i = next_++;
-        const std::function<void(int64_t)> *fn = fn_;
+        const std::function<void(int64_t)> *fn = &fn_;  // not replaced before left_ reaches 0
         g.unlock();
         (*fn)(i);
         g.lock();
@@ -674,23 +684,18 @@ class ReadPool {
   std::vector<std::thread> th_;
   std::mutex m_;
   std::condition_variable cv_, done_;
-  const std::function<void(int64_t)> *fn_ = nullptr;
+  std::function<void(int64_t)> fn_;
   int64_t next_ = 0, total_ = 0, left_ = 0;
   uint64_t gen_ = 0;
   bool stop_ = false;
 };
 
-// Parallel pread of [off, off+n) into dst: pieces of >= 1 MiB over the pool.
-bool pread_par(ReadPool &pool, int n_threads, int fd, unsigned char *dst, size_t n, int64_t off) {
-  const size_t chunk = std::max<size_t>(1 << 20, (n + n_threads - 1) / std::max(1, n_threads));
-  const int64_t pieces = (int64_t)((n + chunk - 1) / chunk);
-  std::vector<char> ok(pieces, 1);
-  pool.run(pieces, [&](int64_t k) {
-    const size_t s = (size_t)k * chunk, len = std::min(chunk, n - s);
-    ok[k] = rmsf_internal_pread_all(fd, dst + s, len, off + (int64_t)s);
-  });
-  return std::all_of(ok.begin(), ok.end(), [](char c) { return c != 0; });
-}
+// Waits for a launched pool on every exit path of the scope (its tasks
+// reference the caller's locals).
+struct PoolWait {
+  ReadPool &p;
+  ~PoolWait() { p.wait(); }
+};
 
 }  // namespace
 
@@ -851,14 +856,36 @@ int xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_t step, float *ou
     const int64_t a = x->offset[f0], e = x->offset[f0 + n - 1] + x->size[f0 + n - 1];
     total = (size_t)(e - a);
     if (total > s.raw_cap) return fail(RMSF_EINVAL, "rmsf_xtcdec_decode: batch larger than the slot");
-    // read in pieces, each copied as soon as it is in the pinned slot: the
-    // host->device DMA of piece k overlaps the file read of piece k+1
-    for (size_t done = 0; done < total;) {
-      const size_t len = std::min(kReadPiece, total - done);
-      if (!pread_par(*d->pool, d->n_threads, x->fd, s.h_raw + done, len, a + (int64_t)done))
-        return fail(RMSF_EINVAL, "xtc: read failed");
-      XD_HIP(hipMemcpyAsync(s.d_raw + done, s.h_raw + done, len, hipMemcpyHostToDevice, s.s));
-      done += len;
+    // read in 4 MiB tasks over the pool with no barrier between them; this
+    // thread copies every completed prefix of >= 64 MiB to the device as it
+    // forms, so the DMA overlaps the rest of the read
+    const int64_t pieces = (int64_t)((total + kReadSub - 1) / kReadSub);
+    std::unique_ptr<std::atomic<char>[]> st(new std::atomic<char>[pieces]);  // 0 pending, 1 read, 2 failed
+    for (int64_t k = 0; k < pieces; ++k) st[k].store(0);
+    std::mutex mu;
+    std::condition_variable cv;
+    unsigned char *h = s.h_raw;
+    const int fd = x->fd;
+    d->pool->launch(pieces, [&, h, fd, a, total](int64_t k) {
+      const size_t o = (size_t)k * kReadSub, len = std::min(kReadSub, total - o);
+      st[k].store(rmsf_internal_pread_all(fd, h + o, len, a + (int64_t)o) ? 1 : 2);
+      { std::lock_guard<std::mutex> g(mu); }
+      cv.notify_one();
+    });
+    PoolWait pw{*d->pool};
+    size_t sent = 0;
+    for (int64_t next = 0; next < pieces;) {
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return st[next].load() != 0; });
+      }
+      for (; next < pieces && st[next].load() != 0; ++next)
+        if (st[next].load() == 2) return fail(RMSF_EINVAL, "xtc: read failed");
+      const size_t ready = std::min(total, (size_t)next * kReadSub);
+      if (ready - sent >= kCopyMin || ready == total) {
+        XD_HIP(hipMemcpyAsync(s.d_raw + sent, s.h_raw + sent, ready - sent, hipMemcpyHostToDevice, s.s));
+        sent = ready;
+      }
     }
     copied = true;
     for (int64_t k = 0; k < n; ++k) {
