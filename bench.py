@@ -78,6 +78,8 @@ def parse():
     ap.add_argument("--xtc-cache", action="store_true",
                     help="c5xtc (GPU decode): keep decoded frames in HBM within a step (RMSF.py's second sweep "
                          "reads them from HBM); dropped before every step, so each step decodes once")
+    ap.add_argument("--host-cache", action="store_true",
+                    help="c5: keep the staged frames in HBM within a step (RMSF.py's second sweep reads them there)")
     ap.add_argument("--align", choices=["none", "frame0", "average"], default=None, help="override the workload's")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo only "
                                                      "to rehearse several ranks on one GPU)")
@@ -238,7 +240,7 @@ def main():
                             n_slots=3, cache=a.xtc_cache)
         else:
             src = HostSource(host, None, batch_frames=a.stager_batch, n_threads=a.stager_threads, offset=b0,
-                             n_traj=n_total)
+                             n_traj=n_total, cache=a.host_cache)
     else:
         src = DeviceSource(traj, offset=b0, n_traj=n_total)
     fl = FrameList(n_total)
@@ -312,6 +314,7 @@ def main():
     # -- aligned modes at N=1 (reported beside the headline) ------------------
     if wl.get("host"):
         out["stager"] = {"h2d_gbs": B_PER_ATOM_FRAME * n_atoms * n_local * a.steps / dt / 1e9,
+                         "host_cache": bool(getattr(src, "cache", None) is not None),
                          "threads": a.stager_threads, "batch_frames": src.batch_frames,
                          "host_link_spec_gbs": 63.0}
         if wl.get("xtc"):

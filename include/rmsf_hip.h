@@ -65,6 +65,11 @@ int rmsf_malloc(void **d_ptr, size_t bytes);
 int rmsf_free(void *d_ptr);
 int rmsf_memcpy_h2d(void *d_dst, const void *h_src, size_t bytes, void *stream);
 int rmsf_memcpy_d2h(void *h_dst, const void *d_src, size_t bytes, void *stream);
+/* Strided device->device copy of `height` rows of `width` bytes (pitches in
+ * bytes), asynchronous on `stream`: fills the HBM frame cache that lets the
+ * second sweep (RMSF.py:124) read the frames the first (RMSF.py:92) staged. */
+int rmsf_memcpy2d_d2d(void *d_dst, size_t dpitch, const void *d_src, size_t spitch,
+                      size_t width, size_t height, void *stream);
 int rmsf_stream_synchronize(void *stream);
 
 /* ---- frame-block decomposition: RMSF.py:63-72 ----------------------------

@@ -1225,6 +1225,14 @@ RMSF_EXPORT int rmsf_memcpy_d2h(void *h, const void *d, size_t bytes, void *stre
   return RMSF_OK;
 }
 
+RMSF_EXPORT int rmsf_memcpy2d_d2d(void *d_dst, size_t dpitch, const void *d_src, size_t spitch, size_t width,
+                                 size_t height, void *stream) {
+  if (!d_dst || !d_src || width > dpitch || width > spitch) return fail(RMSF_EINVAL, "rmsf_memcpy2d_d2d: bad arguments");
+  if (width == 0 || height == 0) return RMSF_OK;
+  HIP_TRY(hipMemcpy2DAsync(d_dst, dpitch, d_src, spitch, width, height, hipMemcpyDeviceToDevice, S(stream)));
+  return RMSF_OK;
+}
+
 RMSF_EXPORT int rmsf_stream_synchronize(void *stream) {
   HIP_TRY(hipStreamSynchronize(S(stream)));
   return RMSF_OK;

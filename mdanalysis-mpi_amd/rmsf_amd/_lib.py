@@ -50,6 +50,7 @@ SIGNATURES = {
     "rmsf_free": (c_int, [P]),
     "rmsf_memcpy_h2d": (c_int, [P, P, c_size_t, P]),
     "rmsf_memcpy_d2h": (c_int, [P, P, c_size_t, P]),
+    "rmsf_memcpy2d_d2d": (c_int, [P, c_size_t, P, c_size_t, c_size_t, c_size_t, P]),
     "rmsf_stream_synchronize": (c_int, [P]),
     "rmsf_block_range": (c_int, [c_int64, c_int, c_int, POINTER(c_int64), POINTER(c_int64)]),
     "rmsf_reference_setup": (c_int, [P, P, c_int64, P, P, P, P, P]),

@@ -143,8 +143,11 @@ class RMSF:
                 x = x.detach().cpu().numpy()
             else:
                 return DeviceSource(x, self.select), self.masses
+        # RMSF.py's two sweeps (align="average") read every frame twice
+        # (RMSF.py:92,124): host sources then keep the staged frames in HBM
+        two = self.align == "average"
         if isinstance(x, np.ndarray):
-            return HostSource(x, self.select, batch_frames=self.batch_frames), self.masses
+            return HostSource(x, self.select, batch_frames=self.batch_frames, cache=two), self.masses
         if isinstance(x, (str, bytes)) or hasattr(x, "__fspath__"):
             import os
             path = os.fspath(x)
@@ -155,7 +158,7 @@ class RMSF:
 
                 with DCDFile(path) as f:
                     frames = f.read(sel=self.select)
-                return HostSource(frames, None, batch_frames=self.batch_frames), self.masses
+                return HostSource(frames, None, batch_frames=self.batch_frames, cache=two), self.masses
             if not str(path).lower().endswith(".xtc"):
                 raise ValueError(f"only .xtc and .dcd trajectory files are read natively, got {path!r}")
             # aligned runs read the reference frame first (and RMSF.py's two sweeps read
@@ -166,5 +169,5 @@ class RMSF:
             masses = self.masses
             if masses is None and self.align is not None:
                 masses = np.asarray(x.masses, dtype=np.float64)
-            return AtomGroupSource(x, batch_frames=self.batch_frames), masses
+            return AtomGroupSource(x, batch_frames=self.batch_frames, cache=two), masses
         raise TypeError(f"unsupported input {type(x)!r}: AtomGroup, numpy array or HIP torch tensor expected")

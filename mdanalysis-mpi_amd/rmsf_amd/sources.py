@@ -145,13 +145,70 @@ class DeviceSource:
             yield Batch(self._ptr(frames.r[i]), self.fstride * frames.step, n, self.sel_dev)
 
 
+class FrameCache:
+    """Staged (selected) frames kept resident in HBM: RMSF.py reads every frame
+    in both of its loops (RMSF.py:92,124), so the second sweep over a host
+    source can read HBM instead of crossing PCIe (or MDAnalysis' reader)
+    again.  Row r of the cache holds the source's row r, [n_sel, 3] float32;
+    a batch whose rows are all present is served from the cache, otherwise
+    it is staged and its rows are copied in (one strided device copy on the
+    consumer stream, before the kernels that read them)."""
+
+    def __init__(self, n_rows: int, n_sel: int, device=None):
+        self.n_sel = n_sel
+        self.buf = torch.empty((n_rows, n_sel, 3), dtype=torch.float32,
+                               device=torch.cuda.current_device() if device is None else device)
+        self.have = np.zeros(n_rows, dtype=bool)
+
+    @staticmethod
+    def fits(n_rows: int, n_sel: int) -> bool:
+        """Cache only what takes at most half of the free device memory."""
+        free, _ = torch.cuda.mem_get_info()
+        return 12 * n_rows * n_sel <= free // 2
+
+    def ptr(self, row: int) -> int:
+        return self.buf.data_ptr() + 12 * self.n_sel * row
+
+    def lookup(self, row: int, step: int, n: int) -> Batch | None:
+        if self.have[row:row + step * (n - 1) + 1:step].all():
+            return Batch(self.ptr(row), 3 * self.n_sel * step, n, None)
+        return None
+
+    def fill(self, row: int, step: int, n: int, src_ptr: int, stream: int) -> Batch:
+        w = 12 * self.n_sel
+        call("rmsf_memcpy2d_d2d", self.ptr(row), w * step, src_ptr, w, w, n, stream)
+        self.have[row:row + step * (n - 1) + 1:step] = True
+        return Batch(self.ptr(row), 3 * self.n_sel * step, n, None)
+
+    def drop(self) -> None:
+        self.have[:] = False
+
+
+def _cached_stage(cache: FrameCache | None, row: int, step: int, n: int, stream: int, stage) -> Batch:
+    """Rows [row, row+step, ...] of a host source: from ``cache`` when all are
+    present; otherwise ``stage()`` -> Batch in a stager slot, whose rows are
+    then copied into the cache (when there is one) and read from there."""
+    if cache is not None:
+        b = cache.lookup(row, step, n)
+        if b is not None:
+            return b
+    b = stage()
+    if cache is None:
+        return b
+    c = cache.fill(row, step, n, b.ptr, stream)
+    c.release = b.release
+    return c
+
+
 class HostSource:
     """Host float32 array [F, n_atoms, 3] streamed through the pinned stager.
     Row r holds global frame ``offset + r`` of a trajectory of ``n_traj``
-    frames (a rank's shard; default: the whole trajectory)."""
+    frames (a rank's shard; default: the whole trajectory).  ``cache=True``
+    keeps the staged frames resident in HBM for later sweeps (FrameCache;
+    ignored when they would take more than half of the free device memory)."""
 
     def __init__(self, traj: np.ndarray, sel=None, batch_frames: int | None = None, n_slots: int = 3,
-                 n_threads: int = 4, offset: int = 0, n_traj: int | None = None):
+                 n_threads: int = 4, offset: int = 0, n_traj: int | None = None, cache: bool = False):
         traj = np.ascontiguousarray(traj, dtype=np.float32)
         if traj.ndim != 3 or traj.shape[2] != 3:
             raise ValueError("trajectory must be [n_frames, n_atoms, 3]")
@@ -167,25 +224,36 @@ class HostSource:
             batch_frames = max(1, min(4096, (64 << 20) // max(1, 12 * self.n_sel)))
         self.batch_frames = batch_frames
         self.stager = Stager(self.n_atoms, self.n_sel, sel_arr, batch_frames, n_slots, n_threads)
+        rows = traj.shape[0]
+        self.cache = FrameCache(rows, self.n_sel) if cache and FrameCache.fits(rows, self.n_sel) else None
 
     def holds(self, frame: int) -> bool:
         return self.offset <= frame < self.offset + self.traj.shape[0]
+
+    def drop_cache(self) -> None:
+        """Forget the HBM-resident frames (the next sweep streams them again)."""
+        if self.cache is not None:
+            self.cache.drop()
 
     def _row(self, frame: int) -> int:
         if not self.holds(frame):
             raise IndexError(f"frame {frame} is not in this host shard")
         return frame - self.offset
 
+    def _stage(self, row: int, step: int, n: int, stream: int) -> Batch:
+        def stage():
+            slot, ptr = self.stager.stage(self.traj, row, step, n, stream)
+            return Batch(ptr, 3 * self.n_sel, n, None, lambda: self.stager.release(slot, stream))
+
+        return _cached_stage(self.cache, row, step, n, stream, stage)
+
     def reference(self, frame: int, stream: int) -> Batch:
-        slot, ptr = self.stager.stage(self.traj, self._row(frame), 1, 1, stream)
-        return Batch(ptr, 3 * self.n_sel, 1, None, lambda: self.stager.release(slot, stream))
+        return self._stage(self._row(frame), 1, 1, stream)
 
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
         bf = min(max_frames, self.batch_frames)
         for i in range(b0, b1, bf):
-            n = min(bf, b1 - i)
-            slot, ptr = self.stager.stage(self.traj, self._row(frames.r[i]), frames.step, n, stream)
-            yield Batch(ptr, 3 * self.n_sel, n, None, lambda s=slot: self.stager.release(s, stream))
+            yield self._stage(self._row(frames.r[i]), frames.step, min(bf, b1 - i), stream)
 
 
 class XtcDecoder:
@@ -345,7 +413,7 @@ class AtomGroupSource:
     """MDAnalysis AtomGroup: per-Timestep ``ag.positions`` (the selection rows,
     RMSF.py:95,128) packed into a host batch and staged to the device."""
 
-    def __init__(self, atomgroup, batch_frames: int | None = None, n_slots: int = 3):
+    def __init__(self, atomgroup, batch_frames: int | None = None, n_slots: int = 3, cache: bool = False):
         self.ag = atomgroup
         self.traj = atomgroup.universe.trajectory
         self.n_traj = len(self.traj)
@@ -356,9 +424,17 @@ class AtomGroupSource:
         self.stager = Stager(self.n_sel, self.n_sel, None, batch_frames, n_slots, 1)
         self._bufs = [np.empty((batch_frames, self.n_sel, 3), np.float32) for _ in range(n_slots)]
         self._next = 0
+        # RMSF.py's second loop (RMSF.py:124) re-reads every Timestep: with a
+        # cache the reader runs once per frame
+        ok = cache and FrameCache.fits(self.n_traj, self.n_sel)
+        self.cache = FrameCache(self.n_traj, self.n_sel) if ok else None
 
     def holds(self, frame: int) -> bool:
         return 0 <= frame < self.n_traj
+
+    def drop_cache(self) -> None:
+        if self.cache is not None:
+            self.cache.drop()
 
     def _buf(self) -> np.ndarray:
         b = self._bufs[self._next]
@@ -366,27 +442,34 @@ class AtomGroupSource:
         return b
 
     def reference(self, frame: int, stream: int) -> Batch:
-        cur = self.traj.ts.frame
-        try:
-            self.traj[frame]
-            buf = self._buf()
-            buf[0] = self.ag.positions
-        finally:
-            self.traj[cur]
-        slot, ptr = self.stager.stage_compact(buf, 1, stream)
-        return Batch(ptr, 3 * self.n_sel, 1, None, lambda: self.stager.release(slot, stream))
+        def stage():
+            cur = self.traj.ts.frame
+            try:
+                self.traj[frame]
+                buf = self._buf()
+                buf[0] = self.ag.positions
+            finally:
+                self.traj[cur]
+            slot, ptr = self.stager.stage_compact(buf, 1, stream)
+            return Batch(ptr, 3 * self.n_sel, 1, None, lambda: self.stager.release(slot, stream))
+
+        return _cached_stage(self.cache, frame, 1, 1, stream, stage)
 
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
         bf = min(max_frames, self.batch_frames)
         for i in range(b0, b1, bf):
             n = min(bf, b1 - i)
-            buf = self._buf()
-            for j in range(n):
-                self.traj[frames.r[i + j]]
-                buf[j] = self.ag.positions
-            slot, ptr = self.stager.stage_compact(buf, n, stream)
-            yield Batch(ptr, 3 * self.n_sel, n, None, lambda s=slot: self.stager.release(s, stream))
+
+            def stage(i=i, n=n):
+                buf = self._buf()
+                for j in range(n):
+                    self.traj[frames.r[i + j]]
+                    buf[j] = self.ag.positions
+                slot, ptr = self.stager.stage_compact(buf, n, stream)
+                return Batch(ptr, 3 * self.n_sel, n, None, lambda: self.stager.release(slot, stream))
+
+            yield _cached_stage(self.cache, frames.r[i], frames.step, n, stream, stage)
 
 
-__all__ = ["Batch", "Stager", "FrameList", "DeviceSource", "HostSource", "XtcDecoder", "XtcSource", "AtomGroupSource",
+__all__ = ["Batch", "Stager", "FrameCache", "FrameList", "DeviceSource", "HostSource", "XtcDecoder", "XtcSource", "AtomGroupSource",
            "_lib"]

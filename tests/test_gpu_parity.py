@@ -172,3 +172,22 @@ def test_captured_pipeline_replay(c1):
     torch.cuda.synchronize()
     exp = O.rmsf_script(traj[::-1].copy(), d["sel"], None, size=1, align="average")["rmsf"]
     np.testing.assert_allclose(r.rmsf.cpu().numpy(), exp, atol=TOL)
+
+
+@pytest.mark.parametrize("kw", [{}, dict(start=3, stop=90, step=2)])
+def test_host_frame_cache(c1, kw):
+    """RMSF.py's second loop (RMSF.py:124) reads the frames the first staged:
+    with the HBM frame cache the two sweeps of a host array cross PCIe once,
+    bit-identical to streaming them twice."""
+    from rmsf_amd import RMSF
+    from rmsf_amd.sources import HostSource
+    d, traj = c1
+    plain = RMSF(HostSource(traj, d["sel"], batch_frames=7), align="average").run(**kw).results
+    src = HostSource(traj, d["sel"], batch_frames=7, cache=True)
+    got = RMSF(src, align="average").run(**kw).results
+    assert src.cache is not None
+    used = np.arange(98)[slice(kw.get("start"), kw.get("stop"), kw.get("step"))]
+    assert src.cache.have[used].all()
+    np.testing.assert_array_equal(got.rmsf, plain.rmsf)
+    np.testing.assert_array_equal(got.average, plain.average)
+    np.testing.assert_allclose(got.rmsf, d["rmsf_average_P1" if not kw else "rmsf_average_slice"], rtol=0, atol=TOL)
