@@ -65,7 +65,7 @@ constexpr int kXform = RMSF_XFORM_DOUBLES;
 constexpr int kStats = 16;       // doubles per (frame, chunk) partial
 constexpr int64_t kAccumBlocks = 3584;       // target workgroups, k_welford_flat
 constexpr int64_t kAccumBlocksAtom = 4608;   // target workgroups, k_accum_atoms
-constexpr int64_t kStatsBlocks = 16384;  // aim for >= this many (frame-group, chunk) blocks
+constexpr int64_t kStatsBlocks = 4096;  // aim for >= this many (frame-group, chunk) blocks (2048-4096 measured best at C3, 16384 ~3 % slower)
 
 // ---------------------------------------------------------------------------
 // Welford coefficients a_k = k/(k+1), b_k = 1/(k+1) (RMSF.py:137-138), folded
