@@ -205,7 +205,9 @@ class HostSource:
     Row r holds global frame ``offset + r`` of a trajectory of ``n_traj``
     frames (a rank's shard; default: the whole trajectory).  ``cache=True``
     keeps the staged frames resident in HBM for later sweeps (FrameCache;
-    ignored when they would take more than half of the free device memory)."""
+    ignored when they would take more than half of the free device memory).
+    A cached row is not re-read: call ``drop_cache()`` after changing the
+    host array in place (``RMSF.run`` builds a fresh source per run)."""
 
     def __init__(self, traj: np.ndarray, sel=None, batch_frames: int | None = None, n_slots: int = 3,
                  n_threads: int = 4, offset: int = 0, n_traj: int | None = None, cache: bool = False):
