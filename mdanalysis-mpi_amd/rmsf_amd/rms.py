@@ -25,7 +25,7 @@ import torch
 from . import parallel
 from .engine import Engine
 from .pipeline import run_pipeline
-from .sources import AtomGroupSource, DeviceSource, FrameList, HostSource, XtcSource
+from .sources import AtomGroupSource, DcdSource, DeviceSource, FrameList, HostSource, XtcSource
 
 
 class Results(dict):
@@ -152,13 +152,9 @@ class RMSF:
             import os
             path = os.fspath(x)
             if str(path).lower().endswith(".dcd"):
-                # DCD frames are raw float32 planes: read the selected rows on the host,
-                # stream them through the pinned stager
-                from .dcd import DCDFile
-
-                with DCDFile(path) as f:
-                    frames = f.read(sel=self.select)
-                return HostSource(frames, None, batch_frames=self.batch_frames, cache=two), self.masses
+                # DCD frames are raw float32 planes: each batch's selected rows are
+                # read from the memory-mapped file and streamed through the stager
+                return DcdSource(path, self.select, batch_frames=self.batch_frames, cache=two), self.masses
             if not str(path).lower().endswith(".xtc"):
                 raise ValueError(f"only .xtc and .dcd trajectory files are read natively, got {path!r}")
             # aligned runs read the reference frame first (and RMSF.py's two sweeps read

@@ -9,8 +9,15 @@ the frame list:
     tensor [F, n_atoms, 3]); zero-copy, the selection is gathered in-kernel.
   * ``HostSource``    a host numpy float32 array, streamed through the pinned
     double-buffered ``Stager`` (C++ in csrc/stager.cpp).
+  * ``XtcSource``     an XTC file: compressed records decompressed on the GPU
+    (or on host threads into the stager).
+  * ``DcdSource``     a DCD file: each batch's selected rows read from the
+    memory-mapped file and staged.
   * ``AtomGroupSource`` an MDAnalysis AtomGroup (when MDAnalysis is present):
     ``ag.positions`` per Timestep, batched through the same stager.
+
+Host sources can keep what they staged resident in HBM (``FrameCache``) so
+that RMSF.py's second sweep does not cross PCIe again.
 """
 from __future__ import annotations
 
@@ -411,6 +418,56 @@ class XtcSource:
         self._check()
 
 
+class DcdSource:
+    """CHARMM/NAMD/X-PLOR DCD file (BASELINE C1's adk trajectory format),
+    streamed: each batch's selected rows are read from the memory-mapped file
+    (the x/y/z planes interleaved on the host -- what RMSF.py:92,124's reader
+    does per frame) and staged, so reading batch k+1 overlaps the copy and
+    kernels of batch k and host memory stays bounded by the batch.
+    ``cache=True``: FrameCache (RMSF.py's second loop reads HBM)."""
+
+    def __init__(self, path, sel=None, batch_frames: int | None = None, n_slots: int = 3, cache: bool = False):
+        from .dcd import DCDFile
+
+        self.f = DCDFile(path)
+        self.n_traj, self.n_atoms = len(self.f), self.f.n_atoms
+        self.sel = None if sel is None else np.ascontiguousarray(sel, dtype=np.int64)
+        if self.sel is not None and self.sel.size and (self.sel.min() < 0 or self.sel.max() >= self.n_atoms):
+            raise IndexError("selection index out of range")
+        self.n_sel = self.n_atoms if self.sel is None else len(self.sel)
+        if batch_frames is None:  # ~64 MB per slot
+            batch_frames = max(1, min(4096, (64 << 20) // max(1, 12 * self.n_sel)))
+        self.batch_frames = batch_frames
+        self.stager = Stager(self.n_sel, self.n_sel, None, batch_frames, n_slots, 1)
+        ok = cache and FrameCache.fits(self.n_traj, self.n_sel)
+        self.cache = FrameCache(self.n_traj, self.n_sel) if ok else None
+
+    def holds(self, frame: int) -> bool:
+        return 0 <= frame < self.n_traj
+
+    def drop_cache(self) -> None:
+        if self.cache is not None:
+            self.cache.drop()
+
+    def _stage(self, first: int, step: int, n: int, stream: int) -> Batch:
+        def stage():
+            buf = np.ascontiguousarray(self.f.read(first, n, step, self.sel))
+            slot, ptr = self.stager.stage_compact(buf, n, stream)  # copied into the pinned slot on return
+            return Batch(ptr, 3 * self.n_sel, n, None, lambda: self.stager.release(slot, stream))
+
+        return _cached_stage(self.cache, first, step, n, stream, stage)
+
+    def reference(self, frame: int, stream: int) -> Batch:
+        if not self.holds(frame):
+            raise IndexError(f"frame {frame} out of range ({self.n_traj} frames)")
+        return self._stage(frame, 1, 1, stream)
+
+    def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
+        bf = min(max_frames, self.batch_frames)
+        for i in range(b0, b1, bf):
+            yield self._stage(frames.r[i], frames.step, min(bf, b1 - i), stream)
+
+
 class AtomGroupSource:
     """MDAnalysis AtomGroup: per-Timestep ``ag.positions`` (the selection rows,
     RMSF.py:95,128) packed into a host batch and staged to the device."""
@@ -473,5 +530,5 @@ class AtomGroupSource:
             yield _cached_stage(self.cache, frames.r[i], frames.step, n, stream, stage)
 
 
-__all__ = ["Batch", "Stager", "FrameCache", "FrameList", "DeviceSource", "HostSource", "XtcDecoder", "XtcSource", "AtomGroupSource",
+__all__ = ["Batch", "Stager", "FrameCache", "FrameList", "DeviceSource", "HostSource", "DcdSource", "XtcDecoder", "XtcSource", "AtomGroupSource",
            "_lib"]

@@ -107,3 +107,27 @@ def test_script_mode_psf_dcd_native(tmp_path):
     got = RMSF(dcd, select=sel, masses=top.masses[sel], align="frame0").run(start=3, stop=90, step=2)
     exp = O.rmsf_script(x, sel, top.masses[sel], size=1, align="frame0", start=3, stop=90, step=2)["rmsf"]
     np.testing.assert_allclose(got.results.rmsf, exp, rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("cache", [False, True])
+def test_dcd_streamed_equals_host_array(tmp_path, cache):
+    """DcdSource reads each batch's selected rows from the memory-mapped file
+    (RMSF.py:92,124's reader) instead of the whole file up front: same frames,
+    same bits as the host array of the same trajectory."""
+    from oracle import synth as SY
+    from rmsf_amd import RMSF
+    from rmsf_amd.dcd import write_dcd
+    from rmsf_amd.sources import DcdSource, HostSource
+    from rmsf_amd.synth import motion_table
+
+    x = SY.frames(5, 700, 0, 61, motion_table(6, 61))
+    sel = np.arange(3, 700, 5)
+    p = str(tmp_path / "t.dcd")
+    write_dcd(p, x)
+    kw = dict(start=2, stop=59, step=3)
+    src = DcdSource(p, sel, batch_frames=4, cache=cache)
+    got = RMSF(src, align="average").run(**kw).results
+    ref = RMSF(HostSource(x, sel, batch_frames=4), align="average").run(**kw).results
+    np.testing.assert_array_equal(got.rmsf, ref.rmsf)
+    np.testing.assert_array_equal(got.average, ref.average)
+    assert (src.cache is not None) == cache
