@@ -36,6 +36,7 @@
 
 #include "rmsf_hip.h"
 #include "xtc_internal.h"
+#include "host_affinity.h"
 
 #define RMSF_EXPORT __attribute__((visibility("default")))
 
@@ -632,8 +633,19 @@ constexpr size_t kCopyMin = 64u << 20;    // host->device copies of at least thi
 // increasing k) and returns; wait() returns when all are done; run() = both.
 class ReadPool {
  public:
-  explicit ReadPool(int n) {
-    for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+  // cpus != nullptr: every worker runs on those CPUs (rmsf_host::device_cpus)
+  explicit ReadPool(int n, const cpu_set_t *cpus = nullptr) {
+    for (int i = 0; i < n; ++i) {
+      if (cpus) {
+        const cpu_set_t c = *cpus;
+        th_.emplace_back([this, c] {
+          rmsf_host::pin_self(c);
+          loop();
+        });
+      } else {
+        th_.emplace_back([this] { loop(); });
+      }
+    }
   }
   ~ReadPool() {
     wait();
@@ -799,7 +811,11 @@ RMSF_EXPORT int rmsf_xtcdec_create(const rmsf_xtc *x, int64_t batch_frames, int 
   d->batch = batch_frames;
   d->n_atoms = x->n_atoms;
   d->n_threads = n_threads;
-  d->pool = std::make_unique<ReadPool>(n_threads);
+  // read threads on the GPU's NUMA node when it is known
+  int dev = 0;
+  cpu_set_t near;
+  const bool pin = hipGetDevice(&dev) == hipSuccess && rmsf_host::device_cpus(dev, &near);
+  d->pool = std::make_unique<ReadPool>(n_threads, pin ? &near : nullptr);
   d->slots.resize(n_slots);
   const size_t raw = (size_t)batch_frames * (size_t)x->max_size;
   for (auto &s : d->slots) {
