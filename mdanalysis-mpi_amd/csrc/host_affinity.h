@@ -1,8 +1,9 @@
 // Host threads next to the GPU: the CPUs of the NUMA node the device's PCIe
 // root sits on (sysfs), restricted to the CPUs this process may use.  The
-// XTC read pool runs there -- its pread copies and the DMA that follows
-// share that socket's memory (C5 on a 2-socket EPYC host: 36-37k frames/s
-// with the readers on the GPU's node vs 32-33k on the other one).
+// XTC read pool and the stager's gather pool run there: their host copies
+// and the DMA that follows share that socket's memory (C5 on a 2-socket EPYC
+// host: 36-37k frames/s with the readers on the GPU's node vs 32-33k on the
+// other one).
 // RMSF_READ_AFFINITY=0 disables it.
 #pragma once
 

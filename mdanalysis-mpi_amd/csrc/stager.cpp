@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "rmsf_hip.h"
+#include "host_affinity.h"
 
 #define RMSF_EXPORT __attribute__((visibility("default")))
 
@@ -45,8 +46,19 @@ int fail(int code, const std::string &m) { return rmsf_internal_set_error(code, 
 // Fixed pool: run(n, fn) calls fn(i) for i in [0, n) on the workers + caller.
 class Pool {
  public:
-  explicit Pool(int n) {
-    for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
+  // cpus != nullptr: the workers run on those CPUs (rmsf_host::device_cpus)
+  explicit Pool(int n, const cpu_set_t *cpus = nullptr) {
+    for (int i = 0; i < n; ++i) {
+      if (cpus) {
+        const cpu_set_t c = *cpus;
+        workers_.emplace_back([this, c] {
+          rmsf_host::pin_self(c);
+          loop();
+        });
+      } else {
+        workers_.emplace_back([this] { loop(); });
+      }
+    }
   }
   ~Pool() {
     {
@@ -249,7 +261,10 @@ RMSF_EXPORT int rmsf_stager_create(int64_t n_atoms_frame, int64_t n_sel, const i
     destroy(st);
     return fail(RMSF_ENOMEM, std::string("rmsf_stager_create: ") + hipGetErrorString(e));
   }
-  st->pool = new Pool(std::max(0, n_threads - 1));
+  int dev = 0;
+  cpu_set_t near;
+  const bool pin = hipGetDevice(&dev) == hipSuccess && rmsf_host::device_cpus(dev, &near);
+  st->pool = new Pool(std::max(0, n_threads - 1), pin ? &near : nullptr);
   st->n_threads = std::max(1, n_threads);
   *out = st;
   return RMSF_OK;
