@@ -149,6 +149,8 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
     devs = device_list(gpus)
     src = _frames_of(inp, select, batch_frames)
     fl = FrameList(src.n_traj, start, stop, step)
+    if fl.r is None:
+        raise NotImplementedError("gpus=: a reversed frame range is not supported; use a positive step")
     if len(fl) == 0:
         raise RmsfEmptyError(-4, "RMSF.run", "no frames selected")
     if align is not None and not 0 <= ref_frame < src.n_traj:

@@ -84,13 +84,14 @@ class RMSF:
 
     # MDAnalysis AnalysisBase compatible signature
     def run(self, start=None, stop=None, step=None, frames=None, verbose=None, **kwargs):
-        if frames is not None:
-            raise NotImplementedError("explicit frame lists are not supported; use start/stop/step")
         if self.gpus is not None:
+            if frames is not None:
+                raise NotImplementedError("frames= with gpus=: use start/stop/step")
             return self._run_multi(start, stop, step)
         eng = Engine(self.device)
         src, masses = self._make_source(eng)
-        fl = FrameList(src.n_traj, start, stop, step)
+        # frames: explicit indices or a boolean mask (AnalysisBase.run(frames=...))
+        fl = FrameList(src.n_traj, start, stop, step, frames=frames)
         rank, size = parallel.world()
         if verbose if verbose is not None else self.verbose:
             b0, b1 = parallel.blocks(len(fl), size)[rank]

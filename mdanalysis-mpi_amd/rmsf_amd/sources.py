@@ -93,21 +93,69 @@ class Stager:
 
 
 class FrameList:
-    """The frame positions ``range(start, stop, step)`` of RMSF.run()."""
+    """The frames of RMSF.run(): ``range(start, stop, step)`` or an explicit
+    ``frames`` selection (indices or a boolean mask over the trajectory, as
+    MDAnalysis' ``AnalysisBase.run(frames=...)`` takes).  An explicit list is
+    taken in ascending order (duplicates kept): the statistics do not depend
+    on the order beyond rounding.  Sources read it as ``runs()``: maximal
+    arithmetic progressions of frames, each one strided batch."""
 
-    def __init__(self, n_traj: int, start=None, stop=None, step=None):
-        self.r = range(n_traj)[slice(start, stop, step)]
+    def __init__(self, n_traj: int, start=None, stop=None, step=None, frames=None):
+        self.idx = None
+        if frames is not None:
+            if start is not None or stop is not None or step is not None:
+                raise ValueError("start/stop/step cannot be combined with frames")
+            f = np.asarray(frames)
+            if f.dtype == bool:
+                if f.shape != (n_traj,):
+                    raise ValueError(f"boolean frames must have one entry per frame ({n_traj})")
+                f = np.flatnonzero(f)
+            f = f.astype(np.int64).reshape(-1)
+            if f.size and (f.min() < -n_traj or f.max() >= n_traj):
+                raise IndexError(f"frame index out of range for {n_traj} frames")
+            self.idx = np.sort(np.where(f < 0, f + n_traj, f), kind="stable")
+            self.r = None
+            return
+        r = range(n_traj)[slice(start, stop, step)]
+        if r.step < 0:  # reversed: the same frames ascending
+            self.idx = np.array(r[::-1], dtype=np.int64)
+            self.r = None
+        else:
+            self.r = r
 
     def __len__(self) -> int:
-        return len(self.r)
+        return len(self.r) if self.r is not None else int(self.idx.size)
+
+    def __getitem__(self, i: int) -> int:
+        return self.r[i] if self.r is not None else int(self.idx[i])
 
     @property
     def start(self) -> int:
-        return self.r.start
+        return self[0]
 
     @property
     def step(self) -> int:
+        if self.r is None:
+            raise ValueError("an explicit frame list has no single step")
         return self.r.step
+
+    def runs(self, b0: int, b1: int, max_n: int) -> Iterator[tuple[int, int, int]]:
+        """(first frame, step >= 1, count) covering positions [b0, b1) in
+        order, each at most ``max_n`` frames."""
+        if self.r is not None:
+            for i in range(b0, b1, max_n):
+                yield self.r[i], self.r.step, min(max_n, b1 - i)
+            return
+        idx = self.idx
+        i = b0
+        while i < b1:
+            st = int(idx[i + 1] - idx[i]) if i + 1 < b1 else 0
+            j = i + 1
+            if st > 0:
+                while j < b1 and j - i < max_n and idx[j] - idx[j - 1] == st:
+                    j += 1
+            yield int(idx[i]), max(st, 1) if j > i + 1 else 1, j - i
+            i = j
 
 
 class DeviceSource:
@@ -147,9 +195,8 @@ class DeviceSource:
         return Batch(self._ptr(frame), self.fstride, 1, self.sel_dev)
 
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
-        for i in range(b0, b1, max_frames):
-            n = min(max_frames, b1 - i)
-            yield Batch(self._ptr(frames.r[i]), self.fstride * frames.step, n, self.sel_dev)
+        for first, step, n in frames.runs(b0, b1, max_frames):
+            yield Batch(self._ptr(first), self.fstride * step, n, self.sel_dev)
 
 
 class FrameCache:
@@ -260,9 +307,8 @@ class HostSource:
         return self._stage(self._row(frame), 1, 1, stream)
 
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
-        bf = min(max_frames, self.batch_frames)
-        for i in range(b0, b1, bf):
-            yield self._stage(self._row(frames.r[i]), frames.step, min(bf, b1 - i), stream)
+        for first, step, n in frames.runs(b0, b1, min(max_frames, self.batch_frames)):
+            yield self._stage(self._row(first), step, n, stream)
 
 
 class XtcDecoder:
@@ -405,12 +451,10 @@ class XtcSource:
         return b
 
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
-        bf = min(max_frames, self.batch_frames)
-        starts = list(range(b0, b1, bf))
         ahead = self.decoder.n_slots - 1 if self.decode_on == "gpu" else 0
         queue = []
-        for k, i in enumerate(starts):
-            queue.append(self._stage(frames.r[i], frames.step, min(bf, b1 - i), stream))
+        for first, step, n in frames.runs(b0, b1, min(max_frames, self.batch_frames)):
+            queue.append(self._stage(first, step, n, stream))
             if len(queue) > ahead:
                 yield queue.pop(0)
         while queue:
@@ -463,9 +507,8 @@ class DcdSource:
         return self._stage(frame, 1, 1, stream)
 
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
-        bf = min(max_frames, self.batch_frames)
-        for i in range(b0, b1, bf):
-            yield self._stage(frames.r[i], frames.step, min(bf, b1 - i), stream)
+        for first, step, n in frames.runs(b0, b1, min(max_frames, self.batch_frames)):
+            yield self._stage(first, step, n, stream)
 
 
 class AtomGroupSource:
@@ -515,19 +558,17 @@ class AtomGroupSource:
         return _cached_stage(self.cache, frame, 1, 1, stream, stage)
 
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
-        bf = min(max_frames, self.batch_frames)
-        for i in range(b0, b1, bf):
-            n = min(bf, b1 - i)
+        for first, step, n in frames.runs(b0, b1, min(max_frames, self.batch_frames)):
 
-            def stage(i=i, n=n):
+            def stage(first=first, step=step, n=n):
                 buf = self._buf()
                 for j in range(n):
-                    self.traj[frames.r[i + j]]
+                    self.traj[first + j * step]
                     buf[j] = self.ag.positions
                 slot, ptr = self.stager.stage_compact(buf, n, stream)
                 return Batch(ptr, 3 * self.n_sel, n, None, lambda: self.stager.release(slot, stream))
 
-            yield _cached_stage(self.cache, frames.r[i], frames.step, n, stream, stage)
+            yield _cached_stage(self.cache, first, step, n, stream, stage)
 
 
 __all__ = ["Batch", "Stager", "FrameCache", "FrameList", "DeviceSource", "HostSource", "DcdSource", "XtcDecoder", "XtcSource", "AtomGroupSource",

@@ -191,3 +191,27 @@ def test_host_frame_cache(c1, kw):
     np.testing.assert_array_equal(got.rmsf, plain.rmsf)
     np.testing.assert_array_equal(got.average, plain.average)
     np.testing.assert_allclose(got.rmsf, d["rmsf_average_P1" if not kw else "rmsf_average_slice"], rtol=0, atol=TOL)
+
+
+@pytest.mark.parametrize("align", [None, "frame0", "average"])
+@pytest.mark.parametrize("where", ["device", "host"])
+def test_explicit_frames(c1, align, where):
+    """run(frames=...) (MDAnalysis AnalysisBase): indices with gaps, strided
+    stretches and a repeated frame, or the same selection as a boolean mask,
+    equal RMSF over the trajectory of just those frames.  Frame 0 is
+    selected, so the frame-0 reference (RMSF.py:80-87) is the same frame."""
+    from rmsf_amd import RMSF
+    d, traj = c1
+    idx = np.array([0, 3, 4, 5, 9, 15, 21, 27, 33, 34, 34, 60, 61, 62, 63, 97])
+    x = torch.tensor(traj, device="cuda") if where == "device" else traj
+    got = RMSF(x, select=d["sel"], align=align, batch_frames=5).run(frames=idx).results
+    exp = RMSF(traj[idx], select=d["sel"], align=align).run().results
+    assert got.n_frames == len(idx)
+    np.testing.assert_allclose(got.rmsf, exp.rmsf, rtol=0, atol=1e-9)
+    mask = np.zeros(98, bool)
+    mask[idx] = True
+    got = RMSF(x, select=d["sel"], align=align).run(frames=mask).results
+    exp = RMSF(traj[mask], select=d["sel"], align=align).run().results
+    np.testing.assert_allclose(got.rmsf, exp.rmsf, rtol=0, atol=1e-9)
+    ref = O.rmsf_script(traj[mask], d["sel"], None, size=1, align=align)["rmsf"]
+    np.testing.assert_allclose(got.rmsf, ref, rtol=0, atol=TOL)
