@@ -89,28 +89,31 @@ class RMSF:
                 raise NotImplementedError("frames= with gpus=: use start/stop/step")
             return self._run_multi(start, stop, step)
         eng = Engine(self.device)
-        src, masses = self._make_source(eng)
-        # frames: explicit indices or a boolean mask (AnalysisBase.run(frames=...))
-        fl = FrameList(src.n_traj, start, stop, step, frames=frames)
-        rank, size = parallel.world()
-        if verbose if verbose is not None else self.verbose:
-            b0, b1 = parallel.blocks(len(fl), size)[rank]
-            print("Process:%3d --> Frames: %10d -- %10d" % (rank, b0, b1))  # RMSF.py:74
-        res = run_pipeline(eng, src, fl, align=self.align, masses=masses, ref_frame=self.ref_frame,
-                           max_batch=self.batch_frames, n_splits=self.n_splits, collect_rmsd=self.collect_rmsd)
-        torch.cuda.current_stream(eng.device).synchronize()
-        r = self.results
-        r.rmsf = res.rmsf.cpu().numpy()
-        r.mean = res.mean.cpu().numpy()
-        r.sumsquares = res.m2.cpu().numpy()
-        r.m2 = r.sumsquares
-        r.n_frames = res.n_frames
-        r.n_local = res.n_local
-        r.block = res.block
-        if res.average is not None:
-            r.average = res.average.cpu().numpy()
-        if res.rmsd is not None:
-            r.rmsd = res.rmsd.cpu().numpy()
+        # torch's current device = the engine's, so the buffers sources and
+        # caches allocate live on the device the kernels run on
+        with torch.cuda.device(eng.device):
+            src, masses = self._make_source(eng)
+            # frames: explicit indices or a boolean mask (AnalysisBase.run(frames=...))
+            fl = FrameList(src.n_traj, start, stop, step, frames=frames)
+            rank, size = parallel.world()
+            if verbose if verbose is not None else self.verbose:
+                b0, b1 = parallel.blocks(len(fl), size)[rank]
+                print("Process:%3d --> Frames: %10d -- %10d" % (rank, b0, b1))  # RMSF.py:74
+            res = run_pipeline(eng, src, fl, align=self.align, masses=masses, ref_frame=self.ref_frame,
+                               max_batch=self.batch_frames, n_splits=self.n_splits, collect_rmsd=self.collect_rmsd)
+            torch.cuda.current_stream(eng.device).synchronize()
+            r = self.results
+            r.rmsf = res.rmsf.cpu().numpy()
+            r.mean = res.mean.cpu().numpy()
+            r.sumsquares = res.m2.cpu().numpy()
+            r.m2 = r.sumsquares
+            r.n_frames = res.n_frames
+            r.n_local = res.n_local
+            r.block = res.block
+            if res.average is not None:
+                r.average = res.average.cpu().numpy()
+            if res.rmsd is not None:
+                r.rmsd = res.rmsd.cpu().numpy()
         self.n_frames = res.n_frames
         return self
 
