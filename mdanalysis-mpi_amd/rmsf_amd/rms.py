@@ -15,7 +15,12 @@ contiguous blocks of RMSF.py:65-69 and merged with RCCL.
 
 Inputs: an MDAnalysis AtomGroup, a host ``numpy`` float32 array
 [n_frames, n_atoms, 3], an HBM-resident torch tensor of that shape, or the
-path of a GROMACS ``.xtc`` file (decoded natively, selection by ``select``).
+path of a GROMACS ``.xtc`` or CHARMM/NAMD ``.dcd`` file (read natively,
+selection by ``select``).
+
+``run(start, stop, step)`` or ``run(frames=...)`` (indices or a boolean mask,
+as ``AnalysisBase.run``; taken in ascending order, so ``results.rmsd`` with
+``collect_rmsd=True`` follows the sorted frames).
 """
 from __future__ import annotations
 
