@@ -66,6 +66,36 @@ class _HostFrames:
             # rows is an arithmetic range: a strided view, pushed with its step
             ctx.push(self.arr[rows.start:rows[-1] + 1], mode, step=rows.step)
 
+    def n_sel(self) -> int:
+        return self.n_atoms if self.sel is None else len(self.sel)
+
+    def stage_block(self, dev: int, rows: range):
+        """The block's selected rows staged once into HBM on ``dev`` (pinned
+        stager, then a resident [n, n_sel, 3] tensor): RMSF.py's two loops
+        (RMSF.py:92,124) then both read HBM (run_multi checks the fit first)."""
+        import torch
+
+        from .sources import FrameCache, Stager
+
+        ns = self.n_sel()
+        if not len(rows):
+            return None
+        with torch.cuda.device(dev):
+            cache = FrameCache(len(rows), ns, device=torch.device("cuda", dev))
+            batch = max(1, min(4096, (64 << 20) // max(1, 12 * ns)))
+            st = Stager(self.n_atoms, ns, self.sel, batch, 3, 4)
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            try:
+                for i in range(0, len(rows), batch):
+                    n = min(batch, len(rows) - i)
+                    slot, ptr = st.stage(self.arr, rows[i], rows.step, n, stream)
+                    cache.fill(i, 1, n, ptr, stream)
+                    st.release(slot, stream)
+                torch.cuda.current_stream(dev).synchronize()
+            finally:
+                st.close()
+        return cache.buf
+
 
 class _XtcFrames:
     """A GROMACS XTC file: each context decompresses its block on its GPU."""
@@ -116,6 +146,16 @@ class _AtomGroupFrames:
             ctx.push(buf[:len(part)], mode)
 
 
+def _blocks_fit(devs, blocks, n_sel: int) -> bool:
+    """Every device can hold its blocks' selected rows in half its free HBM."""
+    import torch
+
+    need = {}
+    for d, r in zip(devs, blocks):
+        need[d] = need.get(d, 0) + 12 * len(r) * n_sel
+    return all(n <= torch.cuda.mem_get_info(d)[0] // 2 for d, n in need.items())
+
+
 def _frames_of(inp, sel, batch_frames):
     import os
 
@@ -157,12 +197,19 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
         raise IndexError(f"ref_frame {ref_frame} outside the trajectory ({src.n_traj} frames)")
     if masses is None and align is not None and isinstance(src, _AtomGroupFrames):
         masses = np.asarray(src.ag.masses, dtype=np.float64)
-    ctxs = [Context(src.n_atoms, sel=src.sel, masses=masses, device=d) for d in devs]
+    # RMSF.py's two sweeps over a host array: each device stages its block's
+    # selected rows into HBM once and both sweeps read them there (contexts
+    # over the selection only: the in-kernel gather becomes the identity)
+    blocks = [range(fl.r[b0], fl.r[b1 - 1] + 1, fl.step) if b1 > b0 else range(0)
+              for b0, b1 in parallel.blocks(len(fl), len(devs))]
+    staged = align == "average" and isinstance(src, _HostFrames) and _blocks_fit(devs, blocks, src.n_sel())
+    if staged:
+        ctxs = [Context(src.n_sel(), sel=None, masses=masses, device=d) for d in devs]
+    else:
+        ctxs = [Context(src.n_atoms, sel=src.sel, masses=masses, device=d) for d in devs]
     try:
         if len(set(devs)) == len(devs) and len(devs) > 1:
             Context.init_all(ctxs)  # ncclCommInitAll: one communicator per device
-        blocks = [range(fl.r[b0], fl.r[b1 - 1] + 1, fl.step) if b1 > b0 else range(0)
-                  for b0, b1 in parallel.blocks(len(fl), len(devs))]
 
         def each(fn):
             if getattr(src, "serial", False) or len(ctxs) == 1:
@@ -176,15 +223,30 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
         out = {}
         if align is not None:
             ref = src.reference(ref_frame)
+            if staged and src.sel is not None:
+                ref = ref[src.sel]
             for c in ctxs:  # every rank reads the reference frame (RMSF.py:80-87)
                 c.set_reference_frame(ref)
+        cached = {}
+        if staged:
+            def stage(c, r):
+                cached[id(c)] = src.stage_block(c.device, r)
+            each(stage)
+
+        def push(c, r, mode):
+            if staged:
+                if len(r):
+                    c.push(cached[id(c)], mode)
+            else:
+                src.push(c, r, mode)
+
         if align == "average":
-            each(lambda c, r: src.push(c, r, PUSH_ALIGN_SUM))
+            each(lambda c, r: push(c, r, PUSH_ALIGN_SUM))
             Context.multi_allreduce_sum(ctxs)
             for c in ctxs:
                 c.set_reference_average()
             out["average"] = ctxs[0].average().reshape(-1)  # flat, as the pipeline returns it
-        each(lambda c, r: src.push(c, r, PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD))
+        each(lambda c, r: push(c, r, PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD))
         Context.multi_chan_merge(ctxs)
         n, mean, m2 = ctxs[0].partial()
         out.update(rmsf=ctxs[0].rmsf(), mean=mean, sumsquares=m2, n_frames=n,
