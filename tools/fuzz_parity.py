@@ -1,6 +1,6 @@
 """Randomised parity sweep (not product code, not a test): random shapes,
 selections, align modes, frame selections and inputs (HBM tensor / host
-array / DCD file) through RMSF(...).run() vs the oracle's RMSF.py
+array / DCD or XTC file) through RMSF(...).run() vs the oracle's RMSF.py
 restatement on the selected frames.  python tools/fuzz_parity.py [n_cases]"""
 import os
 import sys
@@ -16,6 +16,7 @@ from oracle import rmsf_oracle as O  # noqa: E402
 from oracle import synth as SY  # noqa: E402
 from rmsf_amd import RMSF  # noqa: E402
 from rmsf_amd.dcd import write_dcd  # noqa: E402
+from rmsf_amd.xtc import XTCFile, write_xtc  # noqa: E402
 from rmsf_amd.synth import motion_table  # noqa: E402
 
 
@@ -33,14 +34,19 @@ def main():
         frames = np.flatnonzero(rng.random(nf) < rng.uniform(0.2, 1.0))
         if frames.size == 0 or frames[0] != 0:
             frames = np.concatenate([[0], frames[frames != 0]])  # keep the frame-0 reference in the list
-        where = ["device", "host", "dcd"][int(rng.integers(0, 3))]
+        where = ["device", "host", "dcd", "xtc"][int(rng.integers(0, 4))]
         if where == "device":
             x = torch.tensor(traj, device="cuda")
         elif where == "host":
             x = traj
-        else:
+        elif where == "dcd":
             x = os.path.join(tmp, f"c{k}.dcd")
             write_dcd(x, traj)
+        else:  # XTC is lossy: the oracle sees the frames as the (host) codec reads them back
+            x = os.path.join(tmp, f"c{k}.xtc")
+            write_xtc(x, traj)
+            with XTCFile(x) as f:
+                traj = f.read()
         bf = int(rng.integers(1, 64))
         got = RMSF(x, select=sel, align=align, batch_frames=bf).run(frames=frames).results.rmsf
         exp = O.rmsf_script(traj[frames], sel, None, size=1, align=align)["rmsf"]
