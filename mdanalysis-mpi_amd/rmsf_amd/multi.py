@@ -69,28 +69,33 @@ class _HostFrames:
     def n_sel(self) -> int:
         return self.n_atoms if self.sel is None else len(self.sel)
 
-    def stage_block(self, dev: int, rows: range):
-        """The block's selected rows staged once into HBM on ``dev`` (pinned
-        stager, then a resident [n, n_sel, 3] tensor): RMSF.py's two loops
-        (RMSF.py:92,124) then both read HBM (run_multi checks the fit first)."""
+    def stage_block(self, dev: int, runs: list):
+        """The block's selected rows (``runs``: strided ranges of frames)
+        staged once into HBM on ``dev`` (pinned stager, then a resident
+        [n, n_sel, 3] tensor): RMSF.py's two loops (RMSF.py:92,124) then both
+        read HBM (run_multi checks the fit first)."""
         import torch
 
         from .sources import FrameCache, Stager
 
         ns = self.n_sel()
-        if not len(rows):
+        total = sum(len(r) for r in runs)
+        if not total:
             return None
         with torch.cuda.device(dev):
-            cache = FrameCache(len(rows), ns, device=torch.device("cuda", dev))
+            cache = FrameCache(total, ns, device=torch.device("cuda", dev))
             batch = max(1, min(4096, (64 << 20) // max(1, 12 * ns)))
             st = Stager(self.n_atoms, ns, self.sel, batch, 3, 4)
             stream = torch.cuda.current_stream(dev).cuda_stream
             try:
-                for i in range(0, len(rows), batch):
-                    n = min(batch, len(rows) - i)
-                    slot, ptr = st.stage(self.arr, rows[i], rows.step, n, stream)
-                    cache.fill(i, 1, n, ptr, stream)
-                    st.release(slot, stream)
+                row = 0
+                for rows in runs:
+                    for i in range(0, len(rows), batch):
+                        n = min(batch, len(rows) - i)
+                        slot, ptr = st.stage(self.arr, rows[i], rows.step, n, stream)
+                        cache.fill(row, 1, n, ptr, stream)
+                        st.release(slot, stream)
+                        row += n
                 torch.cuda.current_stream(dev).synchronize()
             finally:
                 st.close()
@@ -151,8 +156,8 @@ def _blocks_fit(devs, blocks, n_sel: int) -> bool:
     import torch
 
     need = {}
-    for d, r in zip(devs, blocks):
-        need[d] = need.get(d, 0) + 12 * len(r) * n_sel
+    for d, runs in zip(devs, blocks):
+        need[d] = need.get(d, 0) + 12 * sum(len(r) for r in runs) * n_sel
     return all(n <= torch.cuda.mem_get_info(d)[0] // 2 for d, n in need.items())
 
 
@@ -178,7 +183,7 @@ def _frames_of(inp, sel, batch_frames):
 
 
 def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int = 0, start=None, stop=None,
-              step=None, batch_frames: int | None = None) -> dict:
+              step=None, batch_frames: int | None = None, frames=None) -> dict:
     """RMSF.py's computation over the devices ``gpus`` from one process.
     Returns the ``results`` fields (rmsf, mean, sumsquares, n_frames, ...)."""
     if align not in (None, "frame0", "average"):
@@ -188,9 +193,7 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
                          "(one process per GPU) leave it unset")
     devs = device_list(gpus)
     src = _frames_of(inp, select, batch_frames)
-    fl = FrameList(src.n_traj, start, stop, step)
-    if fl.r is None:
-        raise NotImplementedError("gpus=: a reversed frame range is not supported; use a positive step")
+    fl = FrameList(src.n_traj, start, stop, step, frames=frames)
     if len(fl) == 0:
         raise RmsfEmptyError(-4, "RMSF.run", "no frames selected")
     if align is not None and not 0 <= ref_frame < src.n_traj:
@@ -200,7 +203,9 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
     # RMSF.py's two sweeps over a host array: each device stages its block's
     # selected rows into HBM once and both sweeps read them there (contexts
     # over the selection only: the in-kernel gather becomes the identity)
-    blocks = [range(fl.r[b0], fl.r[b1 - 1] + 1, fl.step) if b1 > b0 else range(0)
+    # each device's RMSF.py:65-69 block of the frame list, as strided runs
+    big = max(1, len(fl))
+    blocks = [[range(f, f + s * n, s) for f, s, n in fl.runs(b0, b1, big)]
               for b0, b1 in parallel.blocks(len(fl), len(devs))]
     staged = align == "average" and isinstance(src, _HostFrames) and _blocks_fit(devs, blocks, src.n_sel())
     if staged:
@@ -233,12 +238,13 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
                 cached[id(c)] = src.stage_block(c.device, r)
             each(stage)
 
-        def push(c, r, mode):
+        def push(c, runs, mode):
             if staged:
-                if len(r):
+                if cached[id(c)] is not None:
                     c.push(cached[id(c)], mode)
             else:
-                src.push(c, r, mode)
+                for r in runs:
+                    src.push(c, r, mode)
 
         if align == "average":
             each(lambda c, r: push(c, r, PUSH_ALIGN_SUM))

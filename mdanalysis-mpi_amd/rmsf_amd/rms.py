@@ -90,9 +90,7 @@ class RMSF:
     # MDAnalysis AnalysisBase compatible signature
     def run(self, start=None, stop=None, step=None, frames=None, verbose=None, **kwargs):
         if self.gpus is not None:
-            if frames is not None:
-                raise NotImplementedError("frames= with gpus=: use start/stop/step")
-            return self._run_multi(start, stop, step)
+            return self._run_multi(start, stop, step, frames)
         eng = Engine(self.device)
         # torch's current device = the engine's, so the buffers sources and
         # caches allocate live on the device the kernels run on
@@ -122,7 +120,7 @@ class RMSF:
         self.n_frames = res.n_frames
         return self
 
-    def _run_multi(self, start, stop, step):
+    def _run_multi(self, start, stop, step, frames=None):
         """``gpus=N`` (or a list of device ids): one process drives N devices
         through the context ABI, RCCL communicators from ncclCommInitAll
         (rmsf_amd.multi)."""
@@ -132,7 +130,7 @@ class RMSF:
             raise NotImplementedError("collect_rmsd is not available with gpus=; use torch.distributed ranks")
         out = run_multi(self._input, self.gpus, select=self.select, align=self.align, masses=self.masses,
                         ref_frame=self.ref_frame, start=start, stop=stop, step=step,
-                        batch_frames=self.batch_frames)
+                        batch_frames=self.batch_frames, frames=frames)
         r = self.results
         r.update(out)
         r.m2 = r.sumsquares

@@ -94,3 +94,17 @@ def test_multi_errors(traj):
         RMSF(traj, gpus=[0, 0]).run(start=5, stop=5)
     with pytest.raises(NotImplementedError):
         RMSF(traj, align="frame0", collect_rmsd=True, gpus=1).run()
+
+
+@pytest.mark.parametrize("align", [None, "frame0", "average"])
+def test_multi_explicit_frames(traj, align):
+    """gpus= with run(frames=...): each device takes its RMSF.py:65-69 block of
+    the frame list as strided runs; same result as one device."""
+    from rmsf_amd import RMSF
+    idx = np.array([0, 2, 4, 6, 7, 8, 13, 14, 20, 20, 29])
+    idx = idx[idx < len(traj)]
+    sel = np.arange(1, traj.shape[1], 3)
+    one = RMSF(traj, select=sel, align=align).run(frames=idx).results
+    r = RMSF(traj, select=sel, align=align, gpus=[0, 0, 0]).run(frames=idx).results
+    np.testing.assert_allclose(r.rmsf, one.rmsf, rtol=0, atol=1e-9)
+    assert r.n_frames == len(idx)
