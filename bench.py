@@ -1,26 +1,40 @@
 #!/usr/bin/env python3
 """Headline benchmark: atom-frames/s of the frame-parallel RMSF path on MI355X.
 
-  python bench.py [--gpus N --steps K --warmup W]            (N=1)
+  python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
       --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
-One "step" = one full RMSF pass of the hot path over the rank's frame block
-(the per-frame Welford accumulator over every frame, the in-GPU Chan merge of
-the frame tiles, the cross-GPU Chan merge over RCCL, the finalise), with the
-synthetic trajectory already resident in HBM.  Workload per GPU (weak
-scaling, frame-sharded by the RMSF.py:65-69 blocks):
-  c2 (default): 100k atoms x 20k frames fp32 per GPU, no alignment
-                (BASELINE.json configs[1]); N GPUs hold 20k*N frames.
-  c4:           1M atoms x 2.5k frames per GPU (at N=8 = configs[3], 240 GB).
-At N=1 the aligned configurations are measured too and reported under
-"modes" (C3 = QCP alignment to frame 0; RMSF.py's own two-sweep "average").
+One "step" = one full RMSF pass of the hot path over the trajectory (the
+per-frame Welford accumulator over every frame of each device's block, the
+in-GPU Chan merge of the frame tiles, the cross-GPU Chan merge over RCCL,
+the finalise), with the synthetic trajectory already resident in HBM.
 
-Rank 0 prints ONE JSON line.  ``roofline`` is measured live with HIP events
-around the dominant kernel (k_welford_flat_sk, the balanced-grid Welford
-stream; k_welford_flat with --splits) on its launch stream;
-``cpu_baseline`` is the oracle's numpy restatement of RMSF.py's per-rank loop
-timed on this host's cores (run before the GPU is touched).
+Scaling (``--scaling``):
+  strong (default)  ONE trajectory of ``--frames`` frames (c2: 100k atoms x
+                    20k frames, BASELINE.json configs[1]; the north star's
+                    "100k-atom x 20k-frame data at 1, 2, 4 and 8 GPUs") split
+                    into the RMSF.py:65-69 frame blocks, one per GPU;
+  weak              every GPU holds a ``--frames``-frame block (c4: 1M atoms x
+                    2.5k frames per GPU = configs[3] at N=8).
+
+Multi-GPU, two launch forms with the same arithmetic:
+  * under torch.distributed.run (WORLD_SIZE set): one process per GPU,
+    merges over torch.distributed's RCCL backend;
+  * ``python bench.py --gpus N`` with no launcher: ONE process drives N
+    devices through the C ABI's contexts (ncclCommInitAll, one
+    stream per device, one host thread per device).  With fewer than N
+    devices visible it fails, unless ``--rehearse`` (device 0 listed N
+    times, in-process fold instead of RCCL; labelled in the output).
+
+At N=1 the aligned configurations are measured too ("modes": C3 = QCP
+alignment to frame 0; RMSF.py's own two-sweep "average").  Rank 0 prints ONE
+JSON line.  ``roofline`` = algorithmic bytes (12 B per atom-frame, SURVEY
+8(d)) of every timed launch of the dominant kernel / their summed duration,
+from HIP events recorded around each launch on its own stream;
+``cpu_baseline`` = the oracle's numpy restatement of RMSF.py's two sweeps on
+the host's usable cores (``mpirun -n <cores> python RMSF.py`` shape), run
+before the GPU is touched, with the unaligned (C2) sweep as a second figure.
 """
 from __future__ import annotations
 
@@ -37,38 +51,48 @@ HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md, chip table)
 FP64_PEAK_TFS = 78.6    # MI355X fp64 vector spec (not in the local guide, unverified)
 B_PER_ATOM_FRAME = 12   # algorithmic bytes per (atom, frame) per sweep
 FLOP_PER_ATOM_FRAME_SUPERPOSE = 27  # covariance 18 + |x|^2 6 + COM 3
+METRIC = "atom-frames/sec (RMSF) + achieved HBM GB/s fraction"
 
 WORKLOADS = {
-    "c2": dict(n_atoms=100_000, frames_per_gpu=20_000, align=None,
-               name="C2: synthetic 100k atoms x 20k frames fp32 per GPU, no alignment, fp64 Welford"),
-    "c3": dict(n_atoms=100_000, frames_per_gpu=20_000, align="frame0",
-               name="C3: synthetic 100k atoms x 20k frames fp32 per GPU, QCP alignment to frame 0"),
-    "average": dict(n_atoms=100_000, frames_per_gpu=20_000, align="average",
-                    name="RMSF.py two-sweep: 100k atoms x 20k frames per GPU, align to frame 0, average, re-align"),
-    "c4": dict(n_atoms=1_000_000, frames_per_gpu=2_500, align=None,
+    "c2": dict(n_atoms=100_000, frames=20_000, align=None,
+               name="C2: synthetic 100k atoms x 20k frames fp32, no alignment, fp64 Welford"),
+    "c3": dict(n_atoms=100_000, frames=20_000, align="frame0",
+               name="C3: synthetic 100k atoms x 20k frames fp32, QCP alignment to frame 0"),
+    "average": dict(n_atoms=100_000, frames=20_000, align="average",
+                    name="RMSF.py two-sweep: 100k atoms x 20k frames, align to frame 0, average, re-align"),
+    "c4": dict(n_atoms=1_000_000, frames=2_500, align=None, scaling="weak",
                name="C4 share: synthetic 1M atoms x 2.5k frames fp32 per GPU (N=8: 1M x 20k, 240 GB)"),
-    "c5": dict(n_atoms=250_000, frames_per_gpu=1_000, align=None, host=True,
+    "c5": dict(n_atoms=250_000, frames=1_000, align=None, host=True,
                name="C5 (pre-decoded): 250k atoms x 1k frames fp32 in host memory, streamed via the pinned "
                     "multi-buffer stager (PCIe-inclusive rate; no XTC decode)"),
-    "c5xtc": dict(n_atoms=250_000, frames_per_gpu=2048, align=None, host=True, xtc=True,
+    "c5xtc": dict(n_atoms=250_000, frames=2048, align=None, host=True, xtc=True,
                   name="C5: 250k-atom XTC file (precision 1000) streamed from the host and decoded "
                        "(--xtc-decode gpu: compressed records via pinned slots, decompressed on the GPU; host: "
                        "decoded on host threads into the pinned stager); read + PCIe + decode inclusive"),
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default=None,
+                    help="strong: --frames in total split over the GPUs (default); weak: --frames per GPU")
     ap.add_argument("--n-atoms", type=int, default=None)
-    ap.add_argument("--frames-per-gpu", type=int, default=None)
+    ap.add_argument("--frames", type=int, default=None,
+                    help="trajectory frames (strong) or frames per GPU (weak); default: the workload's")
+    ap.add_argument("--frames-per-gpu", type=int, default=None, help="shorthand for --scaling weak --frames F")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="one-process --gpus N with fewer devices: list device 0 N times (rehearsal)")
     ap.add_argument("--splits", type=int, default=None)
     ap.add_argument("--batch-frames", type=int, default=None, help="aligned modes: frames per superpose batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=640, help="frames per CPU process in the baseline sample")
+    ap.add_argument("--cpu-frames", type=int, default=640,
+                    help="frames per CPU process for the unaligned (C2) baseline sample")
+    ap.add_argument("--cpu-average-frames", type=int, default=128,
+                    help="frames per CPU process for the RMSF.py two-sweep baseline sample")
     ap.add_argument("--no-modes", action="store_true", help="skip the aligned-mode measurements at N=1")
     ap.add_argument("--mode-steps", type=int, default=3)
     ap.add_argument("--stager-threads", type=int, default=4)
@@ -83,7 +107,41 @@ def parse():
     ap.add_argument("--align", choices=["none", "frame0", "average"], default=None, help="override the workload's")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo only "
                                                      "to rehearse several ranks on one GPU)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def resolve(a, world: int) -> dict:
+    """The workload of this run: atoms, frames in total, this run's scaling."""
+    wl = dict(WORKLOADS[a.workload])
+    if a.n_atoms:
+        wl["n_atoms"] = a.n_atoms
+    scaling = a.scaling or wl.get("scaling", "strong")
+    frames = wl["frames"]
+    if a.frames_per_gpu:
+        scaling, frames = "weak", a.frames_per_gpu
+    if a.frames:
+        frames = a.frames
+    if a.align is not None:
+        wl["align"] = None if a.align == "none" else a.align
+    wl["scaling"] = scaling
+    wl["n_total"] = frames * world if scaling == "weak" else frames
+    if wl["n_total"] < world:
+        raise SystemExit(f"{wl['n_total']} frames cannot give each of {world} GPUs a block")
+    return wl
+
+
+def device_plan(n: int, visible: int, rehearse: bool) -> tuple[list[int], bool]:
+    """Devices for a one-process ``--gpus n`` run: 0..n-1, or (``rehearse``)
+    device 0 listed n times when fewer are visible.  Fails loudly otherwise."""
+    if n < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if visible >= n:
+        return list(range(n)), False
+    if rehearse and visible >= 1:
+        return [0] * n, True
+    raise SystemExit(f"--gpus {n} asks for {n} devices but {visible} are visible "
+                     f"(launch under torch.distributed.run on an {n}-GPU node, or pass --rehearse "
+                     f"to run {n} device contexts on device 0)")
 
 
 def load_traffic(workload: str, n_atoms: int, n_frames: int):
@@ -102,6 +160,18 @@ def load_traffic(workload: str, n_atoms: int, n_frames: int):
     return None
 
 
+def roofline(kernel: str, launches: int, ms: float, atom_frames: float, traffic=None, traffic_source=None) -> dict:
+    """Algorithmic bytes of the timed launches over their summed duration."""
+    s = ms / 1e3
+    achieved = B_PER_ATOM_FRAME * atom_frames / s / 1e9 if s > 0 else 0.0
+    return {"bound": "hbm", "kernel": kernel, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_source,
+            "launches": launches, "avg_launch_ms": ms / max(1, launches),
+            "algorithmic_bytes_per_launch": B_PER_ATOM_FRAME * atom_frames / max(1, launches),
+            "bytes_rule": "12 B per (atom, frame) of each timed launch (SURVEY.md 8(d)); achieved = sum(bytes) / "
+                          "sum(HIP-event launch time)"}
+
+
 def c1_latency(eng, no_cpu: bool) -> dict:
     """Config C1 shape (BASELINE configs[0]): 3341 atoms, 214 selected, 98
     frames, RMSF.py's two-sweep average alignment -- latency of one full
@@ -111,7 +181,7 @@ def c1_latency(eng, no_cpu: bool) -> dict:
     import numpy as np
     import torch
 
-    from rmsf_amd.pipeline import run_pipeline
+    from rmsf_amd.pipeline import CapturedPipeline, run_pipeline
     from rmsf_amd.sources import DeviceSource, FrameList
     from rmsf_amd.synth import generate, motion_table
 
@@ -130,8 +200,6 @@ def c1_latency(eng, no_cpu: bool) -> dict:
         res = run_pipeline(eng, src, fl, align="average")
     torch.cuda.synchronize()
     gpu_ms = (time.perf_counter() - t0) / reps * 1e3
-    from rmsf_amd.pipeline import CapturedPipeline
-
     cap = CapturedPipeline(eng, src, fl, align="average")
     for _ in range(5):
         cap.replay()
@@ -155,29 +223,170 @@ def c1_latency(eng, no_cpu: bool) -> dict:
     return out
 
 
+def cpu_baselines(a, wl) -> tuple[dict | None, dict | None]:
+    """Before any GPU call: RMSF.py's two sweeps (the north star's ``mpirun -n
+    <cores> python RMSF.py``) and the unaligned C2 sweep, both on the usable
+    host cores, bounded samples of the same 100k-atom trajectory."""
+    from oracle import cpu_baseline
+    from rmsf_amd.synth import motion_table  # numpy only: no GPU touched
+
+    cores = cpu_baseline.available_cores()[0]
+    n = wl["n_atoms"]
+    avg = cpu_baseline.run(n, a.cpu_average_frames, align="average",
+                           motion=motion_table(1, a.cpu_average_frames * cores))
+    flat = cpu_baseline.run(n, a.cpu_frames, align="none")
+    return avg, flat
+
+
+def base_line(a, wl, n_gpus: int, dt: float, parallelism: str) -> dict:
+    n_atoms, n_total = wl["n_atoms"], wl["n_total"]
+    return {
+        "metric": METRIC,
+        "value": n_total * n_atoms * a.steps / dt,
+        "unit": "atom-frames/s",
+        "n_gpus": n_gpus,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": wl["scaling"],
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: counter-based generator, fp32 frames resident in HBM (generated on device)",
+        "config": {"workload": wl["name"], "n_atoms": n_atoms, "n_frames_total": n_total,
+                   "n_frames_per_gpu": n_total // n_gpus,
+                   "selection": "all atoms", "align": wl["align"], "parallelism": parallelism},
+    }
+
+
+# ---------------------------------------------------------------------------
+# one process, N devices (no launcher): the C ABI's contexts
+
+
+def main_single_process(a, wl, cpu) -> None:
+    """``--gpus N`` with no WORLD_SIZE: one context per device, each device's
+    RMSF.py:65-69 block generated in its HBM, pushed from its own host
+    thread; the exchanges over ncclCommInitAll communicators (the in-process
+    fold for a --rehearse device list)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+
+    from rmsf_amd import parallel
+    from rmsf_amd.context import PUSH_ALIGN_SUM, PUSH_ALIGN_WELFORD, PUSH_WELFORD, Context
+    from rmsf_amd.engine import Engine
+    from rmsf_amd.synth import generate, motion_table
+
+    if wl.get("host"):
+        raise SystemExit("one-process multi-GPU runs cover the HBM-resident workloads (c2, c3, average, c4)")
+    devs, rehearsal = device_plan(a.gpus, torch.cuda.device_count(), a.rehearse)
+    n = len(devs)
+    n_atoms, n_total, align = wl["n_atoms"], wl["n_total"], wl["align"]
+    blocks = parallel.blocks(n_total, n)
+    motion = motion_table(1, n_total) if align else None
+    ctxs, trajs, refs = [], [], []
+    for d, (b0, b1) in zip(devs, blocks):
+        with torch.cuda.device(d):
+            eng = Engine(torch.device("cuda", d))
+            trajs.append(generate(eng, n_atoms, b0, b1 - b0, seed=0, motion=motion))
+            # every rank reads frame 0 itself (RMSF.py:80-87): an input, like the block
+            refs.append(generate(eng, n_atoms, 0, 1, seed=0, motion=motion) if align else None)
+            torch.cuda.synchronize(d)
+        c = Context(n_atoms, device=d)
+        c.set_timing(True)
+        ctxs.append(c)
+    if not rehearsal and n > 1:
+        Context.init_all(ctxs)
+    pool = ThreadPoolExecutor(n)
+
+    def each(fn):
+        for f in [pool.submit(fn, i) for i in range(n)]:
+            f.result()
+
+    def step():
+        def sweep1(i):
+            c = ctxs[i]
+            c.reset()
+            if align:
+                c.set_reference_frame(refs[i][0])
+            if align == "average":
+                c.push(trajs[i], PUSH_ALIGN_SUM)                            # RMSF.py:89-105
+            else:
+                c.push(trajs[i], PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD)
+
+        each(sweep1)
+        if align == "average":
+            Context.multi_allreduce_sum(ctxs)                               # RMSF.py:107-110
+
+            def sweep2(i):
+                ctxs[i].set_reference_average()                             # RMSF.py:111-118
+                ctxs[i].push(trajs[i], PUSH_ALIGN_WELFORD)                  # RMSF.py:120-138
+            each(sweep2)
+        Context.multi_chan_merge(ctxs)                                      # RMSF.py:140-143
+        return ctxs[0].rmsf()                                               # RMSF.py:145-146
+
+    for _ in range(a.warmup):
+        step()
+    for c in ctxs:  # drop the warm-up's launch records
+        c.kernel_time("accumulate"), c.kernel_time("superpose")
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        rmsf = step()
+    for c in ctxs:
+        c.synchronize()
+    dt = time.perf_counter() - t0
+    acc = [c.kernel_time("accumulate") for c in ctxs]
+    sup = [c.kernel_time("superpose") for c in ctxs]
+    par = (f"one process, {n} device contexts (RMSF.py:65-69 blocks), "
+           + ("REHEARSAL: device 0 listed %d times, in-process fold" % n if rehearsal
+              else "RCCL via ncclCommInitAll") + ", exact k-way Chan merge")
+    out = base_line(a, wl, n, dt, par)
+    out["devices"] = devs
+    out["rehearsal"] = rehearsal
+    kname = ("k_accum_atoms_sk" if align else "k_welford_flat_sk")
+    out["roofline"] = roofline(kname, sum(x[0] for x in acc), sum(x[1] for x in acc), sum(x[2] for x in acc))
+    out["roofline"]["per_device_gbs"] = [B_PER_ATOM_FRAME * x[2] / (x[1] / 1e3) / 1e9 if x[1] else None for x in acc]
+    if align:
+        ms, af = sum(x[1] for x in sup), sum(x[2] for x in sup)
+        out["superpose"] = {"launches": sum(x[0] for x in sup), "avg_launch_ms": ms / max(1, sum(x[0] for x in sup)),
+                            "gflops": FLOP_PER_ATOM_FRAME_SUPERPOSE * af / (ms / 1e3) / 1e9 if ms else None}
+    out["cpu_baseline"] = cpu
+    out["rmsf_checksum"] = float(rmsf.sum())
+    print(json.dumps(out), flush=True)
+    pool.shutdown()
+    for c in ctxs:
+        c.close()
+
+
+# ---------------------------------------------------------------------------
+# one process per GPU (torch.distributed) or N=1
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    wl = dict(WORKLOADS[a.workload])
-    if a.n_atoms:
-        wl["n_atoms"] = a.n_atoms
-    if a.frames_per_gpu:
-        wl["frames_per_gpu"] = a.frames_per_gpu
-    if a.align is not None:
-        wl["align"] = None if a.align == "none" else a.align
-    n_atoms, per_gpu = wl["n_atoms"], wl["frames_per_gpu"]
+    launched = "WORLD_SIZE" in os.environ
+    if launched and a.gpus != world and not a.backend == "gloo":
+        raise SystemExit(f"--gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    single_multi = not launched and a.gpus > 1
+    n_gpus = a.gpus if single_multi else world
+    wl = resolve(a, n_gpus)
+    n_atoms, n_total = wl["n_atoms"], wl["n_total"]
 
     # -- CPU baseline first: no process has touched the GPU yet ---------------
-    cpu = cpu_c3 = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        from oracle import cpu_baseline
-        cpu = cpu_baseline.run(n_atoms, a.cpu_frames, align="none")
-        if not a.no_modes and wl["align"] is None and not wl.get("host"):
-            from rmsf_amd.synth import motion_table as _mt  # numpy only: no GPU touched
-            cpu_c3 = cpu_baseline.run(n_atoms, max(1, a.cpu_frames // 4), align="frame0",
-                                      motion=_mt(1, per_gpu))
+    cpu_avg = cpu_flat = None
+    if rank == 0 and n_gpus == 1 and not a.no_cpu_baseline and not wl.get("host"):
+        cpu_avg, cpu_flat = cpu_baselines(a, wl)
+    cpu = None
+    if cpu_avg is not None:
+        cpu = dict(cpu_avg)
+        cpu["unaligned"] = cpu_flat  # the headline workload's own sweep (C2), second figure
+
+    if single_multi:
+        main_single_process(a, wl, cpu)
+        return
 
     import torch
     import torch.distributed as dist
@@ -206,12 +415,12 @@ def main():
         dist.barrier()
         torch.cuda.synchronize()
         del _t
-    n_total = per_gpu * world
     b0, b1 = parallel.blocks(n_total, world)[rank]
     n_local = b1 - b0
     motion = motion_table(1, n_total) if wl["align"] else None
     traj = generate(eng, n_atoms, b0, n_local, seed=0, motion=motion)
     torch.cuda.synchronize()
+    h2d_bytes = None
     if wl.get("host"):
         # C5: the frames live in (pageable) host memory and every step streams
         # them through the stager: host gather -> pinned slot -> H2D -> kernels
@@ -270,59 +479,49 @@ def main():
         return dt, timer, res
 
     dt, timer, res = timed(wl["align"], a.steps, a.warmup)
-    value = n_total * n_atoms * a.steps / dt
-    acc_ms = timer.ms("accumulate")
-    kern_s = sum(acc_ms) / len(acc_ms) / 1e3
-    bytes_launch = B_PER_ATOM_FRAME * n_atoms * n_local
-    achieved = bytes_launch / kern_s / 1e9
-    traffic = load_traffic(a.workload, n_atoms, n_local)
-    out = {
-        "metric": "atom-frames/sec (RMSF) + achieved HBM GB/s fraction",
-        "value": value,
-        "unit": "atom-frames/s",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": dt / a.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic: counter-based generator, fp32 frames resident in HBM (generated on device)",
-        "config": {"workload": wl["name"], "n_atoms": n_atoms, "n_frames_per_gpu": per_gpu,
-                   "n_frames_total": n_total, "selection": "all atoms", "align": wl["align"],
-                   "parallelism": f"frame-sharded x{world} (RMSF.py:65-69 blocks), RCCL Chan merge"},
-        "roofline": {"bound": "hbm", "kernel": ("k_accum_atoms" if wl["align"] else "k_welford_flat")
-                     + ("" if a.splits else "_sk"),
-                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic, "traffic_source": f"profiles/pmc_{a.workload}.json" if traffic else None,
-                     "algorithmic_bytes_per_launch": bytes_launch,
-                     "avg_launch_ms": kern_s * 1e3, "launches": len(acc_ms)},
-        "cpu_baseline": cpu,
-        # whole-step rate in algorithmic bytes (incl. merges, finalise, launch gaps)
-        "pipeline_hbm_gbs": B_PER_ATOM_FRAME * n_atoms * n_local * a.steps / dt / 1e9,
-    }
+    par = (f"frame-sharded x{world} (RMSF.py:65-69 blocks), one process per GPU, RCCL Chan merge" if world > 1
+           else "1 GPU")
+    out = base_line(a, wl, world, dt, par)
+    launches, acc_ms, acc_af = timer.totals("accumulate")
+    traffic = load_traffic(a.workload, n_atoms, n_local) if launches == a.steps else None
+    kname = ("k_accum_atoms" if wl["align"] else "k_welford_flat") + ("" if a.splits else "_sk")
+    out["roofline"] = roofline(kname, launches, acc_ms, acc_af, traffic,
+                               f"profiles/pmc_{a.workload}.json" if traffic else None)
+    out["cpu_baseline"] = cpu
+    # whole-step rate in algorithmic bytes (incl. merges, finalise, launch gaps)
+    out["pipeline_hbm_gbs"] = B_PER_ATOM_FRAME * n_atoms * n_local * a.steps / dt / 1e9
     if wl["align"]:
-        sup_ms = timer.ms("superpose")
-        if sup_ms:
-            s = sum(sup_ms) / len(sup_ms) / 1e3
-            out["superpose"] = {"avg_launch_ms": s * 1e3,
-                                "gflops": FLOP_PER_ATOM_FRAME_SUPERPOSE * n_atoms * n_local / s / 1e9,
+        k, s_ms, s_af = timer.totals("superpose")
+        if k:
+            out["superpose"] = {"launches": k, "avg_launch_ms": s_ms / k,
+                                "gflops": FLOP_PER_ATOM_FRAME_SUPERPOSE * s_af / (s_ms / 1e3) / 1e9,
                                 "fp64_peak_tflops_spec": FP64_PEAK_TFS,
-                                "hbm_gbs": B_PER_ATOM_FRAME * n_atoms * n_local / s / 1e9}
+                                "hbm_gbs": B_PER_ATOM_FRAME * s_af / (s_ms / 1e3) / 1e9}
 
-    # -- aligned modes at N=1 (reported beside the headline) ------------------
     if wl.get("host"):
-        out["stager"] = {"h2d_gbs": B_PER_ATOM_FRAME * n_atoms * n_local * a.steps / dt / 1e9,
+        # bytes that actually cross PCIe per step: the staged selection rows of
+        # a host array, or the compressed XTC records (GPU decode) / decoded
+        # selection rows (host decode)
+        sweeps = 2 if wl["align"] == "average" and not (a.host_cache or a.xtc_cache) else 1
+        decoded = B_PER_ATOM_FRAME * n_atoms * n_local
+        if wl.get("xtc") and a.xtc_decode == "gpu":
+            h2d_bytes = os.path.getsize(xtc_path) * sweeps
+        else:
+            h2d_bytes = decoded * sweeps
+        out["stager"] = {"h2d_bytes_per_step": h2d_bytes,
+                         "h2d_gbs": h2d_bytes * a.steps / dt / 1e9,
+                         "decoded_frame_gbs": decoded * a.steps / dt / 1e9,
                          "host_cache": bool(getattr(src, "cache", None) is not None),
                          "threads": a.stager_threads, "batch_frames": src.batch_frames,
                          "host_link_spec_gbs": 63.0}
         if wl.get("xtc"):
             out["stager"].update(xtc_decode=a.xtc_decode, xtc_cache=a.xtc_cache,
                                  xtc_bytes=os.path.getsize(xtc_path), xtc_write_s=t_w,
-                                 xtc_frames_per_s=n_local * a.steps / dt,
-                                 xtc_gb_per_s_compressed=os.path.getsize(xtc_path) * a.steps / dt / 1e9)
-        out["roofline"]["note"] = "C5 is PCIe/host bound; the kernel roofline above is the device-side launch"
+                                 xtc_frames_per_s=n_local * a.steps / dt)
+        out["data"] = "synthetic frames in host memory" + (" written to an XTC file" if wl.get("xtc") else "")
+        out["roofline"]["note"] = "C5 is PCIe/host bound; the kernel roofline above is the device-side launches"
+
+    # -- aligned modes at N=1 (reported beside the headline) ------------------
     if world == 1 and not a.no_modes and wl["align"] is None and not wl.get("host"):
         del traj, src
         torch.cuda.empty_cache()
@@ -334,21 +533,24 @@ def main():
         for name, align in (("c3_frame0", "frame0"), ("rmsf_py_average", "average")):
             mdt, mt, _ = timed(align, a.mode_steps, 1)
             sweeps = 2 if align == "average" else 1
-            sup = mt.ms("superpose")
-            acc = mt.ms("accumulate")
             af = n_total * n_atoms * a.mode_steps / mdt
+            k_s, s_ms, s_af = mt.totals("superpose")
+            k_a, a_ms, a_af = mt.totals("accumulate")
             modes[name] = {
                 "atom_frames_per_s": af,
                 "ms_per_step": mdt / a.mode_steps * 1e3,
                 "sweeps": sweeps,
                 "hbm_gbs_algorithmic": af * B_PER_ATOM_FRAME * sweeps / 1e9,
-                "superpose_avg_ms": sum(sup) / len(sup),
-                "superpose_gflops": FLOP_PER_ATOM_FRAME_SUPERPOSE * n_atoms * n_local / (sum(sup) / len(sup) / 1e3) / 1e9,
-                "accumulate_avg_ms": sum(acc) / len(acc),
-                "accumulate_hbm_gbs": B_PER_ATOM_FRAME * n_atoms * n_local / (sum(acc) / len(acc) / 1e3) / 1e9,
+                "superpose_avg_ms": s_ms / max(1, k_s),
+                "superpose_gflops": FLOP_PER_ATOM_FRAME_SUPERPOSE * s_af / (s_ms / 1e3) / 1e9,
+                "superpose_hbm_gbs": B_PER_ATOM_FRAME * s_af / (s_ms / 1e3) / 1e9,
+                "accumulate_avg_ms": a_ms / max(1, k_a),
+                "accumulate_hbm_gbs": B_PER_ATOM_FRAME * a_af / (a_ms / 1e3) / 1e9,
             }
-        if cpu_c3 is not None:
-            modes["c3_frame0"]["cpu_baseline"] = cpu_c3
+        if cpu is not None:
+            modes["rmsf_py_average"]["cpu_baseline"] = {
+                "value": cpu["value"], "cores": cpu["cores"], "sample": cpu["sample"],
+                "gpu_over_cpu": modes["rmsf_py_average"]["atom_frames_per_s"] / cpu["value"]}
         modes["c1_rmsf_py"] = c1_latency(eng, a.no_cpu_baseline)
         out["modes"] = modes
     if rank == 0:

@@ -354,6 +354,25 @@ int rmsf_ctx_synchronize(rmsf_ctx *ctx);
  * (>= 1) and gather threads.  Takes effect at the next host push.           */
 int rmsf_ctx_set_staging(rmsf_ctx *ctx, int64_t batch_frames, int n_slots,
                          int n_threads);
+/* Measurement: with timing on, every superpose and accumulate launch the
+ * context makes is bracketed by HIP events on its stream.
+ * rmsf_ctx_kernel_time() synchronises and returns, for one kernel family,
+ * the number of launches, their summed duration (ms) and the atom-frames
+ * they processed (x 12 B = algorithmic bytes), then clears
+ * that family's record.                                                      */
+#define RMSF_TIME_ACCUMULATE 0 /* rmsf_accumulate_balanced (RMSF.py:99-103,133-138) */
+#define RMSF_TIME_SUPERPOSE 1  /* rmsf_superpose (RMSF.py:94-97 + qcprot, :43-51)  */
+int rmsf_ctx_set_timing(rmsf_ctx *ctx, int on);
+int rmsf_ctx_kernel_time(rmsf_ctx *ctx, int which, int64_t *launches,
+                         double *ms, double *atom_frames);
+/* Per-frame QCP rmsd (the value RMSF.py:48 discards; AlignTraj's
+ * results.rmsd): with collection on, every RMSF_PUSH_ALIGN_WELFORD push
+ * appends its frames' rmsd, in push order, to a device list the context
+ * keeps (cleared by turning collection on and by rmsf_ctx_reset(what & 1)).
+ * rmsf_get_rmsd synchronises; *n = frames collected, h_rmsd (capacity
+ * doubles, may be NULL to query n) receives them.                          */
+int rmsf_ctx_collect_rmsd(rmsf_ctx *ctx, int on);
+int rmsf_get_rmsd(rmsf_ctx *ctx, int64_t *n, double *h_rmsd, int64_t capacity);
 /* Zero the running Welford (what & 1) and/or sweep-1 sum (what & 2) state. */
 int rmsf_ctx_reset(rmsf_ctx *ctx, int what);
 

@@ -165,6 +165,20 @@ struct rmsf_ctx {
   int stage_slots = 2, stage_threads = 4;
   bool stager_dirty = true;
   ncclComm_t comm = nullptr;
+  int comm_size = 0;  // ranks of `comm` (0 = none)
+  // measurement (rmsf_ctx_set_timing): HIP events around each superpose /
+  // accumulate launch on the context stream, with the atom-frames it covered
+  struct Span {
+    hipEvent_t a, b;
+    int which;  // RMSF_TIME_ACCUMULATE / RMSF_TIME_SUPERPOSE
+    int64_t atom_frames;
+  };
+  bool timing = false;
+  std::vector<Span> spans;
+  // per-frame QCP rmsd of the aligned Welford pushes (rmsf_ctx_collect_rmsd)
+  bool collect_rmsd = false;
+  DevBuf rmsd;
+  int64_t n_rmsd = 0;
 
   const int32_t *d_sel() const { return h_sel.empty() ? nullptr : static_cast<const int32_t *>(sel.p); }
   const double *d_masses() const { return has_masses ? masses.d() : nullptr; }
@@ -189,6 +203,36 @@ int zero_running(rmsf_ctx *c, Running &r, bool two) {
   return RMSF_OK;
 }
 
+// Brackets `launch` with timing events on the context stream when timing is on.
+template <class F>
+int timed(rmsf_ctx *c, int which, int64_t atom_frames, F &&launch) {
+  if (!c->timing) return launch();
+  rmsf_ctx::Span sp{nullptr, nullptr, which, atom_frames};
+  CX_HIP(hipEventCreate(&sp.a));
+  if (hipEventCreate(&sp.b) != hipSuccess) {
+    (void)hipEventDestroy(sp.a);
+    return fail(RMSF_EHIP, "hipEventCreate failed");
+  }
+  c->spans.push_back(sp);  // owned by the context from here on
+  CX_HIP(hipEventRecord(sp.a, c->stream));
+  CX_OK(launch());
+  CX_HIP(hipEventRecord(sp.b, c->stream));
+  return RMSF_OK;
+}
+
+void drop_spans(rmsf_ctx *c, int which) {
+  std::vector<rmsf_ctx::Span> keep;
+  for (auto &sp : c->spans) {
+    if (which < 0 || sp.which == which) {
+      (void)hipEventDestroy(sp.a);
+      (void)hipEventDestroy(sp.b);
+    } else {
+      keep.push_back(sp);
+    }
+  }
+  c->spans.swap(keep);
+}
+
 // one launch group over n_frames device frames: [superpose] + accumulate + fold
 int process(rmsf_ctx *c, const float *d_xyz, int64_t stride, int64_t n_frames, const int32_t *d_sel, int mode) {
   const bool aligned = mode == RMSF_PUSH_ALIGN_SUM || mode == RMSF_PUSH_ALIGN_WELFORD;
@@ -199,9 +243,19 @@ int process(rmsf_ctx *c, const float *d_xyz, int64_t stride, int64_t n_frames, c
     CX_OK(c->xform.ensure(sizeof(double) * RMSF_XFORM_DOUBLES * (size_t)n_frames, c->stream));
     const size_t wb = rmsf_superpose_workspace_bytes(c->n_sel, n_frames);
     CX_OK(c->work.ensure(std::max<size_t>(wb, 8), c->stream));
-    CX_OK(rmsf_superpose(d_xyz, stride, n_frames, c->n_sel, d_sel, c->d_masses(), c->ref.d(), c->refinfo.d(),
-                         c->xform.d(), c->work.p, c->work.bytes, c->stream));
+    CX_OK(timed(c, RMSF_TIME_SUPERPOSE, c->n_sel * n_frames, [&] {
+      return rmsf_superpose(d_xyz, stride, n_frames, c->n_sel, d_sel, c->d_masses(), c->ref.d(), c->refinfo.d(),
+                            c->xform.d(), c->work.p, c->work.bytes, c->stream);
+    }));
     xf = c->xform.d();
+  }
+  if (aligned && welford && c->collect_rmsd) {
+    // the rmsd RMSF.py:48 discards: element 12 of each frame's transform record
+    CX_OK(c->rmsd.ensure(sizeof(double) * (size_t)(c->n_rmsd + n_frames), c->stream, true));
+    CX_HIP(hipMemcpy2DAsync(c->rmsd.d() + c->n_rmsd, sizeof(double), c->xform.d() + 12,
+                            sizeof(double) * RMSF_XFORM_DOUBLES, sizeof(double), (size_t)n_frames,
+                            hipMemcpyDeviceToDevice, c->stream));
+    c->n_rmsd += n_frames;
   }
   Running &r = welford ? c->wel : c->sum;
   const int mode_k = welford ? RMSF_MODE_WELFORD : RMSF_MODE_SUM;
@@ -209,8 +263,11 @@ int process(rmsf_ctx *c, const float *d_xyz, int64_t stride, int64_t n_frames, c
   // frame order into the running slot 0
   const size_t wb = rmsf_accumulate_balanced_workspace_bytes(c->n_sel, n_frames, 0);
   CX_OK(c->accwork.ensure(std::max<size_t>(wb, 16), c->stream));
-  CX_OK(rmsf_accumulate_balanced(d_xyz, stride, n_frames, c->n_sel, d_sel, xf, aligned ? c->refinfo.d() : nullptr,
-                                 mode_k, 0, c->accwork.p, c->accwork.bytes, c->stream));
+  CX_OK(timed(c, RMSF_TIME_ACCUMULATE, c->n_sel * n_frames, [&] {
+    return rmsf_accumulate_balanced(d_xyz, stride, n_frames, c->n_sel, d_sel, xf,
+                                    aligned ? c->refinfo.d() : nullptr, mode_k, 0, c->accwork.p, c->accwork.bytes,
+                                    c->stream);
+  }));
   CX_OK(rmsf_fold_balanced(c->accwork.p, c->n_coord, mode_k, r.n, r.parts0.d(), welford ? r.parts1.d() : nullptr,
                            c->stream));
   r.n += n_frames;
@@ -242,7 +299,23 @@ int ensure_stager(rmsf_ctx *c) {
 // n local contexts (each buffer on its context's stream).
 using Reduce = std::function<int(int64_t, double *const *)>;
 
-int count_exchange(rmsf_ctx **cs, int n, const Reduce &red, const std::vector<int64_t> &local, int64_t *total) {
+// The contexts of this process are every rank of the exchange (RCCL
+// communicators of size n from rmsf_multi_init_all, or no communicator at
+// all): the frame counts are all known on the host, no device exchange needed.
+bool whole_group_here(rmsf_ctx *const *cs, int n) {
+  for (int i = 0; i < n; ++i)
+    if (cs[i]->comm ? cs[i]->comm_size != n : false) return false;
+  return true;
+}
+
+int count_exchange(rmsf_ctx **cs, int n, const Reduce &red, const std::vector<int64_t> &local, int64_t *total,
+                   bool host_counts) {
+  if (host_counts) {
+    int64_t t = 0;
+    for (int64_t v : local) t += v;
+    *total = t;
+    return RMSF_OK;
+  }
   std::vector<double *> bufs(n);
   for (int i = 0; i < n; ++i) {
     DeviceScope ds(cs[i]->dev);
@@ -266,7 +339,7 @@ int count_exchange(rmsf_ctx **cs, int n, const Reduce &red, const std::vector<in
   return RMSF_OK;
 }
 
-int exchange_sum(rmsf_ctx **cs, int n, const Reduce &red) {
+int exchange_sum(rmsf_ctx **cs, int n, const Reduce &red, bool host_counts) {
   std::vector<int64_t> local(n);
   for (int i = 0; i < n; ++i) {
     if (cs[i]->sum.parts0.bytes == 0) {
@@ -276,7 +349,7 @@ int exchange_sum(rmsf_ctx **cs, int n, const Reduce &red) {
     local[i] = cs[i]->sum.n;
   }
   int64_t total = 0;
-  CX_OK(count_exchange(cs, n, red, local, &total));
+  CX_OK(count_exchange(cs, n, red, local, &total, host_counts));
   std::vector<double *> bufs(n);
   for (int i = 0; i < n; ++i) bufs[i] = cs[i]->sum.parts0.d();
   CX_OK(red(cs[0]->n_coord, bufs.data()));
@@ -284,7 +357,7 @@ int exchange_sum(rmsf_ctx **cs, int n, const Reduce &red) {
   return RMSF_OK;
 }
 
-int exchange_chan(rmsf_ctx **cs, int n, const Reduce &red) {
+int exchange_chan(rmsf_ctx **cs, int n, const Reduce &red, bool host_counts) {
   std::vector<int64_t> local(n);
   for (int i = 0; i < n; ++i) {
     if (cs[i]->wel.parts0.bytes == 0) {
@@ -294,7 +367,7 @@ int exchange_chan(rmsf_ctx **cs, int n, const Reduce &red) {
     local[i] = cs[i]->wel.n;
   }
   int64_t total = 0;
-  CX_OK(count_exchange(cs, n, red, local, &total));
+  CX_OK(count_exchange(cs, n, red, local, &total, host_counts));
   if (total == 0) return fail(RMSF_EEMPTY, "rmsf chan merge: no frames on any rank (RMSF.py:39 ZeroDivisionError)");
   const int64_t nc = cs[0]->n_coord;
   std::vector<double *> a(n), b(n);
@@ -462,6 +535,7 @@ RMSF_EXPORT int rmsf_ctx_destroy(rmsf_ctx *c) {
     if (c->stager) rmsf_stager_destroy(c->stager);
     if (c->xdec) rmsf_xtcdec_destroy(c->xdec);
     if (c->comm && rccl().ok) rccl().CommDestroy(c->comm);
+    drop_spans(c, -1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;  // DevBufs free on the context's device
   }
@@ -492,9 +566,57 @@ RMSF_EXPORT int rmsf_ctx_set_staging(rmsf_ctx *c, int64_t batch_frames, int n_sl
   return RMSF_OK;
 }
 
+RMSF_EXPORT int rmsf_ctx_set_timing(rmsf_ctx *c, int on) {
+  CX_OK(check_ctx(c, "rmsf_ctx_set_timing"));
+  c->timing = on != 0;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_ctx_kernel_time(rmsf_ctx *c, int which, int64_t *launches, double *ms, double *atom_frames) {
+  CX_OK(check_ctx(c, "rmsf_ctx_kernel_time"));
+  if (which != RMSF_TIME_ACCUMULATE && which != RMSF_TIME_SUPERPOSE)
+    return fail(RMSF_EINVAL, "rmsf_ctx_kernel_time: bad kernel");
+  DeviceScope ds(c->dev);
+  CX_HIP(hipStreamSynchronize(c->stream));
+  int64_t k = 0;
+  double t = 0.0, af = 0.0;
+  for (auto &sp : c->spans) {
+    if (sp.which != which) continue;
+    float e = 0.f;
+    CX_HIP(hipEventElapsedTime(&e, sp.a, sp.b));
+    ++k;
+    t += e;
+    af += (double)sp.atom_frames;
+  }
+  drop_spans(c, which);
+  if (launches) *launches = k;
+  if (ms) *ms = t;
+  if (atom_frames) *atom_frames = af;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_ctx_collect_rmsd(rmsf_ctx *c, int on) {
+  CX_OK(check_ctx(c, "rmsf_ctx_collect_rmsd"));
+  c->collect_rmsd = on != 0;
+  c->n_rmsd = 0;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_get_rmsd(rmsf_ctx *c, int64_t *n, double *h_rmsd, int64_t capacity) {
+  CX_OK(check_ctx(c, "rmsf_get_rmsd"));
+  if (n) *n = c->n_rmsd;
+  if (!h_rmsd || c->n_rmsd == 0) return RMSF_OK;
+  if (capacity < c->n_rmsd) return fail(RMSF_EINVAL, "rmsf_get_rmsd: output holds fewer than n frames");
+  DeviceScope ds(c->dev);
+  CX_HIP(hipMemcpyAsync(h_rmsd, c->rmsd.p, sizeof(double) * c->n_rmsd, hipMemcpyDeviceToHost, c->stream));
+  CX_HIP(hipStreamSynchronize(c->stream));
+  return RMSF_OK;
+}
+
 RMSF_EXPORT int rmsf_ctx_reset(rmsf_ctx *c, int what) {
   CX_OK(check_ctx(c, "rmsf_ctx_reset"));
   DeviceScope ds(c->dev);
+  if (what & 1) c->n_rmsd = 0;
   if (what & 1) CX_OK(zero_running(c, c->wel, true));
   if (what & 2) CX_OK(zero_running(c, c->sum, false));
   return RMSF_OK;
@@ -691,13 +813,13 @@ RMSF_EXPORT int rmsf_set_partial(rmsf_ctx *c, int64_t n, const double *h_mean, c
 RMSF_EXPORT int rmsf_ctx_allreduce_sum(rmsf_ctx *c, rmsf_allreduce_fn fn, void *user) {
   CX_OK(check_ctx(c, "rmsf_ctx_allreduce_sum"));
   if (!fn) return fail(RMSF_EINVAL, "rmsf_ctx_allreduce_sum: NULL callback");
-  return exchange_sum(&c, 1, callback_reduce(c, fn, user));
+  return exchange_sum(&c, 1, callback_reduce(c, fn, user), false);
 }
 
 RMSF_EXPORT int rmsf_ctx_chan_merge(rmsf_ctx *c, rmsf_allreduce_fn fn, void *user) {
   CX_OK(check_ctx(c, "rmsf_ctx_chan_merge"));
   if (!fn) return fail(RMSF_EINVAL, "rmsf_ctx_chan_merge: NULL callback");
-  return exchange_chan(&c, 1, callback_reduce(c, fn, user));
+  return exchange_chan(&c, 1, callback_reduce(c, fn, user), false);
 }
 
 RMSF_EXPORT int rmsf_multi_unique_id(void *id_out) {
@@ -726,6 +848,7 @@ RMSF_EXPORT int rmsf_multi_init(rmsf_ctx *c, const void *id, int nranks, int ran
     c->comm = nullptr;
     return nccl_fail("ncclCommInitRank", e);
   }
+  c->comm_size = nranks;
   return RMSF_OK;
 }
 
@@ -742,20 +865,23 @@ RMSF_EXPORT int rmsf_multi_init_all(rmsf_ctx **cs, int n) {
   std::vector<ncclComm_t> comms(n, nullptr);
   ncclResult_t e = r.CommInitAll(comms.data(), n, devs.data());
   if (e != ncclSuccess) return nccl_fail("ncclCommInitAll", e);
-  for (int i = 0; i < n; ++i) cs[i]->comm = comms[i];
+  for (int i = 0; i < n; ++i) {
+    cs[i]->comm = comms[i];
+    cs[i]->comm_size = n;
+  }
   return RMSF_OK;
 }
 
 RMSF_EXPORT int rmsf_multi_allreduce_sum(rmsf_ctx **cs, int n) {
   Reduce red;
   CX_OK(multi_reduce(cs, n, "rmsf_multi_allreduce_sum", &red));
-  return exchange_sum(cs, n, red);
+  return exchange_sum(cs, n, red, whole_group_here(cs, n));
 }
 
 RMSF_EXPORT int rmsf_multi_chan_merge(rmsf_ctx **cs, int n) {
   Reduce red;
   CX_OK(multi_reduce(cs, n, "rmsf_multi_chan_merge", &red));
-  return exchange_chan(cs, n, red);
+  return exchange_chan(cs, n, red, whole_group_here(cs, n));
 }
 
 }  // extern "C"

@@ -218,10 +218,14 @@ __device__ __forceinline__ void apply_xform(float &x, float &y, float &z, const 
   const float p1 = (float)((double)y - t[10]);
   const float p2 = (float)((double)z - t[11]);
   const double d0 = p0, d1 = p1, d2 = p2;
-  // out_b = sum_a p_a R[a][b]   (np.dot(positions, R), R row-major)
-  const float r0 = (float)(d0 * t[0] + d1 * t[3] + d2 * t[6]);
-  const float r1 = (float)(d0 * t[1] + d1 * t[4] + d2 * t[7]);
-  const float r2 = (float)(d0 * t[2] + d1 * t[5] + d2 * t[8]);
+  // out_b = sum_a p_a R[a][b]   (np.dot(positions, R), R row-major), as the
+  // host BLAS dgemm accumulates it: an FMA chain over a = 0, 1, 2 from
+  // p_0 R[0][b] (tests/test_rotation_rounding.py: numpy's dot equals this
+  // chain bit for bit, the unfused sum in only 60-75 % of values).  Explicit fma,
+  // so the rounding order does not depend on -ffp-contract.
+  const float r0 = (float)__builtin_fma(d2, t[6], __builtin_fma(d1, t[3], d0 * t[0]));
+  const float r1 = (float)__builtin_fma(d2, t[7], __builtin_fma(d1, t[4], d0 * t[1]));
+  const float r2 = (float)__builtin_fma(d2, t[8], __builtin_fma(d1, t[5], d0 * t[2]));
   x = (float)((double)r0 + rc0);
   y = (float)((double)r1 + rc1);
   z = (float)((double)r2 + rc2);

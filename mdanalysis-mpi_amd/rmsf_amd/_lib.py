@@ -99,6 +99,10 @@ SIGNATURES = {
     "rmsf_ctx_synchronize": (c_int, [P]),
     "rmsf_ctx_set_staging": (c_int, [P, c_int64, c_int, c_int]),
     "rmsf_ctx_reset": (c_int, [P, c_int]),
+    "rmsf_ctx_set_timing": (c_int, [P, c_int]),
+    "rmsf_ctx_collect_rmsd": (c_int, [P, c_int]),
+    "rmsf_get_rmsd": (c_int, [P, POINTER(c_int64), P, c_int64]),
+    "rmsf_ctx_kernel_time": (c_int, [P, c_int, POINTER(c_int64), POINTER(c_double), POINTER(c_double)]),
     "rmsf_set_reference": (c_int, [P, P, P]),
     "rmsf_set_reference_frame": (c_int, [P, P, c_int]),
     "rmsf_set_reference_average": (c_int, [P]),
@@ -122,6 +126,7 @@ SIGNATURES = {
 ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int64, c_void_p, c_void_p)
 RMSF_PUSH_WELFORD, RMSF_PUSH_ALIGN_SUM, RMSF_PUSH_ALIGN_WELFORD, RMSF_PUSH_SUM = 0, 1, 2, 3
 RMSF_UNIQUE_ID_BYTES = 128
+RMSF_TIME_ACCUMULATE, RMSF_TIME_SUPERPOSE = 0, 1
 
 _lib = None
 

@@ -28,7 +28,7 @@ import ctypes
 import numpy as np
 
 from ._lib import (ALLREDUCE_FN, RMSF_PUSH_ALIGN_SUM, RMSF_PUSH_ALIGN_WELFORD, RMSF_PUSH_SUM, RMSF_PUSH_WELFORD,
-                   RMSF_UNIQUE_ID_BYTES, call, load)
+                   RMSF_TIME_ACCUMULATE, RMSF_TIME_SUPERPOSE, RMSF_UNIQUE_ID_BYTES, call, load)
 
 PUSH_WELFORD = RMSF_PUSH_WELFORD
 PUSH_ALIGN_SUM = RMSF_PUSH_ALIGN_SUM
@@ -123,6 +123,30 @@ class Context:
 
     def set_staging(self, batch_frames: int = 0, n_slots: int = 2, n_threads: int = 4) -> None:
         call("rmsf_ctx_set_staging", self._h, batch_frames, n_slots, n_threads)
+
+    def set_timing(self, on: bool = True) -> None:
+        """HIP events around every superpose / accumulate launch (measurement)."""
+        call("rmsf_ctx_set_timing", self._h, 1 if on else 0)
+
+    def kernel_time(self, which: str = "accumulate") -> tuple[int, float, float]:
+        """(launches, summed ms, atom-frames) of one kernel family since the
+        last call (``which``: "accumulate" or "superpose"); synchronises."""
+        k = {"accumulate": RMSF_TIME_ACCUMULATE, "superpose": RMSF_TIME_SUPERPOSE}[which]
+        n, ms, af = ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
+        call("rmsf_ctx_kernel_time", self._h, k, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(af))
+        return n.value, ms.value, af.value
+
+    def collect_rmsd(self, on: bool = True) -> None:
+        """Keep the per-frame QCP rmsd of aligned Welford pushes (RMSF.py:48)."""
+        call("rmsf_ctx_collect_rmsd", self._h, 1 if on else 0)
+
+    def rmsd(self) -> np.ndarray:
+        n = ctypes.c_int64()
+        call("rmsf_get_rmsd", self._h, ctypes.byref(n), None, 0)
+        out = np.empty(n.value)
+        if n.value:
+            call("rmsf_get_rmsd", self._h, ctypes.byref(n), out.ctypes.data, out.size)
+        return out
 
     def reset(self, welford: bool = True, sum: bool = True) -> None:  # noqa: A002
         call("rmsf_ctx_reset", self._h, (1 if welford else 0) | (2 if sum else 0))

@@ -122,6 +122,118 @@ class _XtcFrames:
             ctx.push_xtc(self.xtc, rows.start, rows[-1] + 1, rows.step, mode)
 
 
+class _DcdFrames:
+    """A CHARMM/NAMD DCD file: each context reads only its block's runs from
+    the memory-mapped file (``DCDFile.read`` of the selected rows), in
+    batches, and pushes them through its stager -- host memory stays bounded
+    by a batch, as for the single-device ``DcdSource``."""
+
+    def __init__(self, path: str, sel, batch_frames: int | None):
+        from .dcd import DCDFile
+
+        self.f = DCDFile(path)
+        self.n_traj, n_atoms = len(self.f), self.f.n_atoms
+        self.rsel = None if sel is None else np.ascontiguousarray(sel, dtype=np.int64)
+        if self.rsel is not None and self.rsel.size and (self.rsel.min() < 0 or self.rsel.max() >= n_atoms):
+            raise IndexError("selection index out of range")
+        # the reads apply the selection: contexts see selected rows only
+        self.n_atoms = n_atoms if self.rsel is None else len(self.rsel)
+        self.sel = None
+        self.batch = batch_frames or max(1, min(4096, (64 << 20) // max(1, 12 * self.n_atoms)))
+
+    def reference(self, frame: int) -> np.ndarray:
+        return self.f.read(frame, 1, 1, self.rsel)[0]
+
+    def n_sel(self) -> int:
+        return self.n_atoms
+
+    def push(self, ctx: Context, rows: range, mode: int) -> None:
+        for i in range(0, len(rows), self.batch):
+            part = rows[i:i + self.batch]
+            ctx.push(self.f.read(part.start, len(part), part.step, self.rsel), mode)
+
+    def stage_block(self, dev: int, runs: list):
+        """The block's rows read batch by batch and staged into HBM once."""
+        import torch
+
+        from .sources import FrameCache, Stager
+
+        total = sum(len(r) for r in runs)
+        if not total:
+            return None
+        ns = self.n_atoms
+        with torch.cuda.device(dev):
+            cache = FrameCache(total, ns, device=torch.device("cuda", dev))
+            st = Stager(ns, ns, None, self.batch, 3, 1)
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            try:
+                row = 0
+                for rows in runs:
+                    for i in range(0, len(rows), self.batch):
+                        part = rows[i:i + self.batch]
+                        buf = self.f.read(part.start, len(part), part.step, self.rsel)
+                        slot, ptr = st.stage_compact(buf, len(part), stream)
+                        cache.fill(row, 1, len(part), ptr, stream)
+                        st.release(slot, stream)
+                        row += len(part)
+                torch.cuda.current_stream(dev).synchronize()
+            finally:
+                st.close()
+        return cache.buf
+
+
+class _DeviceShards:
+    """An HBM-resident trajectory held as one float32 [F_i, n_atoms, 3] torch
+    tensor per device; concatenated in the given order they are the
+    trajectory.  Each device's context processes the frames of the frame
+    list that lie in its own shard ("owner computes": no frame crosses
+    xGMI), and the exchanges merge them as they merge RMSF.py's blocks."""
+
+    def __init__(self, tensors, sel):
+        import torch
+
+        self.parts = list(tensors)
+        if not self.parts:
+            raise ValueError("no device shards")
+        for t in self.parts:
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32 and t.dim() == 3
+                    and t.shape[2] == 3 and t.is_contiguous()):
+                raise TypeError("device shards must be contiguous float32 HIP tensors [n_frames, n_atoms, 3]")
+        self.n_atoms = self.parts[0].shape[1]
+        if any(t.shape[1] != self.n_atoms for t in self.parts):
+            raise ValueError("device shards differ in their atom count")
+        self.devices = [t.device.index for t in self.parts]
+        self.offsets = np.concatenate([[0], np.cumsum([t.shape[0] for t in self.parts])]).astype(np.int64)
+        self.n_traj = int(self.offsets[-1])
+        self.sel = None if sel is None else np.ascontiguousarray(sel, dtype=np.int64)
+        if self.sel is not None and self.sel.size and (self.sel.min() < 0 or self.sel.max() >= self.n_atoms):
+            raise IndexError("selection index out of range")
+
+    def reference(self, frame: int):
+        i = int(np.searchsorted(self.offsets, frame, side="right") - 1)
+        return self.parts[i][frame - int(self.offsets[i])]
+
+    def owner_blocks(self, fl: FrameList) -> list[tuple[int, int]]:
+        """Positions [p0, p1) of the frame list inside each shard."""
+        pos = np.array([fl[i] for i in range(len(fl))], dtype=np.int64) if fl.r is None else None
+        out = []
+        for i in range(len(self.parts)):
+            lo, hi = int(self.offsets[i]), int(self.offsets[i + 1])
+            if pos is None:
+                r = fl.r
+                p0 = len(range(r.start, lo, r.step)) if lo > r.start else 0
+                p1 = len(range(r.start, hi, r.step)) if hi > r.start else 0
+                out.append((min(p0, len(r)), min(p1, len(r))))
+            else:
+                out.append((int(np.searchsorted(pos, lo)), int(np.searchsorted(pos, hi))))
+        return out
+
+    def push_on(self, i: int, ctx: Context, rows: range, mode: int) -> None:
+        if len(rows):
+            off = int(self.offsets[i])
+            ctx.push(self.parts[i][rows.start - off:rows[-1] - off + 1], mode, step=rows.step)
+
+
 class _AtomGroupFrames:
     """An MDAnalysis AtomGroup: ``ag.positions`` per Timestep (RMSF.py:95,128),
     gathered on this thread (readers are not thread-safe) in batches."""
@@ -166,32 +278,34 @@ def _frames_of(inp, sel, batch_frames):
 
     if isinstance(inp, np.ndarray):
         return _HostFrames(inp, sel)
+    if isinstance(inp, (list, tuple)) or (hasattr(inp, "is_cuda") and inp.is_cuda):
+        return _DeviceShards([inp] if hasattr(inp, "is_cuda") else inp, sel)
     if isinstance(inp, (str, bytes)) or hasattr(inp, "__fspath__"):
         path = os.fspath(inp)
         if str(path).lower().endswith(".xtc"):
             return _XtcFrames(path, sel)
         if str(path).lower().endswith(".dcd"):
-            from .dcd import DCDFile
-
-            with DCDFile(path) as f:
-                return _HostFrames(f.read(sel=sel), None)
+            return _DcdFrames(path, sel, batch_frames)
         raise ValueError(f"only .xtc and .dcd trajectory files are read natively, got {path!r}")
     if hasattr(inp, "universe") and hasattr(inp, "positions"):
         return _AtomGroupFrames(inp, batch_frames)
-    raise TypeError(f"gpus=: unsupported input {type(inp)!r} (numpy array, .xtc/.dcd path or AtomGroup; "
-                    "an HBM tensor lives on one device -- use torch.distributed, one process per GPU)")
+    raise TypeError(f"gpus=: unsupported input {type(inp)!r} (numpy array, .xtc/.dcd path, AtomGroup, or HIP "
+                    "tensors -- one shard per device)")
 
 
 def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int = 0, start=None, stop=None,
-              step=None, batch_frames: int | None = None, frames=None) -> dict:
+              step=None, batch_frames: int | None = None, frames=None, collect_rmsd: bool = False) -> dict:
     """RMSF.py's computation over the devices ``gpus`` from one process.
-    Returns the ``results`` fields (rmsf, mean, sumsquares, n_frames, ...)."""
+    Returns the ``results`` fields (rmsf, mean, sumsquares, n_frames, ...;
+    ``rmsd`` with ``collect_rmsd``: per-frame QCP rmsd of the last sweep in
+    frame-list order, the by-product RMSF.py:48 discards)."""
     if align not in (None, "frame0", "average"):
         raise ValueError(f"align must be one of (None, 'frame0', 'average'), got {align!r}")
     if parallel.world()[1] > 1:
         raise ValueError("gpus= drives several devices from one process; under torch.distributed "
                          "(one process per GPU) leave it unset")
-    devs = device_list(gpus)
+    if collect_rmsd and align is None:
+        raise ValueError("collect_rmsd needs an aligned run (align='frame0' or 'average')")
     src = _frames_of(inp, select, batch_frames)
     fl = FrameList(src.n_traj, start, stop, step, frames=frames)
     if len(fl) == 0:
@@ -200,14 +314,25 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
         raise IndexError(f"ref_frame {ref_frame} outside the trajectory ({src.n_traj} frames)")
     if masses is None and align is not None and isinstance(src, _AtomGroupFrames):
         masses = np.asarray(src.ag.masses, dtype=np.float64)
-    # RMSF.py's two sweeps over a host array: each device stages its block's
+    big = max(1, len(fl))
+    if isinstance(src, _DeviceShards):
+        # the data decide the placement: device i takes the frames in its shard
+        devs = src.devices
+        if gpus is not None and not isinstance(gpus, (int, np.integer)) and device_list(gpus) != devs:
+            raise ValueError(f"gpus={list(gpus)} does not match the shards' devices {devs}")
+        if isinstance(gpus, (int, np.integer)) and int(gpus) != len(devs):
+            raise ValueError(f"gpus={gpus} but {len(devs)} device shards were given")
+        spans = src.owner_blocks(fl)
+    else:
+        devs = device_list(gpus)
+        spans = parallel.blocks(len(fl), len(devs))   # RMSF.py:65-69 over the frame list
+    # each device's block of the frame list, as strided runs
+    blocks = [[range(f, f + s * n, s) for f, s, n in fl.runs(b0, b1, big)] for b0, b1 in spans]
+    # RMSF.py's two sweeps over host frames: each device stages its block's
     # selected rows into HBM once and both sweeps read them there (contexts
     # over the selection only: the in-kernel gather becomes the identity)
-    # each device's RMSF.py:65-69 block of the frame list, as strided runs
-    big = max(1, len(fl))
-    blocks = [[range(f, f + s * n, s) for f, s, n in fl.runs(b0, b1, big)]
-              for b0, b1 in parallel.blocks(len(fl), len(devs))]
-    staged = align == "average" and isinstance(src, _HostFrames) and _blocks_fit(devs, blocks, src.n_sel())
+    staged = (align == "average" and isinstance(src, (_HostFrames, _DcdFrames))
+              and _blocks_fit(devs, blocks, src.n_sel()))
     if staged:
         ctxs = [Context(src.n_sel(), sel=None, masses=masses, device=d) for d in devs]
     else:
@@ -215,48 +340,64 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
     try:
         if len(set(devs)) == len(devs) and len(devs) > 1:
             Context.init_all(ctxs)  # ncclCommInitAll: one communicator per device
+        if collect_rmsd:
+            for c in ctxs:
+                c.collect_rmsd(True)
 
         def each(fn):
             if getattr(src, "serial", False) or len(ctxs) == 1:
-                for c, r in zip(ctxs, blocks):
-                    fn(c, r)
+                for i in range(len(ctxs)):
+                    fn(i)
                 return
             with ThreadPoolExecutor(len(ctxs)) as ex:
-                for f in [ex.submit(fn, c, r) for c, r in zip(ctxs, blocks)]:
+                for f in [ex.submit(fn, i) for i in range(len(ctxs))]:
                     f.result()
 
         out = {}
         if align is not None:
             ref = src.reference(ref_frame)
-            if staged and src.sel is not None:
+            if staged and getattr(src, "sel", None) is not None:
                 ref = ref[src.sel]
             for c in ctxs:  # every rank reads the reference frame (RMSF.py:80-87)
-                c.set_reference_frame(ref)
+                if hasattr(ref, "is_cuda") and ref.device.index != c.device:
+                    import torch
+                    c.set_reference_frame(ref.to(torch.device("cuda", c.device)))  # one frame over xGMI
+                else:
+                    c.set_reference_frame(ref)
         cached = {}
         if staged:
-            def stage(c, r):
-                cached[id(c)] = src.stage_block(c.device, r)
+            def stage(i):
+                cached[i] = src.stage_block(ctxs[i].device, blocks[i])
             each(stage)
 
-        def push(c, runs, mode):
+        def push(i, mode):
+            c = ctxs[i]
             if staged:
-                if cached[id(c)] is not None:
-                    c.push(cached[id(c)], mode)
+                if cached[i] is not None:
+                    c.push(cached[i], mode)
+            elif isinstance(src, _DeviceShards):
+                for r in blocks[i]:
+                    src.push_on(i, c, r, mode)
             else:
-                for r in runs:
+                for r in blocks[i]:
                     src.push(c, r, mode)
 
         if align == "average":
-            each(lambda c, r: push(c, r, PUSH_ALIGN_SUM))
+            each(lambda i: push(i, PUSH_ALIGN_SUM))
             Context.multi_allreduce_sum(ctxs)
             for c in ctxs:
                 c.set_reference_average()
             out["average"] = ctxs[0].average().reshape(-1)  # flat, as the pipeline returns it
-        each(lambda c, r: push(c, r, PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD))
+        if collect_rmsd:
+            for c in ctxs:  # the last sweep's rmsd only, as the pipeline reports it
+                c.collect_rmsd(True)
+        each(lambda i: push(i, PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD))
         Context.multi_chan_merge(ctxs)
         n, mean, m2 = ctxs[0].partial()
         out.update(rmsf=ctxs[0].rmsf(), mean=mean, sumsquares=m2, n_frames=n,
-                   blocks=[(b0, b1) for b0, b1 in parallel.blocks(len(fl), len(devs))], devices=devs)
+                   blocks=[(int(b0), int(b1)) for b0, b1 in spans], devices=devs)
+        if collect_rmsd:
+            out["rmsd"] = np.concatenate([c.rmsd() for c in ctxs])
         return out
     finally:
         for c in ctxs:

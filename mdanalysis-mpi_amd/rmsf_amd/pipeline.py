@@ -31,34 +31,41 @@ ALIGN_MODES = (None, "frame0", "average")
 
 class KernelTimer:
     """HIP-event spans recorded on the launching (current) stream around the
-    ABI calls of the pipeline -- used by bench.py for the per-kernel roofline."""
+    ABI calls of the pipeline -- used by bench.py for the per-kernel roofline.
+    Each span also records the atom-frames its launch processed, so a rate
+    is sum(work) / sum(time) over launches of any size."""
 
     def __init__(self):
         self.spans = defaultdict(list)
 
     @contextlib.contextmanager
-    def span(self, name: str):
+    def span(self, name: str, atom_frames: int = 0):
         s = torch.cuda.current_stream()
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
         a.record(s)
         yield
         b.record(s)
-        self.spans[name].append((a, b))
+        self.spans[name].append((a, b, int(atom_frames)))
 
     def clear(self) -> None:
         self.spans.clear()
 
     def ms(self, name: str) -> list[float]:
         torch.cuda.synchronize()
-        return [a.elapsed_time(b) for a, b in self.spans.get(name, [])]
+        return [a.elapsed_time(b) for a, b, _ in self.spans.get(name, [])]
+
+    def totals(self, name: str) -> tuple[int, float, int]:
+        """(launches, summed ms, summed atom-frames) of ``name``."""
+        t = self.ms(name)
+        return len(t), float(sum(t)), sum(af for _, _, af in self.spans.get(name, []))
 
 
 _NULL = contextlib.nullcontext()
 
 
-def _span(timer, name):
-    return timer.span(name) if timer is not None else _NULL
+def _span(timer, name, atom_frames: int = 0):
+    return timer.span(name, atom_frames) if timer is not None else _NULL
 
 
 class Accumulator:
@@ -104,14 +111,14 @@ class Accumulator:
             need = eng.balanced_workspace_bytes(self.n_sel, b.n_frames)
             if need > self.work.numel() * 8:  # the bound is not monotone in the batch size
                 self.work = eng.empty((need + 7) // 8)
-            with _span(self.timer, "accumulate"):
+            with _span(self.timer, "accumulate", b.n_frames * self.n_sel):
                 eng.accumulate_balanced(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, xform, refinfo, self.mode,
                                         self.work)
             eng.fold_balanced(self.work, self.n_coord, self.mode, self.n, self.parts0[0], p1)
             self.n += b.n_frames
             return
         s = max(self.fixed_splits, -(-b.n_frames // RMSF_MAX_SPLIT_FRAMES))
-        with _span(self.timer, "accumulate"):
+        with _span(self.timer, "accumulate", b.n_frames * self.n_sel):
             eng.accumulate(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, xform, refinfo, self.mode, s,
                            self.parts0[1:], None if self.parts1 is None else self.parts1[1:])
         if self.mode == RMSF_MODE_WELFORD:
@@ -142,7 +149,7 @@ class Superposer:
 
     def run(self, b: Batch, ref: torch.Tensor, refinfo: torch.Tensor) -> torch.Tensor:
         xf = self.xform[: b.n_frames]
-        with _span(self.timer, "superpose"):
+        with _span(self.timer, "superpose", b.n_frames * self.n_sel):
             self.eng.superpose(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, self.masses, ref, refinfo, xf,
                                self.work)
         return xf

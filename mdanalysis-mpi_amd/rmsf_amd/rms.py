@@ -67,7 +67,10 @@ class RMSF:
         Drive this many devices (or these device ids) from one process: each
         takes the RMSF.py:65-69 block of its index and the blocks merge over
         RCCL (``ncclCommInitAll``).  Inputs: host array, ``.xtc``/``.dcd``
-        path or AtomGroup.  Leave unset under ``torch.distributed``.
+        path, AtomGroup, or HBM-resident shards -- a list of float32 HIP
+        tensors, one per device, whose concatenation is the trajectory (each
+        device then takes the frames it holds).  Leave unset under
+        ``torch.distributed``.
     """
 
     def __init__(self, atomgroup, *, select=None, align=None, masses=None, ref_frame: int = 0,
@@ -89,8 +92,8 @@ class RMSF:
 
     # MDAnalysis AnalysisBase compatible signature
     def run(self, start=None, stop=None, step=None, frames=None, verbose=None, **kwargs):
-        if self.gpus is not None:
-            return self._run_multi(start, stop, step, frames)
+        if self.gpus is not None or isinstance(self._input, (list, tuple)):
+            return self._run_multi(start, stop, step, frames)  # several devices, or HBM shards per device
         eng = Engine(self.device)
         # torch's current device = the engine's, so the buffers sources and
         # caches allocate live on the device the kernels run on
@@ -126,11 +129,9 @@ class RMSF:
         (rmsf_amd.multi)."""
         from .multi import run_multi
 
-        if self.collect_rmsd:
-            raise NotImplementedError("collect_rmsd is not available with gpus=; use torch.distributed ranks")
         out = run_multi(self._input, self.gpus, select=self.select, align=self.align, masses=self.masses,
                         ref_frame=self.ref_frame, start=start, stop=stop, step=step,
-                        batch_frames=self.batch_frames, frames=frames)
+                        batch_frames=self.batch_frames, frames=frames, collect_rmsd=self.collect_rmsd)
         r = self.results
         r.update(out)
         r.m2 = r.sumsquares

@@ -106,6 +106,11 @@ class FrameList:
             if start is not None or stop is not None or step is not None:
                 raise ValueError("start/stop/step cannot be combined with frames")
             f = np.asarray(frames)
+            if f.size == 0:
+                f = f.astype(np.int64)
+            elif f.dtype != bool and not np.issubdtype(f.dtype, np.integer):
+                # AnalysisBase.run(frames=...) indexes with them: 1.7 is not a frame
+                raise TypeError(f"frames must be integer indices or a boolean mask, got dtype {f.dtype}")
             if f.dtype == bool:
                 if f.shape != (n_traj,):
                     raise ValueError(f"boolean frames must have one entry per frame ({n_traj})")
@@ -194,9 +199,25 @@ class DeviceSource:
     def reference(self, frame: int, stream: int) -> Batch:
         return Batch(self._ptr(frame), self.fstride, 1, self.sel_dev)
 
+    @property
+    def n_rows(self) -> int:
+        return self.traj.shape[0]
+
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
         for first, step, n in frames.runs(b0, b1, max_frames):
+            _check_run(self, first, step, n, "HBM shard")
             yield Batch(self._ptr(first), self.fstride * step, n, self.sel_dev)
+
+
+def _check_run(src, first: int, step: int, n: int, what: str) -> None:
+    """A run reads frames first, first+step, ..., first+step*(n-1): a sharded
+    source must hold the last one too, or the kernels / the stager would read
+    past the shard (runs are arithmetic, so first and last bound them all)."""
+    for f in (first, first + step * (n - 1)):
+        if not src.holds(f):
+            lo = getattr(src, "offset", 0)
+            raise IndexError(f"frame {f} is outside this {what} (frames [{lo}, {lo + src.n_rows})): the rank's "
+                             "block of the frame list must lie inside the frames it holds")
 
 
 class FrameCache:
@@ -308,7 +329,12 @@ class HostSource:
 
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
         for first, step, n in frames.runs(b0, b1, min(max_frames, self.batch_frames)):
+            _check_run(self, first, step, n, "host shard")
             yield self._stage(self._row(first), step, n, stream)
+
+    @property
+    def n_rows(self) -> int:
+        return self.traj.shape[0]
 
 
 class XtcDecoder:

@@ -1,20 +1,33 @@
 """bench.py's ``cpu_baseline`` leg -- BENCH/TEST INFRASTRUCTURE ONLY.
 
-Times the oracle's numpy restatement of RMSF.py's per-rank loop on the host
-cores, the way ``mpirun -n P python RMSF.py`` would run it: P independent
-processes, one BLAS/OMP thread each (RMSF.py:23-25), each owning one
-contiguous frame block (RMSF.py:65-69) of the same synthetic workload, then
-the Chan fold of the P partials (RMSF.py:143).  Frames are generated before
-the timed loop (RMSF.py re-decodes an XTC instead, so this baseline is
-optimistic: no decode and no per-frame re-selection).
+Times the oracle's numpy restatement of RMSF.py on the host cores, the way
+``mpirun -n P python RMSF.py`` runs it: P independent processes, one
+BLAS/OMP thread each (RMSF.py:23-25), each owning one contiguous frame block
+(RMSF.py:65-69) of the same synthetic workload.
 
-Run as ``python -m oracle.cpu_baseline --worker ...`` (one process per
-core, started with subprocess -- never fork()ed from a GPU process).
+  align="average"  RMSF.py itself: sweep 1 (align to frame 0 + f64 sum,
+                   RMSF.py:89-105) in every process; the parent sums the
+                   per-process sums and writes the average (the Allreduce of
+                   RMSF.py:107-111) while the workers wait; sweep 2 (align to
+                   the average + Welford, RMSF.py:113-140); the parent's Chan
+                   fold of the partials (RMSF.py:141-143) and finalise (:146).
+  align="frame0"   one aligned Welford sweep against frame 0 (config C3).
+  align="none"     the bare Welford sweep (config C2).
+
+P defaults to the host cores this process may actually use: its CPU
+affinity, capped by the cgroup CPU quota (a 16-CPU quota on a 256-CPU
+affinity mask gives 16 -- more processes than that would only time-slice).
+Frames are generated before the timed loops (RMSF.py re-decodes an XTC
+instead, so this baseline is optimistic: no decode, no per-frame
+re-selection).  Run as ``python -m oracle.cpu_baseline --worker ...`` (one
+process per core, started with subprocess -- never fork()ed from a GPU
+process).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import subprocess
 import sys
@@ -24,6 +37,31 @@ import time
 _ENV1 = {"MKL_NUM_THREADS": "1", "NUMEXPR_NUM_THREADS": "1", "OMP_NUM_THREADS": "1", "OPENBLAS_NUM_THREADS": "1"}
 
 
+def cgroup_cpu_quota() -> int | None:
+    """CPUs' worth of time the cgroup grants (cgroup v2 ``cpu.max`` or v1
+    ``cfs_quota_us``), rounded up; None when unlimited or unknown."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, math.ceil(int(q) / int(p)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return max(1, math.ceil(q / p)) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
+def available_cores() -> tuple[int, int, int | None]:
+    """(usable cores, affinity size, cgroup quota)."""
+    aff = len(os.sched_getaffinity(0))
+    q = cgroup_cpu_quota()
+    return (min(aff, q) if q else aff), aff, q
+
+
 def _worker(a):
     os.environ.update(_ENV1)
     import numpy as np
@@ -31,36 +69,54 @@ def _worker(a):
     from oracle import rmsf_oracle as O
     from oracle import synth as SY
 
-    motion = None
-    if a.align != "none":
-        motion = np.load(a.motion)
+    motion = None if a.align == "none" else np.load(a.motion)
     traj = SY.frames(a.seed, a.n_atoms, a.f0, a.nf, motion)
     sel = np.arange(a.n_atoms)
-    t0 = time.perf_counter()
     if a.align == "none":
+        t0 = time.perf_counter()
         S = O.rank_sweep2(traj, sel, None, 0, a.nf)
-    else:
-        ref0 = SY.frames(a.seed, a.n_atoms, 0, 1, motion)[0]
-        ref_com, ref_c = O.centred_reference(ref0[sel])
-        S = O.rank_sweep2(traj, sel, None, 0, a.nf, ref_c, ref_com)
-    dt = time.perf_counter() - t0
-    np.savez(a.out, n=S[0], mean=S[1], m2=S[2], dt=dt)
+        np.savez(a.out, n=S[0], mean=S[1], m2=S[2], dt=time.perf_counter() - t0, dt1=0.0)
+        return
+    ref0 = SY.frames(a.seed, a.n_atoms, 0, 1, motion)[0]  # every rank reads frame 0 (RMSF.py:80-87)
+    t0 = time.perf_counter()
+    ref_com, ref_c = O.centred_reference(ref0[sel])
+    dt1 = 0.0
+    if a.align == "average":
+        pos = O.rank_sweep1(traj, sel, None, 0, a.nf, ref_c, ref_com)       # RMSF.py:89-105
+        dt1 = time.perf_counter() - t0
+        np.save(a.out + ".sum.npy", pos)
+        sys.stdout.write("ready\n")
+        sys.stdout.flush()
+        if sys.stdin.readline().strip() != "go":                            # the Allreduce (RMSF.py:107-110)
+            raise SystemExit("cpu baseline worker: no average")
+        t0 = time.perf_counter()
+        average = np.load(a.avg)                                            # RMSF.py:111
+        ref_com, ref_c = O.centred_reference(average)                       # RMSF.py:113-118
+    S = O.rank_sweep2(traj, sel, None, 0, a.nf, ref_c, ref_com)             # RMSF.py:120-140
+    np.savez(a.out, n=S[0], mean=S[1], m2=S[2], dt=time.perf_counter() - t0, dt1=dt1)
 
 
 def run(n_atoms: int, frames_per_proc: int, procs: int | None = None, seed: int = 0, align: str = "none",
-        motion=None) -> dict:
-    """Launch ``procs`` worker processes; returns the atom-frames/s figure."""
+        motion=None, want_rmsf: bool = False) -> dict:
+    """Launch ``procs`` worker processes; returns the atom-frames/s figure
+    (each atom-frame counted once, whatever the number of sweeps).
+    ``want_rmsf``: also return the computed RMSF (key "rmsf", numpy; tests)."""
     import numpy as np
 
     from oracle import rmsf_oracle as O
 
+    cores, aff, quota = available_cores()
     if procs is None:
-        procs = max(1, min(len(os.sched_getaffinity(0)), 16))
+        procs = cores
+    if align != "none" and motion is None:
+        raise ValueError("aligned baselines need the motion table the GPU run uses")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, **_ENV1)
     env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+    n_frames = frames_per_proc * procs
     with tempfile.TemporaryDirectory(prefix="rmsf_cpu_") as tmp:
         mpath = os.path.join(tmp, "motion.npy")
+        apath = os.path.join(tmp, "average.npy")
         if motion is not None:
             np.save(mpath, motion)
         ps, outs = [], []
@@ -69,27 +125,54 @@ def run(n_atoms: int, frames_per_proc: int, procs: int | None = None, seed: int 
             outs.append(out)
             cmd = [sys.executable, "-m", "oracle.cpu_baseline", "--worker", "--n-atoms", str(n_atoms), "--f0",
                    str(r * frames_per_proc), "--nf", str(frames_per_proc), "--seed", str(seed), "--align", align,
-                   "--motion", mpath, "--out", out]
-            ps.append(subprocess.Popen(cmd, env=env, cwd=root))
-        for p in ps:
-            if p.wait() != 0:
-                raise RuntimeError("cpu baseline worker failed")
-        parts, dts = [], []
+                   "--motion", mpath, "--avg", apath, "--out", out]
+            pipes = dict(stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True) if align == "average" else {}
+            ps.append(subprocess.Popen(cmd, env=env, cwd=root, **pipes))
+        t_x = 0.0
+        try:
+            if align == "average":
+                for p in ps:
+                    if p.stdout.readline().strip() != "ready":
+                        raise RuntimeError("cpu baseline worker failed in sweep 1")
+                t0 = time.perf_counter()
+                total = sum(np.load(o + ".sum.npy") for o in outs)              # RMSF.py:110
+                np.save(apath, total / float(n_frames))                         # RMSF.py:111
+                t_x = time.perf_counter() - t0
+                for p in ps:
+                    p.stdin.write("go\n")
+                    p.stdin.flush()
+            for p in ps:
+                if p.wait() != 0:
+                    raise RuntimeError("cpu baseline worker failed")
+        finally:
+            for p in ps:
+                if p.poll() is None:
+                    p.kill()
+        parts, dts, dt1s = [], [], []
         for out in outs:
             d = np.load(out)
             parts.append([int(d["n"]), d["mean"], d["m2"]])
             dts.append(float(d["dt"]))
+            dt1s.append(float(d["dt1"]))
         t0 = time.perf_counter()
         Data = O.chan_fold(parts)  # RMSF.py:143 (root fold)
-        np.sqrt(Data[2].sum(axis=1) / Data[0])  # RMSF.py:146
+        rmsf = np.sqrt(Data[2].sum(axis=1) / Data[0])  # RMSF.py:146
         t_merge = time.perf_counter() - t0
-    total = n_atoms * frames_per_proc * procs
-    wall = max(dts) + t_merge
-    return {"value": total / wall, "unit": "atom-frames/s", "cores": procs, "kind": "port",
-            "sample": f"{n_atoms} atoms x {frames_per_proc * procs} frames ({frames_per_proc}/process), "
-                      f"align={align}, numpy restatement of RMSF.py per-rank loop, {procs} processes x 1 thread, "
+    total_af = n_atoms * n_frames
+    wall = max(dt1s) + t_x + max(dts) + t_merge
+    what = {"none": "Welford sweep (RMSF.py:120-140 without alignment; config C2)",
+            "frame0": "aligned Welford sweep against frame 0 (config C3)",
+            "average": "RMSF.py's two sweeps (align+sum, Allreduce average, align+Welford, Chan reduce)"}[align]
+    out = {"value": total_af / wall, "unit": "atom-frames/s", "cores": procs, "kind": "port",
+            "workload": what,
+            "sample": f"{n_atoms} atoms x {n_frames} frames ({frames_per_proc}/process), align={align}: numpy "
+                      f"restatement of RMSF.py, {procs} processes x 1 thread (mpirun -n {procs} shape), "
                       f"frames pre-generated (no XTC decode): optimistic",
-            "seconds": wall, "cpu_seconds": sum(dts)}
+            "host": {"affinity_cpus": aff, "cgroup_cpu_quota": quota},
+            "seconds": wall, "cpu_seconds": sum(dts) + sum(dt1s)}
+    if want_rmsf:
+        out["rmsf"] = rmsf
+    return out
 
 
 if __name__ == "__main__":
@@ -99,12 +182,19 @@ if __name__ == "__main__":
     ap.add_argument("--f0", type=int, default=0)
     ap.add_argument("--nf", type=int, default=16)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--align", default="none")
+    ap.add_argument("--align", default="none", choices=["none", "frame0", "average"])
     ap.add_argument("--motion", default="")
+    ap.add_argument("--avg", default="")
     ap.add_argument("--out", default="")
     ap.add_argument("--procs", type=int, default=None)
     a = ap.parse_args()
     if a.worker:
         _worker(a)
     else:
-        print(json.dumps(run(a.n_atoms, a.nf, a.procs, a.seed, a.align)))
+        mot = None
+        if a.align != "none":
+            sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                            "mdanalysis-mpi_amd"))
+            from rmsf_amd.synth import motion_table
+            mot = motion_table(1, a.nf * (a.procs or available_cores()[0]))
+        print(json.dumps(run(a.n_atoms, a.nf, a.procs, a.seed, a.align, mot)))

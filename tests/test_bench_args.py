@@ -1,0 +1,47 @@
+"""bench.py's argument handling (no GPU): strong scaling of one trajectory
+by default, weak scaling on request, and a one-process ``--gpus N`` that
+fails loudly when fewer devices are visible unless it is a labelled
+rehearsal."""
+import pytest
+
+import bench
+
+
+def test_default_is_strong_scaling_of_c2():
+    a = bench.parse(["--gpus", "8"])
+    wl = bench.resolve(a, 8)
+    assert wl["scaling"] == "strong" and wl["n_total"] == 20_000 and wl["n_atoms"] == 100_000
+    assert wl["align"] is None
+    assert bench.resolve(bench.parse([]), 1)["n_total"] == 20_000
+
+
+def test_weak_scaling_and_c4():
+    wl = bench.resolve(bench.parse(["--scaling", "weak"]), 4)
+    assert wl["scaling"] == "weak" and wl["n_total"] == 80_000
+    wl = bench.resolve(bench.parse(["--workload", "c4"]), 8)
+    assert wl["scaling"] == "weak" and wl["n_total"] == 20_000 and wl["n_atoms"] == 1_000_000
+    wl = bench.resolve(bench.parse(["--frames-per-gpu", "100"]), 2)
+    assert wl["scaling"] == "weak" and wl["n_total"] == 200
+
+
+def test_too_few_frames_for_the_gpus():
+    with pytest.raises(SystemExit):
+        bench.resolve(bench.parse(["--frames", "3"]), 4)
+
+
+def test_device_plan():
+    assert bench.device_plan(2, 8, False) == ([0, 1], False)
+    assert bench.device_plan(1, 1, False) == ([0], False)
+    with pytest.raises(SystemExit, match="2 devices but 1"):
+        bench.device_plan(2, 1, False)
+    assert bench.device_plan(3, 1, True) == ([0, 0, 0], True)
+    with pytest.raises(SystemExit):
+        bench.device_plan(2, 0, True)
+
+
+def test_roofline_sums_bytes_over_launch_time():
+    # 3 launches of different sizes: sum(bytes) / sum(time), never > the data
+    r = bench.roofline("k", 3, 3.0, 3.0e8)
+    assert r["achieved"] == pytest.approx(12 * 3.0e8 / 3.0e-3 / 1e9)
+    assert r["frac"] == pytest.approx(r["achieved"] / 8000.0)
+    assert r["algorithmic_bytes_per_launch"] == pytest.approx(12 * 1.0e8)

@@ -61,3 +61,44 @@ def test_frame_selection_errors():
     with pytest.raises(ValueError):
         FrameList(10, frames=np.ones(9, bool))
     assert len(FrameList(10, frames=[])) == 0
+
+
+def test_non_integer_frames_rejected():
+    with pytest.raises(TypeError):
+        FrameList(10, frames=[1.7, 2.0])
+    with pytest.raises(TypeError):
+        FrameList(10, frames=np.array(["1"]))
+    assert len(FrameList(10, frames=[])) == 0
+    assert list(FrameList(10, frames=np.array([3, 1], dtype=np.int32)).idx) == [1, 3]
+
+
+def _shard(offset, rows, n_traj):
+    """A DeviceSource over a CPU tensor (bounds logic only: no kernel runs)."""
+    import torch
+
+    from rmsf_amd.sources import DeviceSource
+
+    src = DeviceSource.__new__(DeviceSource)
+    src.traj = torch.zeros(rows, 4, 3)
+    src.n_atoms, src.fstride, src.offset, src.n_traj = 4, 12, offset, n_traj
+    src.sel_dev = None
+    return src
+
+
+def test_sharded_run_checks_both_ends():
+    """a rank's shard holds its RMSF.py:65-69 block of the
+    trajectory, but with start/step the block of the *frame list* can run
+    past it -- the last frame of a run is checked, not only the first."""
+    from rmsf_amd import parallel
+
+    n_traj, world = 20, 2
+    blocks = parallel.blocks(n_traj, world)
+    shard = _shard(blocks[0][0], blocks[0][1] - blocks[0][0], n_traj)  # rank 0 holds frames [0, 10)
+    fl = FrameList(n_traj)
+    assert sum(b.n_frames for b in shard.batches(fl, *blocks[0], 100, 0)) == 10
+    fl = FrameList(n_traj, start=4)                                   # 16 frames: rank 0 gets positions [0, 8)
+    b0, b1 = parallel.blocks(len(fl), world)[0]                       # = frames 4..11: past the shard
+    with pytest.raises(IndexError, match="frame 11"):
+        list(shard.batches(fl, b0, b1, 100, 0))
+    with pytest.raises(IndexError, match="frame 11"):                 # split into runs: the failing one raises
+        list(shard.batches(fl, b0, b1, 4, 0))

@@ -1,0 +1,77 @@
+"""bench.py on the GPU at small sizes: the JSON line keeps the driver's
+contract, the roofline is computed from the bytes of the timed launches
+(never above the data's own bytes), and the one-process multi-device form
+(``--gpus N`` without a launcher; a labelled rehearsal on a one-GPU box)
+computes the same RMSF as the oracle's ``mpirun -n N`` emulation."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import bench
+from oracle import rmsf_oracle as O
+from oracle import synth as SY
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("align", ["none", "frame0", "average"])
+def test_single_process_rehearsal_matches_oracle(align, capsys):
+    a = bench.parse(["--gpus", "3", "--rehearse", "--n-atoms", "1500", "--frames", "61", "--steps", "2",
+                     "--warmup", "1", "--no-cpu-baseline", "--align", align])
+    wl = bench.resolve(a, 3)
+    bench.main_single_process(a, wl, None)
+    line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert line["n_gpus"] == 3 and line["rehearsal"] is True and line["devices"] == [0, 0, 0]
+    assert line["scaling"] == "strong" and line["config"]["n_frames_total"] == 61
+    assert line["roofline"]["launches"] == 3 * 2 * (2 if align == "average" else 1)
+    assert 0 < line["roofline"]["frac"] < 1.0
+    from rmsf_amd.synth import motion_table
+
+    mt = motion_table(1, 61) if align != "none" else None
+    traj = SY.frames(0, 1500, 0, 61, mt)
+    exp = O.rmsf_script(traj, None, None, size=3, align=None if align == "none" else align)["rmsf"]
+    assert abs(line["rmsf_checksum"] - float(exp.sum())) < 1e-6 * len(exp)
+
+
+def test_bench_cli_small_json_line():
+    cmd = [sys.executable, "bench.py", "--n-atoms", "20000", "--frames", "300", "--steps", "3", "--warmup", "1",
+           "--no-cpu-baseline", "--mode-steps", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in line
+    assert line["n_gpus"] == 1 and line["steps"] == 3 and line["scaling"] == "strong"
+    rf = line["roofline"]
+    assert rf["launches"] == 3 and 0 < rf["frac"] < 1.0
+    assert rf["algorithmic_bytes_per_launch"] == 12 * 20000 * 300
+    m = line["modes"]
+    for name in ("c3_frame0", "rmsf_py_average"):
+        assert 0 < m[name]["accumulate_hbm_gbs"] < 8000 and 0 < m[name]["superpose_hbm_gbs"] < 8000
+
+
+def test_bench_batched_launches_roofline_below_peak():
+    # several launches per step of different sizes: bytes are charged per launch
+    cmd = [sys.executable, "bench.py", "--n-atoms", "20000", "--frames", "1000", "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline", "--no-modes", "--align", "frame0", "--batch-frames", "300"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rf = json.loads(r.stdout.strip().splitlines()[-1])["roofline"]
+    assert rf["launches"] == 2 * 4  # 300+300+300+100 per step
+    assert rf["algorithmic_bytes_per_launch"] == pytest.approx(12 * 20000 * 250)
+    assert 0 < rf["frac"] < 1.0
+
+
+def test_single_process_refuses_missing_devices():
+    import torch
+
+    n = torch.cuda.device_count() + 1
+    with pytest.raises(SystemExit, match="visible"):
+        bench.device_plan(n, torch.cuda.device_count(), False)
+    np.testing.assert_equal(bench.device_plan(n, torch.cuda.device_count(), True)[0], [0] * n)

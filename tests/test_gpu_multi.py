@@ -88,12 +88,95 @@ def test_multi_atomgroup_duck_typed(traj):
 
 def test_multi_errors(traj):
     from rmsf_amd import RMSF
-    with pytest.raises(TypeError):
+    with pytest.raises(ValueError, match="shards' devices"):
         RMSF(torch.tensor(traj, device="cuda"), gpus=[0, 0]).run()
     with pytest.raises(ZeroDivisionError):
         RMSF(traj, gpus=[0, 0]).run(start=5, stop=5)
-    with pytest.raises(NotImplementedError):
-        RMSF(traj, align="frame0", collect_rmsd=True, gpus=1).run()
+    with pytest.raises(ValueError, match="collect_rmsd"):
+        RMSF(traj, collect_rmsd=True, gpus=1).run()
+    with pytest.raises(TypeError):
+        RMSF([torch.tensor(traj, device="cuda").double()], gpus=1).run()
+
+
+def _shards(traj, cuts):
+    t = torch.tensor(traj, device="cuda")
+    edges = [0] + list(cuts) + [len(traj)]
+    return [t[a:b].contiguous() for a, b in zip(edges[:-1], edges[1:])]
+
+
+@pytest.mark.parametrize("align", [None, "frame0", "average"])
+@pytest.mark.parametrize("run", [{}, {"start": 3, "step": 4}, {"frames": [0, 1, 2, 11, 12, 30, 31, 36]},
+                                 {"step": -2}])
+def test_multi_device_shards(traj, align, run):
+    """HBM-resident shards, one tensor per device (here: three on device 0,
+    the in-process fold): each context takes the frames its shard holds;
+    equal to the oracle on the same (ascending) frames."""
+    from rmsf_amd import RMSF
+    sel = np.arange(3, 700, 4)
+    parts = _shards(traj, (10, 25))
+    r = RMSF(parts, select=sel, align=align, collect_rmsd=align is not None).run(**run).results
+    fl = np.sort(np.arange(len(traj))[slice(run.get("start"), None, run.get("step"))]) if "frames" not in run \
+        else np.array(run["frames"])
+    exp = O.rmsf_script(traj[fl], sel, None, size=1, align=align)
+    np.testing.assert_allclose(r.rmsf, exp["rmsf"], rtol=0, atol=TOL)
+    assert r.n_frames == len(fl) and r.devices == [0, 0, 0]
+    assert sum(b1 - b0 for b0, b1 in r.blocks) == len(fl)
+    if align is not None:
+        one = RMSF(torch.tensor(traj[fl], device="cuda"), select=sel, align=align, collect_rmsd=True).run()
+        np.testing.assert_allclose(r.rmsd, one.results.rmsd, rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("align", ["frame0", "average"])
+def test_multi_collect_rmsd_host(traj, align):
+    """The per-frame QCP rmsd (RMSF.py:48's discarded by-product) under gpus=,
+    in frame-list order across the devices' blocks."""
+    from rmsf_amd import RMSF
+    sel = np.arange(0, 700, 5)
+    r = RMSF(traj, select=sel, align=align, collect_rmsd=True, gpus=[0, 0, 0]).run(step=2).results
+    one = RMSF(torch.tensor(traj, device="cuda"), select=sel, align=align, collect_rmsd=True).run(step=2).results
+    assert r.rmsd.shape == (len(range(0, len(traj), 2)),)
+    np.testing.assert_allclose(r.rmsd, one.rmsd, rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("sl", [dict(step=-2), dict(start=30, stop=2, step=-3)])
+def test_multi_reversed_ranges(traj, sl):
+    from rmsf_amd import RMSF
+    sel = np.arange(1, 700, 6)
+    r = RMSF(traj, select=sel, align="average", gpus=[0, 0, 0]).run(**sl).results
+    fl = np.sort(np.arange(len(traj))[slice(sl.get("start"), sl.get("stop"), sl["step"])])
+    exp = O.rmsf_script(traj[fl], sel, None, size=3, align="average")
+    np.testing.assert_allclose(r.rmsf, exp["rmsf"], rtol=0, atol=TOL)
+    assert r.n_frames == len(fl)
+
+
+def test_multi_frames_xtc_atomgroup_dcd(tmp_path, traj):
+    """frames= (indices / a boolean mask) with gpus= for the file and
+    AtomGroup inputs, against the oracle on those frames."""
+    from oracle import xtc_py
+    from rmsf_amd import RMSF
+    from rmsf_amd.dcd import write_dcd
+    from rmsf_amd.xtc import write_xtc
+    from test_gpu_multirank import _FakeAtomGroup, _FakeUniverse
+    sel = np.arange(2, 700, 5)
+    idx = np.array([1, 3, 5, 6, 7, 19, 30, 33, 36])
+    xp = str(tmp_path / "m.xtc")
+    write_xtc(xp, traj)
+    q = xtc_py.read_xtc(xp)
+    r = RMSF(xp, select=sel, align="average", gpus=[0, 0]).run(frames=idx).results
+    exp = O.rmsf_script(q[idx], sel, None, size=2, align="average")
+    np.testing.assert_allclose(r.rmsf, exp["rmsf"], rtol=0, atol=TOL)
+    ag = _FakeAtomGroup(_FakeUniverse(traj), sel, None)
+    r = RMSF(ag, align="frame0", masses=np.ones(len(sel)), gpus=[0, 0, 0]).run(frames=idx).results
+    exp = O.rmsf_script(traj[idx], sel, None, size=3, align="frame0")
+    np.testing.assert_allclose(r.rmsf, exp["rmsf"], rtol=0, atol=TOL)
+    dp = str(tmp_path / "m.dcd")
+    write_dcd(dp, traj)
+    mask = np.zeros(len(traj), bool)
+    mask[idx] = True
+    for align in (None, "average"):  # streamed runs; staged into HBM for the two sweeps
+        r = RMSF(dp, select=sel, align=align, gpus=[0, 0]).run(frames=mask).results
+        exp = O.rmsf_script(traj[idx], sel, None, size=2, align=align)
+        np.testing.assert_allclose(r.rmsf, exp["rmsf"], rtol=0, atol=TOL)
 
 
 @pytest.mark.parametrize("align", [None, "frame0", "average"])
