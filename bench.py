@@ -479,8 +479,9 @@ def main():
         return dt, timer, res
 
     dt, timer, res = timed(wl["align"], a.steps, a.warmup)
-    par = (f"frame-sharded x{world} (RMSF.py:65-69 blocks), one process per GPU, RCCL Chan merge" if world > 1
-           else "1 GPU")
+    transport = "RCCL" if a.backend == "nccl" else f"{a.backend} (REHEARSAL: ranks may share a device)"
+    par = (f"frame-sharded x{world} (RMSF.py:65-69 blocks), one process per GPU, {transport} Chan merge"
+           if world > 1 else "1 GPU")
     out = base_line(a, wl, world, dt, par)
     launches, acc_ms, acc_af = timer.totals("accumulate")
     traffic = load_traffic(a.workload, n_atoms, n_local) if launches == a.steps else None

@@ -65,7 +65,8 @@ constexpr int kXform = RMSF_XFORM_DOUBLES;
 constexpr int kStats = 16;       // doubles per (frame, chunk) partial
 constexpr int64_t kAccumBlocks = 3584;       // target workgroups, k_welford_flat
 constexpr int64_t kAccumBlocksAtom = 4608;   // target workgroups, k_accum_atoms
-constexpr int64_t kStatsBlocks = 4096;  // aim for >= this many (frame-group, chunk) blocks (2048-4096 measured best at C3, 16384 ~3 % slower)
+constexpr int64_t kStatsGroups = 3072;  // k_frame_stats workgroups (balanced grid; 4 rounds of 3 per CU on MI355X)
+constexpr int64_t kStatsMinUnits = 1;   // ... at least this many (64-frame, 32-atom) units each
 
 // ---------------------------------------------------------------------------
 // Welford coefficients a_k = k/(k+1), b_k = 1/(k+1) (RMSF.py:137-138), folded
@@ -529,17 +530,28 @@ __device__ __forceinline__ void wave_sum(double (&v)[N]) {
   }
 }
 
-// k_frame_stats -- "lanes over frames".  grid = (ceil(n_frames/64), n_chunks).
-// Block (g, c): frames [64g, 64g+64) (lane = frame), atoms [c*chunk, ...).
-// Tiles of 64 frames x kTA atoms are staged HBM -> registers -> LDS (the next
-// tile's loads are in flight while the current one is consumed); wave w
-// consumes atoms [w*kTA/4, (w+1)*kTA/4) of every tile for its 64 frames.  The
-// atom index is wave-uniform, so the f64 reference (and masses) arrive by
-// scalar loads and no per-atom cross-lane reduction exists: each lane owns
-// its frame's sums.  Sums are relative to a per-frame pivot p (the frame's
-// first selected atom, for conditioning):
+// k_frame_stats -- "lanes over frames" on a balanced grid.
+// Work units: (64-frame group g, 32-atom tile t); unit u = g*ntiles + t
+// (group-major).  Workgroup b takes the equal contiguous range
+// [T b / G, T (b+1) / G) of the T = ngroups*ntiles units and walks it as
+// segments (maximal runs inside one frame group); each segment writes one
+// partial -- 16 sums x 64 frames -- into slot b*P + j (j = segment index in
+// the workgroup).  Equal ranges leave no tail wave, and the partials stay
+// small (G*P slots, independent of the trajectory length).
+// Inside a segment: lane = frame, the 4 waves of the block split each
+// 32-atom tile that is staged HBM -> registers -> LDS (pitch 100 dwords:
+// 16-B rows, conflict-free ds_read_b128 column reads), with the next tile's
+// loads in flight.  The atom index is wave-uniform, so the f64 reference and
+// masses arrive by scalar loads and no per-atom cross-lane reduction exists:
+// each lane owns its frame's sums.  Sums are relative to a per-frame pivot p
+// (the frame's first selected atom, for conditioning):
 //   [0..2]  sum x'            [3..5]  sum m x'   (only with masses)
 //   [6..14] sum x'_a r_b      [15]    sum |x'|^2
+// Epilogue: the 4 waves' sums meet in LDS and all 256 threads add them (wave
+// order 0..3, fixed) and store the partial stat-major, [16][64] -- every
+// store instruction writes 512 contiguous bytes.  (The former epilogue, wave
+// 0 alone storing 16 doubles per lane at a 128-B lane stride, cost 3-18 % of
+// the kernel: tools/ubench_stats2.hip.)
 // VEC4: contiguous selection, 16-B aligned frames -> float4 staging loads;
 // otherwise (gathered selection / odd strides) element-wise staging loads.
 constexpr int kTF = 64;                    // frames per block (one per lane)
@@ -549,104 +561,107 @@ constexpr int kRow4 = 3 * kTA / 4;         // float4 per tile row
 constexpr int kNPre = kTF * kRow4 / kBlock;  // float4 per thread per tile (VEC4)
 constexpr int kNEl = kTF * kTA / kBlock;     // atoms per thread per tile (element path)
 constexpr int kAPW = kTA / 4;              // atoms per wave per tile
+constexpr int kStatsLds = (kTF * kPitch > 2 * (kBlock / 64) * kStats * kTF) ? kTF * kPitch : 2 * (kBlock / 64) * kStats * kTF;
 static_assert(kTF * kRow4 % kBlock == 0 && kTF * kTA % kBlock == 0, "tile shape");
-static_assert((kBlock / 64 - 1) * kStats * 64 * 2 <= kTF * kPitch, "wave fold (doubles) fits in the tile buffer (floats)");
+static_assert(kStats * kTF % kBlock == 0, "epilogue: whole outputs per thread");
+
+// balanced-grid plan of k_frame_stats (computed identically on the host for
+// the launch and for k_qcp_frames' fold)
+struct StatsPlan {
+  int64_t ntiles, ngroups, T;
+  int G, P;
+};
+
+__host__ __device__ inline int64_t st_lo(const StatsPlan &p, int64_t b) { return p.T * b / p.G; }
 
 template <bool GATHER, bool MASSES, bool VEC4>
 __global__ __launch_bounds__(kBlock) void k_frame_stats(
     const float *__restrict__ xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
     const int32_t *__restrict__ sel, const double *__restrict__ masses, const double *__restrict__ ref,
-    int64_t chunk, int n_chunks, double *__restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float tile[kTF * kPitch];
+    StatsPlan pl, double *__restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float tile[kStatsLds];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t f0 = (int64_t)blockIdx.x * kTF;
-  const int ch = blockIdx.y;
-  const int64_t a_beg = (int64_t)ch * chunk, a_end = min(n_sel, a_beg + chunk);
-  const int64_t f = f0 + lane;
   const int64_t last = n_frames - 1;
-  const float *myfr = xyz + min(f, last) * fstride;
   const int64_t o0 = GATHER ? 3 * (int64_t)sel[0] : 0;
-  const double px = myfr[o0], py = myfr[o0 + 1], pz = myfr[o0 + 2];
-
-  double acc[kStats];
-#pragma unroll
-  for (int j = 0; j < kStats; ++j) acc[j] = 0.0;
-
-  f32x4 pre[VEC4 ? kNPre : 1];
-  float pel[VEC4 ? 1 : 3 * kNEl];
   const int64_t lim = 3 * n_sel;  // floats of the selection inside a frame row (VEC4)
-  auto gload = [&](int64_t t0) {
-    if (VEC4) {
+  int64_t lo = uni64(st_lo(pl, blockIdx.x));
+  const int64_t hi = uni64(st_lo(pl, blockIdx.x + 1));
+  int64_t slot = (int64_t)blockIdx.x * pl.P;
+  while (lo < hi) {
+    const int64_t g = uni64(lo / pl.ntiles);
+    const int64_t t_lo = lo - g * pl.ntiles;
+    const int64_t t_hi = min(pl.ntiles, t_lo + (hi - lo));
+    const int64_t f0 = g * kTF;
+    const int64_t a_beg = t_lo * kTA, a_end = min(n_sel, t_hi * kTA);
+    const float *myfr = xyz + min(f0 + lane, last) * fstride;
+    const double px = myfr[o0], py = myfr[o0 + 1], pz = myfr[o0 + 2];
+    double acc[kStats];
 #pragma unroll
-      for (int k = 0; k < kNPre; ++k) {
-        const int idx = threadIdx.x + k * kBlock;
-        const int row = idx / kRow4, col = idx % kRow4;
-        const float *src = xyz + min(f0 + row, last) * fstride;
-        const int64_t e = 3 * t0 + 4 * col;
-        if (e + 3 < lim) {
-          pre[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(src + e));
-        } else {  // selection tail: never read past the selection
-          pre[k] = f32x4{e < lim ? src[e] : 0.f, e + 1 < lim ? src[e + 1] : 0.f, e + 2 < lim ? src[e + 2] : 0.f, 0.f};
-        }
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < kNEl; ++k) {
-        const int idx = threadIdx.x + k * kBlock;
-        const int row = idx / kTA, j = idx % kTA;
-        const int64_t a = t0 + j;
-        const float *src = xyz + min(f0 + row, last) * fstride;
-        if (a < a_end) {
-          const int64_t off = GATHER ? 3 * (int64_t)sel[a] : 3 * a;
-          pel[3 * k] = __builtin_nontemporal_load(src + off);
-          pel[3 * k + 1] = __builtin_nontemporal_load(src + off + 1);
-          pel[3 * k + 2] = __builtin_nontemporal_load(src + off + 2);
-        } else {
-          pel[3 * k] = pel[3 * k + 1] = pel[3 * k + 2] = 0.f;
-        }
-      }
-    }
-  };
-  auto lstore = [&]() {
-    if (VEC4) {
-#pragma unroll
-      for (int k = 0; k < kNPre; ++k) {
-        const int idx = threadIdx.x + k * kBlock;
-        const int row = idx / kRow4, col = idx % kRow4;
-        *reinterpret_cast<f32x4 *>(tile + row * kPitch + 4 * col) = pre[k];
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < kNEl; ++k) {
-        const int idx = threadIdx.x + k * kBlock;
-        const int row = idx / kTA, j = idx % kTA;
-        float *d = tile + row * kPitch + 3 * j;
-        d[0] = pel[3 * k];
-        d[1] = pel[3 * k + 1];
-        d[2] = pel[3 * k + 2];
-      }
-    }
-  };
+    for (int j = 0; j < kStats; ++j) acc[j] = 0.0;
 
-  gload(a_beg);
-  for (int64_t t0 = a_beg; t0 < a_end; t0 += kTA) {
-    __syncthreads();
-    lstore();
-    __syncthreads();
-    if (t0 + kTA < a_end) gload(t0 + kTA);
-    const f32x4 *my = reinterpret_cast<const f32x4 *>(tile + lane * kPitch + w * 3 * kAPW);
-    const int64_t ab = t0 + w * kAPW;  // first atom of this wave's slab (uniform)
-#pragma unroll 1
-    for (int g = 0; g < kAPW / 4; ++g) {
-      const int64_t a4 = ab + 4 * g;
-      if (a4 >= a_end) break;  // uniform
-      const f32x4 q0 = my[3 * g], q1 = my[3 * g + 1], q2 = my[3 * g + 2];
+    f32x4 pre[VEC4 ? kNPre : 1];
+    float pel[VEC4 ? 1 : 3 * kNEl];
+    auto gload = [&](int64_t t0) {
+      if (VEC4) {
+#pragma unroll
+        for (int k = 0; k < kNPre; ++k) {
+          const int idx = threadIdx.x + k * kBlock;
+          const int row = idx / kRow4, col = idx % kRow4;
+          const float *src = xyz + min(f0 + row, last) * fstride;
+          const int64_t e = 3 * t0 + 4 * col;
+          if (e + 3 < lim) {
+            pre[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(src + e));
+          } else {  // selection tail: never read past the selection
+            pre[k] = f32x4{e < lim ? src[e] : 0.f, e + 1 < lim ? src[e + 1] : 0.f, e + 2 < lim ? src[e + 2] : 0.f, 0.f};
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < kNEl; ++k) {
+          const int idx = threadIdx.x + k * kBlock;
+          const int row = idx / kTA, j = idx % kTA;
+          const int64_t a = t0 + j;
+          const float *src = xyz + min(f0 + row, last) * fstride;
+          if (a < a_end) {
+            const int64_t off = GATHER ? 3 * (int64_t)sel[a] : 3 * a;
+            pel[3 * k] = __builtin_nontemporal_load(src + off);
+            pel[3 * k + 1] = __builtin_nontemporal_load(src + off + 1);
+            pel[3 * k + 2] = __builtin_nontemporal_load(src + off + 2);
+          } else {
+            pel[3 * k] = pel[3 * k + 1] = pel[3 * k + 2] = 0.f;
+          }
+        }
+      }
+    };
+    auto lstore = [&]() {
+      if (VEC4) {
+#pragma unroll
+        for (int k = 0; k < kNPre; ++k) {
+          const int idx = threadIdx.x + k * kBlock;
+          const int row = idx / kRow4, col = idx % kRow4;
+          *reinterpret_cast<f32x4 *>(tile + row * kPitch + 4 * col) = pre[k];
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < kNEl; ++k) {
+          const int idx = threadIdx.x + k * kBlock;
+          const int row = idx / kTA, j = idx % kTA;
+          float *d = tile + row * kPitch + 3 * j;
+          d[0] = pel[3 * k];
+          d[1] = pel[3 * k + 1];
+          d[2] = pel[3 * k + 2];
+        }
+      }
+    };
+    // one 4-atom group of this wave's slab (atoms a4..a4+3, a wave-uniform index)
+    auto group = [&](const f32x4 *my, int gi, int64_t a4, int n_at) {
+      const f32x4 q0 = my[3 * gi], q1 = my[3 * gi + 1], q2 = my[3 * gi + 2];
       const float c[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
       const double *rr = ref + 3 * a4;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (a4 + i >= a_end) break;  // uniform
+        if (i >= n_at) break;  // uniform; n_at < 4 only in the selection's last tile
         const double r0 = rr[3 * i], r1 = rr[3 * i + 1], r2 = rr[3 * i + 2];
         const double x = (double)c[3 * i] - px, y = (double)c[3 * i + 1] - py, z = (double)c[3 * i + 2] - pz;
         acc[0] += x;
@@ -669,26 +684,46 @@ __global__ __launch_bounds__(kBlock) void k_frame_stats(
         acc[14] = fma(z, r2, acc[14]);
         acc[15] = fma(x, x, fma(y, y, fma(z, z, acc[15])));
       }
+    };
+
+    gload(a_beg);
+    for (int64_t t0 = a_beg; t0 < a_end; t0 += kTA) {
+      __syncthreads();
+      lstore();
+      __syncthreads();
+      if (t0 + kTA < a_end) gload(t0 + kTA);
+      const f32x4 *my = reinterpret_cast<const f32x4 *>(tile + lane * kPitch + w * 3 * kAPW);
+      const int64_t ab = t0 + w * kAPW;  // first atom of this wave's slab (uniform)
+      if (t0 + kTA <= a_end) {           // a whole tile: no per-atom checks
+#pragma unroll 1
+        for (int gi = 0; gi < kAPW / 4; ++gi) group(my, gi, ab + 4 * gi, 4);
+      } else {
+#pragma unroll 1
+        for (int gi = 0; gi < kAPW / 4; ++gi) {
+          const int64_t a4 = ab + 4 * gi;
+          if (a4 >= a_end) break;  // uniform
+          group(my, gi, a4, (int)min((int64_t)4, a_end - a4));
+        }
+      }
     }
-  }
-  // fold waves 1..3 into wave 0 through the (now free) tile buffer, in a
-  // fixed order (deterministic), then each lane of wave 0 writes its frame.
-  __syncthreads();
-  double *red = reinterpret_cast<double *>(tile);
-  if (w > 0) {
+    // the 4 waves' sums meet in LDS (the tile buffer is free after this
+    // barrier); thread t then adds outputs o = t + 256 k (o = stat*64 + frame)
+    __syncthreads();
+    double *red = reinterpret_cast<double *>(tile);
 #pragma unroll
-    for (int j = 0; j < kStats; ++j) red[((w - 1) * kStats + j) * 64 + lane] = acc[j];
-  }
-  __syncthreads();
-  if (w == 0 && f < n_frames) {
-    double *o = part + (f * n_chunks + ch) * kStats;
+    for (int j = 0; j < kStats; ++j) red[(w * kStats + j) * kTF + lane] = acc[j];
+    __syncthreads();
+    double *out = part + slot * (kStats * kTF);
 #pragma unroll
-    for (int j = 0; j < kStats; ++j) {
-      double t = acc[j];
+    for (int k = 0; k < kStats * kTF / kBlock; ++k) {
+      const int o = threadIdx.x + k * kBlock;
+      double t = red[o];
 #pragma unroll
-      for (int v = 0; v < kBlock / 64 - 1; ++v) t += red[(v * kStats + j) * 64 + lane];
-      o[j] = t;
+      for (int v = 1; v < kBlock / 64; ++v) t += red[v * kStats * kTF + o];
+      out[o] = t;
     }
+    lo += t_hi - t_lo;
+    ++slot;
   }
 }
 
@@ -810,19 +845,31 @@ __host__ __device__ inline void qcp_solve(const double *A, double E0, double len
 // order (deterministic), forms COM / A / E0 and solves QCP on lane 0.
 template <bool GATHER, bool MASSES>
 __global__ __launch_bounds__(kBlock) void k_qcp_frames(
-    const double *__restrict__ part, int n_chunks, int64_t n_frames, const float *__restrict__ xyz,
+    const double *__restrict__ part, StatsPlan pl, int64_t n_frames, const float *__restrict__ xyz,
     int64_t fstride, const int32_t *__restrict__ sel, const double *__restrict__ refinfo,
     double *__restrict__ xform) {
   const int64_t f = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (f >= n_frames) return;
+  // the workgroups whose ranges cover frame group g (units [g*ntiles,
+  // (g+1)*ntiles)): b0.. while their range starts inside it; workgroup b's
+  // segment for g is its (g - first group of b)-th
+  const int64_t g = f / kTF, fl = f - g * kTF;
+  const int64_t ulo = g * pl.ntiles, uhi = ulo + pl.ntiles;
+  int64_t b0 = ulo * pl.G / pl.T;
+  while (b0 > 0 && st_lo(pl, b0) > ulo) --b0;
+  while (st_lo(pl, b0 + 1) <= ulo) ++b0;
   double s[kStats];
 #pragma unroll
   for (int j = 0; j < kStats; ++j) s[j] = 0.0;
-  for (int c = lane; c < n_chunks; c += 64) {
-    const double *pp = part + ((int64_t)f * n_chunks + c) * kStats;
+  for (int64_t b = b0 + lane; b < pl.G; b += 64) {
+    const int64_t blo = st_lo(pl, b);
+    if (blo >= uhi) break;
+    if (st_lo(pl, b + 1) <= blo) continue;  // an empty range writes nothing
+    const int64_t seg = g - blo / pl.ntiles;
+    const double *pp = part + ((int64_t)b * pl.P + seg) * (kStats * kTF) + fl;
 #pragma unroll
-    for (int j = 0; j < kStats; ++j) s[j] += pp[j];
+    for (int j = 0; j < kStats; ++j) s[j] += pp[j * kTF];
   }
   wave_sum(s);
   if (lane != 0) return;
@@ -1169,16 +1216,19 @@ __global__ __launch_bounds__(kBlock) void k_synth(float *__restrict__ out, int64
 
 inline unsigned grid1(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
-// Atom chunk per block of k_frame_stats: as long as possible (fewer partials)
-// while the grid still has >= kStatsBlocks blocks; a multiple of the tile.
-void stats_chunks(int64_t n_sel, int64_t n_frames, int64_t *chunk, int64_t *n_chunks) {
-  const int64_t groups = std::max<int64_t>(1, (n_frames + kTF - 1) / kTF);
-  int64_t nc = (kStatsBlocks + groups - 1) / groups;
-  nc = std::max<int64_t>(1, std::min<int64_t>(nc, std::min<int64_t>((n_sel + kTA - 1) / kTA, 65535)));
-  int64_t c = (n_sel + nc - 1) / nc;
-  c = (c + kTA - 1) / kTA * kTA;
-  *chunk = c;
-  *n_chunks = (n_sel + c - 1) / c;
+// Balanced grid of k_frame_stats: kStatsGroups workgroups (a fixed count,
+// so the summation order -- hence the bits -- does not depend on the device),
+// fewer when the batch has fewer than kStatsMinUnits units per workgroup.
+// P = the most segments any workgroup's range can cross: ceil(len/ntiles)+1.
+StatsPlan stats_plan(int64_t n_sel, int64_t n_frames) {
+  StatsPlan p;
+  p.ntiles = (n_sel + kTA - 1) / kTA;
+  p.ngroups = std::max<int64_t>(1, (n_frames + kTF - 1) / kTF);
+  p.T = p.ntiles * p.ngroups;
+  p.G = (int)std::max<int64_t>(1, std::min<int64_t>(kStatsGroups, p.T / kStatsMinUnits));
+  const int64_t len = (p.T + p.G - 1) / p.G;
+  p.P = (int)((len + p.ntiles - 1) / p.ntiles + 1);
+  return p;
 }
 
 }  // namespace
@@ -1288,9 +1338,8 @@ RMSF_EXPORT int rmsf_reference_setup(const float *d_frame, const double *d_avg, 
 
 RMSF_EXPORT size_t rmsf_superpose_workspace_bytes(int64_t n_sel, int64_t n_frames) {
   if (n_sel < 1 || n_frames < 0) return 0;
-  int64_t chunk, nch;
-  stats_chunks(n_sel, n_frames, &chunk, &nch);
-  return (size_t)n_frames * (size_t)nch * kStats * sizeof(double);
+  const StatsPlan p = stats_plan(n_sel, n_frames);
+  return (size_t)p.G * (size_t)p.P * kStats * kTF * sizeof(double);
 }
 
 RMSF_EXPORT int rmsf_superpose(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
@@ -1301,17 +1350,16 @@ RMSF_EXPORT int rmsf_superpose(const float *d_xyz, int64_t fstride, int64_t n_fr
   if (!d_xyz || !d_ref || !d_refinfo || !d_xform || !d_work || n_sel < 1 || n_frames < 0 ||
       fstride < (d_sel ? 3 : 3 * n_sel))
     return fail(RMSF_EINVAL, "rmsf_superpose: bad arguments");
-  int64_t chunk, nch;
-  stats_chunks(n_sel, n_frames, &chunk, &nch);
+  const StatsPlan plan = stats_plan(n_sel, n_frames);
   if (work_bytes < rmsf_superpose_workspace_bytes(n_sel, n_frames))
     return fail(RMSF_ENOMEM, "rmsf_superpose: workspace too small");
   hipStream_t s = S(stream);
   double *part = static_cast<double *>(d_work);
   const bool g = d_sel != nullptr, m = d_masses != nullptr;
   const bool vec4 = !g && fstride % 4 == 0 && reinterpret_cast<uintptr_t>(d_xyz) % 16 == 0;
-  dim3 grid((unsigned)((n_frames + kTF - 1) / kTF), (unsigned)nch);
+  dim3 grid((unsigned)plan.G);
 #define ST_LAUNCH(G, M, V) \
-  hipLaunchKernelGGL((k_frame_stats<G, M, V>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, chunk, (int)nch, part)
+  hipLaunchKernelGGL((k_frame_stats<G, M, V>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, plan, part)
   if (g && m) ST_LAUNCH(true, true, false);
   else if (g) ST_LAUNCH(true, false, false);
   else if (m && vec4) ST_LAUNCH(false, true, true);
@@ -1323,7 +1371,7 @@ RMSF_EXPORT int rmsf_superpose(const float *d_xyz, int64_t fstride, int64_t n_fr
   if (rc) return rc;
   const unsigned gq = (unsigned)((n_frames + 3) / 4);
 #define QCP_LAUNCH(G, M) \
-  hipLaunchKernelGGL((k_qcp_frames<G, M>), dim3(gq), dim3(kBlock), 0, s, part, (int)nch, n_frames, d_xyz, fstride, d_sel, d_refinfo, d_xform)
+  hipLaunchKernelGGL((k_qcp_frames<G, M>), dim3(gq), dim3(kBlock), 0, s, part, plan, n_frames, d_xyz, fstride, d_sel, d_refinfo, d_xform)
   if (g && m) QCP_LAUNCH(true, true);
   else if (g) QCP_LAUNCH(true, false);
   else if (m) QCP_LAUNCH(false, true);

@@ -40,6 +40,61 @@ CME ASF
 """.split())
 BACKBONE_NAMES = frozenset(["N", "CA", "C", "O"])
 
+# MDAnalysis' mass guessing (upstream topology/guessers.py + tables.py;
+# restated, not vendored -- parity UNPINNED here, MDAnalysis absent).  A GRO
+# file carries no masses, so MDAnalysis guesses each atom's element from its
+# name and takes the element's mass; RMSF.py's center_of_mass (RMSF.py:84,
+# 94,117,127) weights with those.
+#   tables.atomelements: special atom names -> element
+_ATOM_ELEMENTS = {
+    "BR": "BR", "CAL": "CA", "C0": "CA", "CA2+": "CA", "CES": "CS", "CLA": "CL", "CLAL": "CL", "CL": "CL",
+    "CL-": "CL", "IOD": "I", "FE": "FE", "FE2": "FE", "LIT": "LI", "LI": "LI", "LI+": "LI", "QL": "LI",
+    "MG": "MG", "MG2+": "MG", "K": "K", "POT": "K", "K+": "K", "QK": "K", "SOD": "NA", "NA": "NA",
+    "NA+": "NA", "QN": "NA", "ZN": "ZN", "CU": "CU", "CS": "CS", "CS+": "CS", "QC": "CE", "RB": "RB",
+    "QR": "RB", "BC": "C", "AC": "C", "MW": "DUMMY",
+}
+#   tables.elements: the elements a name may be cut down to
+_ELEMENTS = frozenset(["H", "LI", "BE", "B", "C", "N", "O", "F", "NA", "MG", "AL", "P", "SI", "S", "CL", "K"])
+#   tables.masses (the elements above and the ion names' elements)
+ELEMENT_MASSES = {
+    "H": 1.008, "LI": 6.941, "BE": 9.012182, "B": 10.811, "C": 12.011, "N": 14.007, "O": 15.999,
+    "F": 18.9984032, "NA": 22.989768, "MG": 24.305, "AL": 26.981539, "SI": 28.0855, "P": 30.973762,
+    "S": 32.06, "CL": 35.45, "K": 39.10, "CA": 40.08, "FE": 55.847, "CU": 63.546, "ZN": 65.39, "BR": 79.904,
+    "RB": 85.4678, "I": 126.90447, "CS": 132.90, "CE": 140.115, "DUMMY": 0.0,
+}
+
+
+def guess_atom_element(name: str) -> str:
+    """MDAnalysis ``guess_atom_element``: the special-name table first, then
+    the name without charge symbols and digits cut down to a known element
+    (whole, without its last or first letter, else from the right)."""
+    if name == "":
+        return ""
+    up = name.upper()
+    if up in _ATOM_ELEMENTS:
+        return _ATOM_ELEMENTS[up]
+    no_symbols = re.sub(r"[*+-]", "", name)
+    nm = re.sub(r"[0-9]", "", no_symbols).upper()
+    if nm in _ATOM_ELEMENTS:
+        return _ATOM_ELEMENTS[nm]
+    while nm:
+        if nm in _ELEMENTS:
+            return nm
+        if nm[:-1] in _ELEMENTS:
+            return nm[:-1]
+        if nm[1:] in _ELEMENTS:
+            return nm[1:]
+        if len(nm) <= 2:
+            return nm[0]
+        nm = nm[:-1]
+    return no_symbols
+
+
+def guess_masses(names) -> np.ndarray:
+    """f64 masses from atom names (MDAnalysis ``guess_masses(guess_types(names))``;
+    unknown elements get 0.0, as upstream)."""
+    return np.array([ELEMENT_MASSES.get(guess_atom_element(str(n)).upper(), 0.0) for n in names], dtype=np.float64)
+
 
 class Topology:
     """Per-atom resids, resnames, names (and masses when the file has them)."""
@@ -109,7 +164,10 @@ class GroTopology(Topology):
     """Atoms (resid, resname, name) and the frames of a .gro file.
 
     ``positions`` follow MDAnalysis' GROReader rounding: the text is parsed
-    into float32 nm, then converted in place to Angstrom (x10 in float32)."""
+    into float32 nm, then converted in place to Angstrom (x10 in float32).
+    ``masses`` are guessed from the atom names as MDAnalysis' GROParser does
+    (``guess_masses``), so a mass-weighted centre of mass matches RMSF.py's
+    for any selection, not only uniform-mass ones."""
 
     def __init__(self, path: str):
         self.path = path
@@ -117,6 +175,7 @@ class GroTopology(Topology):
         self.resids = np.array([a[0] for a in atoms], dtype=np.int64)
         self.resnames = np.array([a[1] for a in atoms], dtype=object)
         self.names = np.array([a[2] for a in atoms], dtype=object)
+        self.masses = guess_masses(self.names)
         self.n_atoms = len(atoms)
         self.frames = np.stack(frames)  # [n_frames, n_atoms, 3] float32 Angstrom
 

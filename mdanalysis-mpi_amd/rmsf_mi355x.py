@@ -82,8 +82,9 @@ def main(argv=None) -> int:
             rmsf = RMSF(ag, align=align, ref_frame=a.ref_frame, verbose=True).run().results.rmsf
         else:
             # native fallback: GRO or PSF topology + selection subset; XTC, DCD (or
-            # multi-frame GRO) trajectory.  PSF masses feed the mass-weighted
-            # centre of mass RMSF.py uses (RMSF.py:84,94,117,127).
+            # multi-frame GRO) trajectory.  PSF masses (GRO: masses guessed from
+            # the atom names, as MDAnalysis' GROParser does) feed the
+            # mass-weighted centre of mass RMSF.py uses (RMSF.py:84,94,117,127).
             from rmsf_amd.topology import GroTopology, PsfTopology
 
             ext = a.topology.lower().rsplit(".", 1)[-1]

@@ -117,12 +117,13 @@ def test_multi_device_shards(traj, align, run):
     r = RMSF(parts, select=sel, align=align, collect_rmsd=align is not None).run(**run).results
     fl = np.sort(np.arange(len(traj))[slice(run.get("start"), None, run.get("step"))]) if "frames" not in run \
         else np.array(run["frames"])
-    exp = O.rmsf_script(traj[fl], sel, None, size=1, align=align)
+    # the oracle on those frames, with trajectory frame 0 as the reference (RMSF.py:63,80-87)
+    exp = O.rmsf_script(traj[np.concatenate([[0], fl])], sel, None, size=1, align=align, start=1)
     np.testing.assert_allclose(r.rmsf, exp["rmsf"], rtol=0, atol=TOL)
     assert r.n_frames == len(fl) and r.devices == [0, 0, 0]
     assert sum(b1 - b0 for b0, b1 in r.blocks) == len(fl)
     if align is not None:
-        one = RMSF(torch.tensor(traj[fl], device="cuda"), select=sel, align=align, collect_rmsd=True).run()
+        one = RMSF(torch.tensor(traj, device="cuda"), select=sel, align=align, collect_rmsd=True).run(frames=fl)
         np.testing.assert_allclose(r.rmsd, one.results.rmsd, rtol=0, atol=1e-9)
 
 
@@ -144,7 +145,7 @@ def test_multi_reversed_ranges(traj, sl):
     sel = np.arange(1, 700, 6)
     r = RMSF(traj, select=sel, align="average", gpus=[0, 0, 0]).run(**sl).results
     fl = np.sort(np.arange(len(traj))[slice(sl.get("start"), sl.get("stop"), sl["step"])])
-    exp = O.rmsf_script(traj[fl], sel, None, size=3, align="average")
+    exp = O.rmsf_script(traj[np.concatenate([[0], fl])], sel, None, size=3, align="average", start=1)
     np.testing.assert_allclose(r.rmsf, exp["rmsf"], rtol=0, atol=TOL)
     assert r.n_frames == len(fl)
 
@@ -163,11 +164,11 @@ def test_multi_frames_xtc_atomgroup_dcd(tmp_path, traj):
     write_xtc(xp, traj)
     q = xtc_py.read_xtc(xp)
     r = RMSF(xp, select=sel, align="average", gpus=[0, 0]).run(frames=idx).results
-    exp = O.rmsf_script(q[idx], sel, None, size=2, align="average")
+    exp = O.rmsf_script(q[np.concatenate([[0], idx])], sel, None, size=2, align="average", start=1)
     np.testing.assert_allclose(r.rmsf, exp["rmsf"], rtol=0, atol=TOL)
     ag = _FakeAtomGroup(_FakeUniverse(traj), sel, None)
     r = RMSF(ag, align="frame0", masses=np.ones(len(sel)), gpus=[0, 0, 0]).run(frames=idx).results
-    exp = O.rmsf_script(traj[idx], sel, None, size=3, align="frame0")
+    exp = O.rmsf_script(traj[np.concatenate([[0], idx])], sel, None, size=3, align="frame0", start=1)
     np.testing.assert_allclose(r.rmsf, exp["rmsf"], rtol=0, atol=TOL)
     dp = str(tmp_path / "m.dcd")
     write_dcd(dp, traj)
@@ -175,7 +176,7 @@ def test_multi_frames_xtc_atomgroup_dcd(tmp_path, traj):
     mask[idx] = True
     for align in (None, "average"):  # streamed runs; staged into HBM for the two sweeps
         r = RMSF(dp, select=sel, align=align, gpus=[0, 0]).run(frames=mask).results
-        exp = O.rmsf_script(traj[idx], sel, None, size=2, align=align)
+        exp = O.rmsf_script(traj[np.concatenate([[0], idx])], sel, None, size=2, align=align, start=1)
         np.testing.assert_allclose(r.rmsf, exp["rmsf"], rtol=0, atol=TOL)
 
 

@@ -33,9 +33,12 @@ def test_rmsf_from_xtc(tmp_path, align):
     np.testing.assert_allclose(s.results.rmsf, exp, rtol=0, atol=1e-6)
 
 
-def test_script_mode_gro_xtc_native(tmp_path):
+@pytest.mark.parametrize("select", ["protein and name CA", "backbone"])
+def test_script_mode_gro_xtc_native(tmp_path, select):
     """RMSF.py's own input pair (GRO topology + XTC trajectory, "protein and
-    name CA", two-sweep average alignment) end to end without MDAnalysis."""
+    name CA", two-sweep average alignment) end to end without MDAnalysis; the
+    centre of mass weights with masses guessed from the GRO names, as
+    MDAnalysis does (a mixed-element backbone selection exercises it)."""
     import subprocess
     import sys
 
@@ -58,14 +61,17 @@ def test_script_mode_gro_xtc_native(tmp_path):
     write_gro(gro, resids, resnames, names, x[0])
     write_xtc(xtc, x)
     r = subprocess.run([sys.executable, f"{ROOT}/mdanalysis-mpi_amd/rmsf_mi355x.py", "--topology", gro,
-                        "--trajectory", xtc, "--out", out], capture_output=True, text=True, timeout=120)
+                        "--trajectory", xtc, "--out", out, "--select", select], capture_output=True, text=True,
+                       timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "Process:  0 --> Frames:" in r.stdout
-    sel = GroTopology(gro).select("protein and name CA")
-    assert len(sel) == n_res
+    top = GroTopology(gro)
+    sel = top.select(select)
+    assert len(sel) == (n_res if select.endswith("CA") else 4 * n_res)
+    assert len(set(top.masses[sel])) == (1 if select.endswith("CA") else 3)
     with XTCFile(xtc) as f:
         dec = f.read()
-    exp = O.rmsf_script(dec, sel, None, size=1, align="average")["rmsf"]
+    exp = O.rmsf_script(dec, sel, top.masses[sel], size=1, align="average")["rmsf"]
     np.testing.assert_allclose(np.load(out), exp, rtol=0, atol=1e-6)
 
 

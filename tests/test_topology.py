@@ -53,3 +53,24 @@ def test_selections(gro):
                                   np.flatnonzero(np.isin(resnames, ["SOL", "CA"]) & ~np.isin(names, ["HW1", "HW2"])))
     with pytest.raises(ValueError):
         top.select("around 5 protein")
+
+
+def test_guess_masses_like_mdanalysis():
+    """MDAnalysis' name -> element -> mass guess (upstream guessers; restated,
+    unpinned): C-alphas are carbon (also a calcium ion *named* CA -- the
+    upstream quirk), ion names go through the special-name table."""
+    from rmsf_amd.topology import guess_atom_element, guess_masses
+    cases = {"CA": "C", "N": "N", "OW": "O", "HW1": "H", "1HB": "H", "OC1": "O", "SD": "S", "CB": "C",
+             "CLA": "CL", "SOD": "NA", "POT": "K", "CAL": "CA", "ZN": "ZN", "MW": "DUMMY", "NA+": "NA", "P": "P"}
+    for name, el in cases.items():
+        assert guess_atom_element(name) == el, name
+    np.testing.assert_array_equal(guess_masses(["CA", "N", "O", "H", "S", "CAL", "XQ"]),
+                                  [12.011, 14.007, 15.999, 1.008, 32.06, 40.08, 0.0])
+
+
+def test_gro_topology_has_guessed_masses(gro):
+    from rmsf_amd.topology import GroTopology, guess_masses
+    path, _, _, names, _ = gro
+    top = GroTopology(path)
+    np.testing.assert_array_equal(top.masses, guess_masses(names))
+    assert top.masses[list(names).index("CA")] == 12.011
