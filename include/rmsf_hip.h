@@ -198,6 +198,15 @@ int rmsf_calc_rmsd_rotational_matrix(const double *h_ref, const double *h_conf,
                                      const double *h_weights,
                                      double *rmsd_out);
 
+/* ---- scattered frames (RMSF.run(frames=...), RMSF.py:92,124 frame source) --
+ * Compact batch d_dst[k][j][3] (k < n_frames <= 65535, j < n_sel) of the
+ * frames at d_src + d_frames[k]*frame_stride (device int64 indices), the
+ * selection d_sel (NULL = atoms 0..n_sel-1) gathered: one launch per batch
+ * of a scattered frame list instead of kernel launches per frame.           */
+int rmsf_gather_frames(const float *d_src, int64_t frame_stride,
+                       const int64_t *d_frames, int64_t n_frames, int64_t n_sel,
+                       const int32_t *d_sel, float *d_dst, void *stream);
+
 /* ---- synthetic trajectories -------------------------------
  * out[f*frame_stride + 3*a + c] for frames [f0, f0+nf) of n_atoms atoms:
  *   base(a,c) ~ U[0,100), sigma(a) ~ U[0.2,2.0), g ~ triangular, unit var,
@@ -289,6 +298,13 @@ int rmsf_xtcdec_destroy(rmsf_xtcdec *d);
 int rmsf_xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n_frames,
                        int64_t step, void *consumer_stream, int *slot,
                        float **d_frames);
+/* Decode the n_frames frames h_frames[0..n) (any order, repeats allowed;
+ * n_frames <= batch_frames) into the next slot, frame k of the list at
+ * *d_frames + k*3*n_atoms: a run(frames=...) list of scattered frames costs
+ * one batched read + decode instead of one per frame.                      */
+int rmsf_xtcdec_decode_list(rmsf_xtcdec *d, const int64_t *h_frames,
+                            int64_t n_frames, void *consumer_stream, int *slot,
+                            float **d_frames);
 /* The same into the caller's device buffer: frame k of the batch at
  * d_out + k*out_stride floats (e.g. a trajectory kept resident in HBM). */
 int rmsf_xtcdec_decode_into(rmsf_xtcdec *d, int64_t f0, int64_t n_frames,
@@ -401,6 +417,16 @@ int rmsf_push_frames(rmsf_ctx *ctx, const float *xyz, int64_t n_frames,
  * Synchronises at the end to report corrupt frames.                          */
 int rmsf_push_xtc(rmsf_ctx *ctx, const rmsf_xtc *x, int64_t f0,
                   int64_t n_frames, int64_t step, int mode);
+
+/* Push the XTC frames h_frames[0..n) (a frame list, e.g. run(frames=...)):
+ * decoded on the GPU in batches of scattered records, one wait at the end. */
+int rmsf_push_xtc_frames(rmsf_ctx *ctx, const rmsf_xtc *x, const int64_t *h_frames,
+                         int64_t n_frames, int mode);
+/* Push n_frames host frames given as one pointer per frame (n_atoms float32
+ * atoms each; e.g. the rows of a frame list, or per-Timestep buffers): the
+ * stager gathers the selection from every frame into its pinned slots.      */
+int rmsf_push_frame_ptrs(rmsf_ctx *ctx, const float *const *h_ptrs,
+                         int64_t n_frames, int mode);
 
 /* Running Welford partial (RMSF.py:120-121,137-138): *n frames, mean and M2
  * f64 [n_sel][3] (any output may be NULL).  Synchronises.                    */

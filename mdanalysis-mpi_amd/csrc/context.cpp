@@ -709,30 +709,34 @@ RMSF_EXPORT int rmsf_push_frames(rmsf_ctx *c, const float *xyz, int64_t n_frames
   return RMSF_OK;
 }
 
-RMSF_EXPORT int rmsf_push_xtc(rmsf_ctx *c, const rmsf_xtc *x, int64_t f0, int64_t n_frames, int64_t step, int mode) {
-  CX_OK(check_ctx(c, "rmsf_push_xtc"));
-  CX_OK(check_mode(mode, "rmsf_push_xtc"));
-  if (!x || n_frames < 0 || step < 1 || f0 < 0) return fail(RMSF_EINVAL, "rmsf_push_xtc: bad arguments");
-  if (n_frames == 0) return RMSF_OK;
-  if (x->n_atoms != c->n_atoms) return fail(RMSF_EINVAL, "rmsf_push_xtc: the file's atom count differs");
-  DeviceScope ds(c->dev);
-  // the records are decompressed on the GPU (csrc/xtc_gpu.hip) into full
-  // frames; the accumulate kernels gather the selection
-  constexpr int kSlots = 3;
+}  // extern "C"
+
+namespace {
+
+// The context's GPU XTC decoder for file x (made on first use, remade for another file).
+int ensure_xdec(rmsf_ctx *c, const rmsf_xtc *x, int n_slots, int64_t *batch) {
+  *batch = std::max<int64_t>(1, std::min<int64_t>(4096, (int64_t(2) << 30) / (12 * c->n_atoms)));
   if (!c->xdec || c->xdec_serial != x->serial) {
     if (c->xdec) CX_OK(rmsf_xtcdec_destroy(c->xdec));
     c->xdec = nullptr;
-    const int64_t batch = std::max<int64_t>(1, std::min<int64_t>(4096, (int64_t(2) << 30) / (12 * c->n_atoms)));
-    CX_OK(rmsf_xtcdec_create(x, batch, kSlots, 16, &c->xdec));
+    CX_OK(rmsf_xtcdec_create(x, *batch, n_slots, 16, &c->xdec));
     c->xdec_serial = x->serial;
   }
-  const int64_t batch = std::max<int64_t>(1, std::min<int64_t>(4096, (int64_t(2) << 30) / (12 * c->n_atoms)));
+  return RMSF_OK;
+}
+
+// Decode n_frames frames batch by batch (decode(i, n, &slot, &d) queues batch
+// frames i..i+n) with up to kSlots decodes in flight ahead of the kernels,
+// then wait once and report corrupt frames.
+template <class Decode>
+int push_decoded(rmsf_ctx *c, int64_t n_frames, int64_t batch, int mode, Decode &&decode) {
+  constexpr size_t kSlots = 3;
   struct Pending {
     int slot;
     float *d;
     int64_t n;
   };
-  std::vector<Pending> q;  // up to kSlots decodes in flight ahead of the kernels
+  std::vector<Pending> q;
   size_t head = 0;
   auto consume = [&]() -> int {
     const Pending p = q[head++];
@@ -742,12 +746,68 @@ RMSF_EXPORT int rmsf_push_xtc(rmsf_ctx *c, const rmsf_xtc *x, int64_t f0, int64_
   };
   for (int64_t i = 0; i < n_frames; i += batch) {
     Pending p{-1, nullptr, std::min(batch, n_frames - i)};
-    CX_OK(rmsf_xtcdec_decode(c->xdec, f0 + i * step, p.n, step, c->stream, &p.slot, &p.d));
+    CX_OK(decode(i, p.n, &p.slot, &p.d));
     q.push_back(p);
-    if (q.size() - head >= (size_t)kSlots) CX_OK(consume());
+    if (q.size() - head >= kSlots) CX_OK(consume());
   }
   while (head < q.size()) CX_OK(consume());
   return rmsf_xtcdec_synchronize(c->xdec);
+}
+
+}  // namespace
+
+extern "C" {
+
+RMSF_EXPORT int rmsf_push_xtc(rmsf_ctx *c, const rmsf_xtc *x, int64_t f0, int64_t n_frames, int64_t step, int mode) {
+  CX_OK(check_ctx(c, "rmsf_push_xtc"));
+  CX_OK(check_mode(mode, "rmsf_push_xtc"));
+  if (!x || n_frames < 0 || step < 1 || f0 < 0) return fail(RMSF_EINVAL, "rmsf_push_xtc: bad arguments");
+  if (n_frames == 0) return RMSF_OK;
+  if (x->n_atoms != c->n_atoms) return fail(RMSF_EINVAL, "rmsf_push_xtc: the file's atom count differs");
+  DeviceScope ds(c->dev);
+  // the records are decompressed on the GPU (csrc/xtc_gpu.hip) into full
+  // frames; the accumulate kernels gather the selection
+  int64_t batch = 0;
+  CX_OK(ensure_xdec(c, x, 3, &batch));
+  return push_decoded(c, n_frames, batch, mode, [&](int64_t i, int64_t n, int *slot, float **d) {
+    return rmsf_xtcdec_decode(c->xdec, f0 + i * step, n, step, c->stream, slot, d);
+  });
+}
+
+RMSF_EXPORT int rmsf_push_xtc_frames(rmsf_ctx *c, const rmsf_xtc *x, const int64_t *h_frames, int64_t n_frames,
+                                     int mode) {
+  CX_OK(check_ctx(c, "rmsf_push_xtc_frames"));
+  CX_OK(check_mode(mode, "rmsf_push_xtc_frames"));
+  if (!x || n_frames < 0 || (n_frames > 0 && !h_frames)) return fail(RMSF_EINVAL, "rmsf_push_xtc_frames: bad arguments");
+  if (n_frames == 0) return RMSF_OK;
+  if (x->n_atoms != c->n_atoms) return fail(RMSF_EINVAL, "rmsf_push_xtc_frames: the file's atom count differs");
+  DeviceScope ds(c->dev);
+  int64_t batch = 0;
+  CX_OK(ensure_xdec(c, x, 3, &batch));
+  return push_decoded(c, n_frames, batch, mode, [&](int64_t i, int64_t n, int *slot, float **d) {
+    return rmsf_xtcdec_decode_list(c->xdec, h_frames + i, n, c->stream, slot, d);
+  });
+}
+
+RMSF_EXPORT int rmsf_push_frame_ptrs(rmsf_ctx *c, const float *const *h_ptrs, int64_t n_frames, int mode) {
+  CX_OK(check_ctx(c, "rmsf_push_frame_ptrs"));
+  CX_OK(check_mode(mode, "rmsf_push_frame_ptrs"));
+  if (n_frames < 0 || (n_frames > 0 && !h_ptrs)) return fail(RMSF_EINVAL, "rmsf_push_frame_ptrs: bad arguments");
+  if (n_frames == 0) return RMSF_OK;
+  DeviceScope ds(c->dev);
+  if (ds.err != hipSuccess) return fail(RMSF_EHIP, "rmsf_push_frame_ptrs: hipSetDevice failed");
+  CX_OK(ensure_stager(c));
+  for (int64_t f = 0; f < n_frames; f += c->stage_batch) {
+    const int64_t nf = std::min(c->stage_batch, n_frames - f);
+    int slot = -1;
+    float *d = nullptr;
+    CX_OK(rmsf_stager_stage_ptrs(c->stager, h_ptrs + f, nf, c->stream, &slot, &d));
+    int rc = process(c, d, 3 * c->n_sel, nf, nullptr, mode);
+    int rc2 = rmsf_stager_release(c->stager, slot, c->stream);
+    CX_OK(rc);
+    CX_OK(rc2);
+  }
+  return RMSF_OK;
 }
 
 RMSF_EXPORT int rmsf_get_partial(rmsf_ctx *c, int64_t *n, double *h_mean, double *h_m2) {

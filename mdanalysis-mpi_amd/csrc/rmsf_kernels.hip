@@ -1175,6 +1175,21 @@ __host__ __device__ inline uint64_t skey(uint64_t seed, uint64_t stream, uint64_
   return sm64(sm64(sm64(seed ^ (stream * 0xD1B54A32D192ED03ull)) + i) + j);
 }
 
+// k_gather_frames: compact batch of scattered frames (a run(frames=...) list):
+// dst[k][j] = the selected atom j of frame src + frames[k]*fstride, one float
+// per thread, grid = (coordinate blocks, frames).
+template <bool GATHER>
+__global__ __launch_bounds__(kBlock) void k_gather_frames(const float *__restrict__ src, int64_t fstride,
+                                                          const int64_t *__restrict__ frames, int64_t n_sel,
+                                                          const int32_t *__restrict__ sel, float *__restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= 3 * n_sel) return;
+  const int64_t k = blockIdx.y;
+  const float *fr = src + frames[k] * fstride;
+  const int64_t a = i / 3, c = i - 3 * a;
+  dst[k * 3 * n_sel + i] = __builtin_nontemporal_load(fr + (GATHER ? 3 * (int64_t)sel[a] + c : i));
+}
+
 __global__ __launch_bounds__(kBlock) void k_synth(float *__restrict__ out, int64_t fstride, int64_t n_atoms,
                                                   int64_t f0, int64_t nf, uint64_t seed,
                                                   const double *__restrict__ motion) {
@@ -1690,6 +1705,22 @@ RMSF_EXPORT int rmsf_calc_rmsd_rotational_matrix(const double *h_ref, const doub
   } while (0);
   (void)hipFree(d);
   return rc;
+}
+
+RMSF_EXPORT int rmsf_gather_frames(const float *d_src, int64_t fstride, const int64_t *d_frames, int64_t n_frames,
+                                   int64_t n_sel, const int32_t *d_sel, float *d_dst, void *stream) {
+  if (!d_src || !d_frames || !d_dst || n_frames < 0 || n_sel < 1 || fstride < (d_sel ? 3 : 3 * n_sel))
+    return fail(RMSF_EINVAL, "rmsf_gather_frames: bad arguments");
+  if (n_frames == 0) return RMSF_OK;
+  if (n_frames > 65535) return fail(RMSF_EINVAL, "rmsf_gather_frames: at most 65535 frames per call");
+  const dim3 grid((unsigned)grid1(3 * n_sel), (unsigned)n_frames);
+  if (d_sel)
+    hipLaunchKernelGGL(k_gather_frames<true>, grid, dim3(kBlock), 0, S(stream), d_src, fstride, d_frames, n_sel, d_sel,
+                       d_dst);
+  else
+    hipLaunchKernelGGL(k_gather_frames<false>, grid, dim3(kBlock), 0, S(stream), d_src, fstride, d_frames, n_sel,
+                       d_sel, d_dst);
+  return after_launch("k_gather_frames");
 }
 
 RMSF_EXPORT int rmsf_synth_frames(float *d_out, int64_t fstride, int64_t n_atoms, int64_t f0, int64_t nf,

@@ -729,6 +729,7 @@ struct rmsf_xtcdec {
     hipEvent_t done = nullptr, released = nullptr;
     int64_t pending = 0;  // frames whose status is not yet checked
     int64_t f0 = 0, step = 1;
+    std::vector<int64_t> list;  // the frames of a list decode (else f0 + k*step)
   };
   std::vector<Slot> slots;
   int next = 0;
@@ -743,7 +744,8 @@ int check_slot(rmsf_xtcdec *d, rmsf_xtcdec::Slot &s) {
   s.pending = 0;
   for (int64_t k = 0; k < n; ++k)
     if (s.h_status[k] != kOk)
-      return fail(RMSF_EINVAL, "xtc (GPU decode): frame " + std::to_string(s.f0 + k * s.step) + ": " +
+      return fail(RMSF_EINVAL, "xtc (GPU decode): frame " +
+                                   std::to_string(s.list.empty() ? s.f0 + k * s.step : s.list[k]) + ": " +
                                    status_text(s.h_status[k]));
   return RMSF_OK;
 }
@@ -856,8 +858,9 @@ namespace {
 // out == nullptr: into the slot's own frame buffer (allocated on first use),
 // reused once the consumer released the slot; otherwise into the caller's
 // buffer, frame k at out + k*out_stride.
+// list != nullptr: the frames list[0..n) in that order (f0/step unused).
 int xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_t step, float *out, int64_t out_stride,
-                  void *consumer_stream, int *slot, float **d_frames) {
+                  void *consumer_stream, int *slot, float **d_frames, const int64_t *list = nullptr) {
   const int si = d->next;
   d->next = (d->next + 1) % (int)d->slots.size();
   auto &s = d->slots[si];
@@ -868,7 +871,8 @@ int xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_t step, float *ou
   int64_t *off = s.h_tab, *len = s.h_tab + d->batch;
   size_t total = 0;
   bool copied = false;
-  if (step == 1) {
+  auto frame = [&](int64_t k) { return list ? list[k] : f0 + k * step; };
+  if (!list && step == 1) {
     const int64_t a = x->offset[f0], e = x->offset[f0 + n - 1] + x->size[f0 + n - 1];
     total = (size_t)(e - a);
     if (total > s.raw_cap) return fail(RMSF_EINVAL, "rmsf_xtcdec_decode: batch larger than the slot");
@@ -910,7 +914,7 @@ int xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_t step, float *ou
     }
   } else {
     for (int64_t k = 0; k < n; ++k) {
-      const int64_t f = f0 + k * step;
+      const int64_t f = frame(k);
       off[k] = (int64_t)(total / 4);
       len[k] = x->size[f] / 4;
       total += (size_t)x->size[f];
@@ -918,7 +922,7 @@ int xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_t step, float *ou
     if (total > s.raw_cap) return fail(RMSF_EINVAL, "rmsf_xtcdec_decode: batch larger than the slot");
     std::vector<char> ok(n, 1);
     d->pool->run(n, [&](int64_t k) {
-      const int64_t f = f0 + k * step;
+      const int64_t f = frame(k);
       ok[k] = rmsf_internal_pread_all(x->fd, s.h_raw + 4 * off[k], (size_t)x->size[f], x->offset[f]);
     });
     for (char c : ok)
@@ -945,6 +949,8 @@ int xtcdec_decode(rmsf_xtcdec *d, int64_t f0, int64_t n, int64_t step, float *ou
   s.pending = n;
   s.f0 = f0;
   s.step = step;
+  if (list) s.list.assign(list, list + n);
+  else s.list.clear();
   *slot = si;
   if (d_frames) *d_frames = out;
   return RMSF_OK;
@@ -968,6 +974,17 @@ RMSF_EXPORT int rmsf_xtcdec_decode_into(rmsf_xtcdec *d, int64_t f0, int64_t n, i
       f0 + (n - 1) * step >= (int64_t)d->x->offset.size())
     return fail(RMSF_EINVAL, "rmsf_xtcdec_decode_into: bad arguments");
   return xtcdec_decode(d, f0, n, step, d_out, out_stride, consumer_stream, slot, nullptr);
+}
+
+RMSF_EXPORT int rmsf_xtcdec_decode_list(rmsf_xtcdec *d, const int64_t *h_frames, int64_t n, void *consumer_stream,
+                                        int *slot, float **d_frames) {
+  if (!d || !h_frames || !slot || !d_frames || n < 1 || n > d->batch)
+    return fail(RMSF_EINVAL, "rmsf_xtcdec_decode_list: bad arguments");
+  const int64_t nf = (int64_t)d->x->offset.size();
+  for (int64_t k = 0; k < n; ++k)
+    if (h_frames[k] < 0 || h_frames[k] >= nf)
+      return fail(RMSF_EINVAL, "rmsf_xtcdec_decode_list: frame " + std::to_string(h_frames[k]) + " out of range");
+  return xtcdec_decode(d, 0, n, 1, nullptr, 0, consumer_stream, slot, d_frames, h_frames);
 }
 
 RMSF_EXPORT int rmsf_xtcdec_release(rmsf_xtcdec *d, int slot, void *consumer_stream) {

@@ -71,6 +71,7 @@ SIGNATURES = {
     "rmsf_qcp_batch": (c_int, [P, P, P, c_int64, P, P, P]),
     "rmsf_calc_rmsd_rotational_matrix": (c_int, [P, P, c_int64, P, P, POINTER(c_double)]),
     "rmsf_synth_frames": (c_int, [P, c_int64, c_int64, c_int64, c_int64, c_uint64, P, P]),
+    "rmsf_gather_frames": (c_int, [P, c_int64, P, c_int64, c_int64, P, P, P]),
     "rmsf_stager_create": (c_int, [c_int64, c_int64, P, c_int64, c_int, c_int, POINTER(c_void_p)]),
     "rmsf_stager_destroy": (c_int, [P]),
     "rmsf_stager_stage": (c_int, [P, P, c_int64, c_int64, P, POINTER(c_int), POINTER(c_void_p)]),
@@ -88,6 +89,7 @@ SIGNATURES = {
     "rmsf_xtcdec_destroy": (c_int, [P]),
     "rmsf_xtcdec_decode": (c_int, [P, c_int64, c_int64, c_int64, P, POINTER(c_int), POINTER(c_void_p)]),
     "rmsf_xtcdec_decode_into": (c_int, [P, c_int64, c_int64, c_int64, P, c_int64, P, POINTER(c_int)]),
+    "rmsf_xtcdec_decode_list": (c_int, [P, P, c_int64, P, POINTER(c_int), POINTER(c_void_p)]),
     "rmsf_xtcdec_release": (c_int, [P, c_int, P]),
     "rmsf_xtcdec_synchronize": (c_int, [P]),
     "rmsf_xtc_decode_records": (c_int, [P, P, P, c_int64, c_int64, P, c_int64, P, P]),
@@ -108,6 +110,8 @@ SIGNATURES = {
     "rmsf_set_reference_average": (c_int, [P]),
     "rmsf_push_frames": (c_int, [P, P, c_int64, c_int64, c_int, c_int]),
     "rmsf_push_xtc": (c_int, [P, P, c_int64, c_int64, c_int64, c_int]),
+    "rmsf_push_xtc_frames": (c_int, [P, P, P, c_int64, c_int]),
+    "rmsf_push_frame_ptrs": (c_int, [P, P, c_int64, c_int]),
     "rmsf_get_partial": (c_int, [P, POINTER(c_int64), P, P]),
     "rmsf_get_sum": (c_int, [P, POINTER(c_int64), P]),
     "rmsf_get_average": (c_int, [P, P]),

@@ -198,6 +198,24 @@ class Context:
         n = len(range(start, stop, step))
         call("rmsf_push_xtc", self._h, xtc.handle, start, n, step, mode)
 
+    def push_xtc_frames(self, xtc, frames, mode: int = PUSH_WELFORD) -> None:
+        """Push the XTC frames ``frames`` (a frame list: scattered records are
+        read and decoded in batches, one wait at the end)."""
+        f = np.ascontiguousarray(frames, dtype=np.int64)
+        call("rmsf_push_xtc_frames", self._h, xtc.handle, f.ctypes.data, f.size, mode)
+
+    def push_rows(self, frames: np.ndarray, rows, mode: int = PUSH_WELFORD) -> None:
+        """Push rows ``rows`` of a host float32 trajectory [F, n_atoms, 3]
+        (any frame list) as one pointer per frame through the stager."""
+        a = frames
+        if a.dtype != np.float32 or not a.flags.c_contiguous or a.ndim != 3 or a.shape[1] != self.n_atoms:
+            raise ValueError("push_rows: a C-contiguous float32 [F, n_atoms, 3] host array is required")
+        r = np.asarray(rows, dtype=np.int64)
+        if r.size and (r.min() < 0 or r.max() >= a.shape[0]):
+            raise IndexError("push_rows: row out of range")
+        ptrs = (a.ctypes.data + r * (a.strides[0])).astype(np.uint64)
+        call("rmsf_push_frame_ptrs", self._h, ptrs.ctypes.data, r.size, mode)
+
     # -- results --------------------------------------------------------------
     def partial(self):
         n = ctypes.c_int64()

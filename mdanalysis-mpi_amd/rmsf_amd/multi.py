@@ -66,6 +66,14 @@ class _HostFrames:
             # rows is an arithmetic range: a strided view, pushed with its step
             ctx.push(self.arr[rows.start:rows[-1] + 1], mode, step=rows.step)
 
+    def push_block(self, ctx: Context, runs: list, mode: int) -> None:
+        """A block of several runs (a scattered frame list): one push of one
+        pointer per frame, batched by the stager, instead of one per run."""
+        if len(runs) == 1:
+            self.push(ctx, runs[0], mode)
+        elif runs:
+            ctx.push_rows(self.arr, np.concatenate([np.arange(r.start, r.stop, r.step) for r in runs]), mode)
+
     def n_sel(self) -> int:
         return self.n_atoms if self.sel is None else len(self.sel)
 
@@ -88,14 +96,15 @@ class _HostFrames:
             st = Stager(self.n_atoms, ns, self.sel, batch, 3, 4)
             stream = torch.cuda.current_stream(dev).cuda_stream
             try:
-                row = 0
-                for rows in runs:
-                    for i in range(0, len(rows), batch):
-                        n = min(batch, len(rows) - i)
-                        slot, ptr = st.stage(self.arr, rows[i], rows.step, n, stream)
-                        cache.fill(row, 1, n, ptr, stream)
-                        st.release(slot, stream)
-                        row += n
+                # every frame of the block by address: a scattered frame list
+                # fills whole stager batches too
+                frames = np.concatenate([np.arange(r.start, r.stop, r.step) for r in runs])
+                addr = (self.arr.ctypes.data + frames * self.arr.strides[0]).astype(np.uint64)
+                for row in range(0, total, batch):
+                    n = min(batch, total - row)
+                    slot, ptr = st.stage_ptrs(addr[row:row + n], stream)
+                    cache.fill(row, 1, n, ptr, stream)
+                    st.release(slot, stream)
                 torch.cuda.current_stream(dev).synchronize()
             finally:
                 st.close()
@@ -120,6 +129,14 @@ class _XtcFrames:
     def push(self, ctx: Context, rows: range, mode: int) -> None:
         if len(rows):
             ctx.push_xtc(self.xtc, rows.start, rows[-1] + 1, rows.step, mode)
+
+    def push_block(self, ctx: Context, runs: list, mode: int) -> None:
+        """A block of several runs: the scattered records are decoded in
+        batches by one push (one wait), not one blocking decode per run."""
+        if len(runs) == 1:
+            self.push(ctx, runs[0], mode)
+        elif runs:
+            ctx.push_xtc_frames(self.xtc, np.concatenate([np.arange(r.start, r.stop, r.step) for r in runs]), mode)
 
 
 class _DcdFrames:
@@ -378,6 +395,8 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
             elif isinstance(src, _DeviceShards):
                 for r in blocks[i]:
                     src.push_on(i, c, r, mode)
+            elif hasattr(src, "push_block"):
+                src.push_block(c, blocks[i], mode)
             else:
                 for r in blocks[i]:
                     src.push(c, r, mode)

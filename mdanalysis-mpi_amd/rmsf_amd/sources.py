@@ -68,6 +68,13 @@ class Stager:
              ctypes.byref(dptr))
         return slot.value, dptr.value
 
+    def stage_ptrs(self, ptrs: np.ndarray, stream: int) -> tuple[int, int]:
+        """Stage the frames at host addresses ``ptrs`` (uint64, one per frame)."""
+        p = np.ascontiguousarray(ptrs, dtype=np.uint64)
+        slot, dptr = ctypes.c_int(), ctypes.c_void_p()
+        call("rmsf_stager_stage_ptrs", self._h, p.ctypes.data, p.size, stream, ctypes.byref(slot), ctypes.byref(dptr))
+        return slot.value, dptr.value
+
     def stage_compact(self, buf: np.ndarray, n: int, stream: int) -> tuple[int, int]:
         slot, dptr = ctypes.c_int(), ctypes.c_void_p()
         call("rmsf_stager_stage", self._h, buf.ctypes.data, buf.shape[1] * 3, n, stream, ctypes.byref(slot),
@@ -163,6 +170,46 @@ class FrameList:
             i = j
 
 
+SCATTER_RUN = 8  # a frame list whose runs average fewer frames is read as gathered batches
+
+
+def _scattered(frames: FrameList, b0: int, b1: int, nb: int) -> bool:
+    """An explicit frame list whose block [b0, b1) is mostly short runs: read
+    it as compact batches of up to ``nb`` frames (one gather / stage / decode
+    each) instead of one batch -- and one set of kernel launches -- per run."""
+    if frames.idx is None or b1 <= b0:
+        return False
+    return (b1 - b0) < SCATTER_RUN * sum(1 for _ in frames.runs(b0, b1, nb))
+
+
+def _list_runs(rows: np.ndarray):
+    """(first, step, n) runs of a sorted row list (arithmetic progressions)."""
+    fl = FrameList(int(rows.max()) + 1 if rows.size else 0, frames=rows)
+    return fl.runs(0, len(rows), max(1, len(rows)))
+
+
+class _Gather:
+    """A device scratch batch [nb, n_sel, 3] filled by rmsf_gather_frames from
+    HBM-resident frames: one launch per batch of scattered frames.  Reused
+    batch after batch -- the kernels that read it are queued on the same
+    stream before the next gather."""
+
+    def __init__(self, n_sel: int, nb: int, device):
+        self.n_sel = n_sel
+        self.buf = torch.empty((nb, n_sel, 3), dtype=torch.float32, device=device)
+
+    def __call__(self, base_ptr: int, fstride: int, rows: np.ndarray, sel: torch.Tensor | None, stream: int) -> Batch:
+        idx = torch.as_tensor(np.ascontiguousarray(rows, dtype=np.int64)).to(self.buf.device)
+        call("rmsf_gather_frames", base_ptr, fstride, idx.data_ptr(), len(rows), self.n_sel,
+             None if sel is None else sel.data_ptr(), self.buf.data_ptr(), stream)
+        return Batch(self.buf.data_ptr(), 3 * self.n_sel, len(rows), None)
+
+
+def _gather_batch_frames(n_sel: int, nb: int) -> int:
+    """Frames per gathered batch: the pipeline's batch, at most ~256 MB of scratch."""
+    return max(1, min(nb, 65535, (256 << 20) // max(1, 12 * n_sel)))
+
+
 class DeviceSource:
     """HBM-resident float32 trajectory [F_local, n_atoms, 3] holding global frames
     [offset, offset + F_local) of a trajectory with ``n_traj`` frames."""
@@ -204,6 +251,16 @@ class DeviceSource:
         return self.traj.shape[0]
 
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
+        if _scattered(frames, b0, b1, max_frames):
+            nb = _gather_batch_frames(self.n_sel, max_frames)
+            g = _Gather(self.n_sel, nb, self.traj.device)
+            idx = frames.idx[b0:b1]
+            for i in range(0, len(idx), nb):
+                part = idx[i:i + nb]
+                _check_run(self, int(part[0]), 1, 1, "HBM shard")
+                _check_run(self, int(part[-1]), 1, 1, "HBM shard")
+                yield g(self.traj.data_ptr(), self.fstride, part - self.offset, self.sel_dev, stream)
+            return
         for first, step, n in frames.runs(b0, b1, max_frames):
             _check_run(self, first, step, n, "HBM shard")
             yield Batch(self._ptr(first), self.fstride * step, n, self.sel_dev)
@@ -257,6 +314,27 @@ class FrameCache:
 
     def drop(self) -> None:
         self.have[:] = False
+
+    def fill_rows(self, rows: np.ndarray, src_ptr: int, stream: int) -> None:
+        """Copy a compact batch (frame k = rows[k]) into its rows, run by run."""
+        w = 12 * self.n_sel
+        k = 0
+        for first, step, n in _list_runs(rows):
+            call("rmsf_memcpy2d_d2d", self.ptr(first), w * step, src_ptr + w * k, w, w, n, stream)
+            k += n
+        self.have[rows] = True
+
+
+def _cached_list(cache: FrameCache | None, gather, rows: np.ndarray, stream: int, stage) -> Batch:
+    """Rows ``rows`` (a scattered list) of a host source as one compact batch:
+    gathered from ``cache`` when all are resident; otherwise ``stage(rows)``
+    -> compact Batch, copied into the cache when there is one."""
+    if cache is not None and cache.have[rows].all():
+        return gather(cache.buf.data_ptr(), 3 * cache.n_sel, rows, None, stream)
+    b = stage(rows)
+    if cache is not None:
+        cache.fill_rows(rows, b.ptr, stream)
+    return b
 
 
 def _cached_stage(cache: FrameCache | None, row: int, step: int, n: int, stream: int, stage) -> Batch:
@@ -328,7 +406,23 @@ class HostSource:
         return self._stage(self._row(frame), 1, 1, stream)
 
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
-        for first, step, n in frames.runs(b0, b1, min(max_frames, self.batch_frames)):
+        nb = min(max_frames, self.batch_frames)
+        if _scattered(frames, b0, b1, nb):
+            g = _Gather(self.n_sel, nb, self.cache.buf.device) if self.cache is not None else None
+            idx = frames.idx[b0:b1]
+            fb = self.traj.strides[0]
+
+            def stage(rows):
+                slot, ptr = self.stager.stage_ptrs(self.traj.ctypes.data + rows * fb, stream)
+                return Batch(ptr, 3 * self.n_sel, len(rows), None, lambda: self.stager.release(slot, stream))
+
+            for i in range(0, len(idx), nb):
+                part = idx[i:i + nb]
+                _check_run(self, int(part[0]), 1, 1, "host shard")
+                _check_run(self, int(part[-1]), 1, 1, "host shard")
+                yield _cached_list(self.cache, g, part - self.offset, stream, stage)
+            return
+        for first, step, n in frames.runs(b0, b1, nb):
             _check_run(self, first, step, n, "host shard")
             yield self._stage(self._row(first), step, n, stream)
 
@@ -348,6 +442,13 @@ class XtcDecoder:
     def decode(self, first: int, n: int, step: int, stream: int) -> tuple[int, int]:
         slot, dptr = ctypes.c_int(), ctypes.c_void_p()
         call("rmsf_xtcdec_decode", self._h, first, n, step, stream, ctypes.byref(slot), ctypes.byref(dptr))
+        return slot.value, dptr.value
+
+    def decode_list(self, frames: np.ndarray, stream: int) -> tuple[int, int]:
+        """Decode the frames ``frames`` (any list) into the next slot, in order."""
+        f = np.ascontiguousarray(frames, dtype=np.int64)
+        slot, dptr = ctypes.c_int(), ctypes.c_void_p()
+        call("rmsf_xtcdec_decode_list", self._h, f.ctypes.data, f.size, stream, ctypes.byref(slot), ctypes.byref(dptr))
         return slot.value, dptr.value
 
     def decode_into(self, first: int, n: int, step: int, out_ptr: int, out_stride: int, stream: int) -> int:
@@ -407,6 +508,7 @@ class XtcSource:
                 batch_frames = max(1, min(4096, (2 << 30) // max(1, 12 * self.n_atoms)))
             self.decoder = XtcDecoder(self.xtc, batch_frames, n_slots, n_threads)
             self.cache = None
+            self._gather = None  # scratch for scattered frame lists served from the cache
             if cache:
                 need = 12 * self.n_atoms * self.n_traj
                 free, _ = torch.cuda.mem_get_info()
@@ -476,13 +578,41 @@ class XtcSource:
         self._check()
         return b
 
+    def _list_batch(self, part: np.ndarray, stream: int) -> list[Batch]:
+        """Frames ``part`` of an explicit frame list (scattered records):
+        decoded as ONE batch (rmsf_xtcdec_decode_list) instead of one decode
+        per run; with the HBM cache their rows are copied in, and a batch whose
+        frames are all resident is served from the cache run by run."""
+        fs = 3 * self.n_atoms
+        if self.cache is not None and self._cached[part].all():
+            if self._gather is None or self._gather.buf.shape[0] < len(part):
+                self._gather = _Gather(self.n_sel, self.batch_frames, self.cache.device)
+            return [self._gather(self.cache.data_ptr(), fs, part, self.sel_dev, stream)]
+        slot, ptr = self.decoder.decode_list(part, stream)
+        if self.cache is not None:
+            w = 4 * fs
+            k = 0
+            for first, step, n in FrameList(self.n_traj, frames=part).runs(0, len(part), len(part)):
+                call("rmsf_memcpy2d_d2d", self.cache.data_ptr() + w * first, w * step, ptr + w * k, w, w, n, stream)
+                k += n
+            self._cached[part] = True
+        return [Batch(ptr, fs, len(part), self.sel_dev, lambda: self.decoder.release(slot, stream))]
+
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
         ahead = self.decoder.n_slots - 1 if self.decode_on == "gpu" else 0
         queue = []
-        for first, step, n in frames.runs(b0, b1, min(max_frames, self.batch_frames)):
-            queue.append(self._stage(first, step, n, stream))
-            if len(queue) > ahead:
-                yield queue.pop(0)
+        nb = min(max_frames, self.batch_frames)
+        if self.decode_on == "gpu" and _scattered(frames, b0, b1, nb):
+            idx = frames.idx[b0:b1]
+            for i in range(0, len(idx), nb):
+                queue.extend(self._list_batch(idx[i:i + nb], stream))
+                while len(queue) > ahead:
+                    yield queue.pop(0)
+        else:
+            for first, step, n in frames.runs(b0, b1, nb):
+                queue.append(self._stage(first, step, n, stream))
+                if len(queue) > ahead:
+                    yield queue.pop(0)
         while queue:
             yield queue.pop(0)
         self._check()
@@ -533,7 +663,20 @@ class DcdSource:
         return self._stage(frame, 1, 1, stream)
 
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
-        for first, step, n in frames.runs(b0, b1, min(max_frames, self.batch_frames)):
+        nb = min(max_frames, self.batch_frames)
+        if _scattered(frames, b0, b1, nb):
+            g = _Gather(self.n_sel, nb, self.cache.buf.device) if self.cache is not None else None
+
+            def stage(rows):
+                buf = np.concatenate([self.f.read(first, n, step, self.sel) for first, step, n in _list_runs(rows)])
+                slot, ptr = self.stager.stage_compact(buf, len(rows), stream)
+                return Batch(ptr, 3 * self.n_sel, len(rows), None, lambda: self.stager.release(slot, stream))
+
+            idx = frames.idx[b0:b1]
+            for i in range(0, len(idx), nb):
+                yield _cached_list(self.cache, g, idx[i:i + nb], stream, stage)
+            return
+        for first, step, n in frames.runs(b0, b1, nb):
             yield self._stage(first, step, n, stream)
 
 
@@ -584,7 +727,23 @@ class AtomGroupSource:
         return _cached_stage(self.cache, frame, 1, 1, stream, stage)
 
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
-        for first, step, n in frames.runs(b0, b1, min(max_frames, self.batch_frames)):
+        nb = min(max_frames, self.batch_frames)
+        if _scattered(frames, b0, b1, nb):
+            g = _Gather(self.n_sel, nb, self.cache.buf.device) if self.cache is not None else None
+
+            def stage_list(rows):
+                buf = self._buf()
+                for j, f in enumerate(rows):
+                    self.traj[int(f)]
+                    buf[j] = self.ag.positions
+                slot, ptr = self.stager.stage_compact(buf, len(rows), stream)
+                return Batch(ptr, 3 * self.n_sel, len(rows), None, lambda: self.stager.release(slot, stream))
+
+            idx = frames.idx[b0:b1]
+            for i in range(0, len(idx), nb):
+                yield _cached_list(self.cache, g, idx[i:i + nb], stream, stage_list)
+            return
+        for first, step, n in frames.runs(b0, b1, nb):
 
             def stage(first=first, step=step, n=n):
                 buf = self._buf()

@@ -220,3 +220,41 @@ def test_explicit_frames(c1, align, where):
     np.testing.assert_allclose(got.rmsf, exp.rmsf, rtol=0, atol=1e-9)
     ref = O.rmsf_script(traj[mask], d["sel"], None, size=1, align=align)["rmsf"]
     np.testing.assert_allclose(got.rmsf, ref, rtol=0, atol=TOL)
+
+
+@pytest.mark.parametrize("align", [None, "average"])
+@pytest.mark.parametrize("where", ["device", "host", "host_cache", "dcd", "atomgroup"])
+def test_scattered_frames_gathered_batches(tmp_path, c1, align, where):
+    """A scattered frame list (runs of 1-2 frames) is read as compact gathered
+    batches -- rmsf_gather_frames from HBM (and from the HBM frame cache on the
+    second sweep), pointer-staged host rows, per-run DCD reads, per-frame
+    AtomGroup positions -- one set of launches per batch instead of per run;
+    equal to the oracle on just those frames."""
+    from rmsf_amd import RMSF
+    from rmsf_amd.sources import AtomGroupSource, DcdSource, HostSource
+    from test_gpu_multirank import _FakeAtomGroup, _FakeUniverse
+    d, traj = c1
+    sel = d["sel"]
+    idx = np.sort(np.random.default_rng(5).choice(np.arange(1, 98), 40, replace=False))
+    idx = np.concatenate([[0], idx])  # frame 0 in the list: the frame-0 reference is the list's first frame
+    if where == "device":
+        src = torch.tensor(traj, device="cuda")
+    elif where == "host":
+        src = HostSource(traj, sel, batch_frames=9)
+    elif where == "host_cache":
+        src = HostSource(traj, sel, batch_frames=9, cache=True)
+    elif where == "dcd":
+        from rmsf_amd.dcd import write_dcd
+        p = str(tmp_path / "t.dcd")
+        write_dcd(p, traj)
+        src = DcdSource(p, sel, batch_frames=9, cache=align == "average")
+    else:
+        src = AtomGroupSource(_FakeAtomGroup(_FakeUniverse(traj), sel, np.ones(len(sel))), batch_frames=9,
+                              cache=align == "average")
+    kw = dict(select=sel) if where == "device" else {}
+    got = RMSF(src, align=align, batch_frames=9, **kw).run(frames=idx).results
+    exp = O.rmsf_script(traj[idx], sel, None, size=1, align=align)["rmsf"]
+    assert got.n_frames == len(idx)
+    np.testing.assert_allclose(got.rmsf, exp, rtol=0, atol=TOL)
+    if where == "host_cache" and align == "average":
+        assert src.cache.have[idx].all() and src.cache.have.sum() == len(idx)
