@@ -485,7 +485,8 @@ def main():
     out = base_line(a, wl, world, dt, par)
     launches, acc_ms, acc_af = timer.totals("accumulate")
     traffic = load_traffic(a.workload, n_atoms, n_local) if launches == a.steps else None
-    kname = ("k_accum_atoms" if wl["align"] else "k_welford_flat") + ("" if a.splits else "_sk")
+    kname = (("k_accum_atoms" if wl["align"] else "k_welford_flat") if a.splits
+             else ("k_accum_atoms_sk" if wl["align"] else "k_welford_flat_sk"))
     out["roofline"] = roofline(kname, launches, acc_ms, acc_af, traffic,
                                f"profiles/pmc_{a.workload}.json" if traffic else None)
     out["cpu_baseline"] = cpu

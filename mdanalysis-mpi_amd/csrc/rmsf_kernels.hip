@@ -184,14 +184,19 @@ __device__ __forceinline__ void wel_flat_run(const f32x4 *__restrict__ p, int64_
 #endif
 }
 
+// Partials are written with nontemporal stores: beside the nt-load streams,
+// plain stores of a few percent of the bytes cost 2-8 % of the stream's time
+// on gfx950, nt stores about a third of that (tools/ubench_welford2.hip).
+__device__ __forceinline__ void nt_store(double v, double *p) { __builtin_nontemporal_store(v, p); }
+
 __device__ __forceinline__ void store4(double *__restrict__ om, double *__restrict__ oq, const double (&m)[4],
                                        const double (&q)[4]) {
   f64x2 *a = reinterpret_cast<f64x2 *>(om);
   f64x2 *b = reinterpret_cast<f64x2 *>(oq);
-  a[0] = f64x2{m[0], m[1]};
-  a[1] = f64x2{m[2], m[3]};
-  b[0] = f64x2{q[0], q[1]};
-  b[1] = f64x2{q[2], q[3]};
+  __builtin_nontemporal_store(f64x2{m[0], m[1]}, a);
+  __builtin_nontemporal_store(f64x2{m[2], m[3]}, a + 1);
+  __builtin_nontemporal_store(f64x2{q[0], q[1]}, b);
+  __builtin_nontemporal_store(f64x2{q[2], q[3]}, b + 1);
 }
 
 // k_welford_flat (split grid): grid = (ceil(n4/256), n_splits).
@@ -298,13 +303,13 @@ __device__ __forceinline__ void accum_atoms_run(const float *__restrict__ p, int
 template <int MODE>
 __device__ __forceinline__ void store3(double *__restrict__ o0, double *__restrict__ o1, const double (&m)[3],
                                        const double (&q)[3]) {
-  o0[0] = m[0];
-  o0[1] = m[1];
-  o0[2] = m[2];
+  nt_store(m[0], o0);
+  nt_store(m[1], o0 + 1);
+  nt_store(m[2], o0 + 2);
   if (MODE == RMSF_MODE_WELFORD) {
-    o1[0] = q[0];
-    o1[1] = q[1];
-    o1[2] = q[2];
+    nt_store(q[0], o1);
+    nt_store(q[1], o1 + 1);
+    nt_store(q[2], o1 + 2);
   }
 }
 
@@ -348,7 +353,8 @@ constexpr int64_t kSkMinSeg = 32;  // auto grid: ranges of >= this many frames
 struct SkPlan {
   int64_t lanes, C, nf, T;
   int G, P, cpl, mode;
-  int S;  // > 0: chunk-aligned ranges, S per chunk, dispatched split-major
+  int S;   // > 0: chunk-aligned ranges, S per chunk, dispatched split-major
+  int cw;  // lanes per chunk (kBlock; 16 for the tiled float4 stream)
 };
 
 // range processed by hardware workgroup `hw`: with chunk-aligned ranges the
@@ -388,6 +394,7 @@ __device__ __forceinline__ void sk_write_header(int64_t *hdr, const SkPlan &p) {
   hdr[6] = p.cpl;
   hdr[7] = p.mode;
   hdr[8] = p.S;
+  hdr[9] = p.cw;
 }
 
 template <int U>
@@ -468,9 +475,10 @@ __global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ 
   pl.cpl = (int)hdr[6];
   pl.mode = (int)hdr[7];
   pl.S = (int)hdr[8];
+  pl.cw = (int)hdr[9];
   const int64_t lane = j / pl.cpl;
-  const int64_t c = lane / kBlock;
-  const int64_t slot_d = (int64_t)kBlock * pl.cpl;
+  const int64_t c = lane / pl.cw;
+  const int64_t slot_d = (int64_t)pl.cw * pl.cpl;
   const int64_t off = j - c * slot_d;
   const int64_t clo = c * pl.nf, chi = clo + pl.nf;
   const double *__restrict__ parts1 = parts0 + (int64_t)pl.G * pl.P * slot_d;
@@ -720,7 +728,7 @@ __global__ __launch_bounds__(kBlock) void k_frame_stats(
       double t = red[o];
 #pragma unroll
       for (int v = 1; v < kBlock / 64; ++v) t += red[v * kStats * kTF + o];
-      out[o] = t;
+      nt_store(t, out + o);
     }
     lo += t_hi - t_lo;
     ++slot;
@@ -1487,11 +1495,13 @@ int cu_count() {
 // 3.73 vs 3.77 ms (sum) at 32/CU.
 constexpr int kSkPerCuFlat = 3, kSkPerCuAtoms = 2, kSkPerCuAligned = 32;
 
+
 // Balanced-grid plan for `lanes` lanes (cpl coordinates each) over nf frames.
-SkPlan sk_plan(int64_t lanes, int cpl, int64_t nf, int n_groups, int mode, int per_cu) {
+SkPlan sk_plan(int64_t lanes, int cpl, int64_t nf, int n_groups, int mode, int per_cu, int cw = kBlock) {
   SkPlan p{};
   p.lanes = lanes;
-  p.C = (lanes + kBlock - 1) / kBlock;
+  p.cw = cw;
+  p.C = (lanes + cw - 1) / cw;
   p.nf = nf;
   p.T = p.C * nf;
   p.cpl = cpl;
@@ -1524,7 +1534,7 @@ SkPlan sk_plan(int64_t lanes, int cpl, int64_t nf, int n_groups, int mode, int p
 }
 
 size_t sk_bytes(const SkPlan &p, bool two) {
-  const size_t part = (size_t)p.G * (size_t)p.P * kBlock * (size_t)p.cpl * sizeof(double);
+  const size_t part = (size_t)p.G * (size_t)p.P * (size_t)p.cw * (size_t)p.cpl * sizeof(double);
   return kSkHdr * sizeof(int64_t) + part * (two ? 2 : 1);
 }
 

@@ -578,16 +578,11 @@ class XtcSource:
         self._check()
         return b
 
-    def _list_batch(self, part: np.ndarray, stream: int) -> list[Batch]:
+    def _list_batch(self, part: np.ndarray, stream: int) -> Batch:
         """Frames ``part`` of an explicit frame list (scattered records):
         decoded as ONE batch (rmsf_xtcdec_decode_list) instead of one decode
-        per run; with the HBM cache their rows are copied in, and a batch whose
-        frames are all resident is served from the cache run by run."""
+        per run; with the HBM cache their rows are copied in."""
         fs = 3 * self.n_atoms
-        if self.cache is not None and self._cached[part].all():
-            if self._gather is None or self._gather.buf.shape[0] < len(part):
-                self._gather = _Gather(self.n_sel, self.batch_frames, self.cache.device)
-            return [self._gather(self.cache.data_ptr(), fs, part, self.sel_dev, stream)]
         slot, ptr = self.decoder.decode_list(part, stream)
         if self.cache is not None:
             w = 4 * fs
@@ -596,7 +591,15 @@ class XtcSource:
                 call("rmsf_memcpy2d_d2d", self.cache.data_ptr() + w * first, w * step, ptr + w * k, w, w, n, stream)
                 k += n
             self._cached[part] = True
-        return [Batch(ptr, fs, len(part), self.sel_dev, lambda: self.decoder.release(slot, stream))]
+        return Batch(ptr, fs, len(part), self.sel_dev, lambda: self.decoder.release(slot, stream))
+
+    def _cached_list(self, part: np.ndarray, stream: int) -> Batch:
+        """Frames ``part``, all resident in the HBM cache, gathered into one
+        compact batch (a scratch buffer reused by the next gather: yield it
+        before gathering again)."""
+        if self._gather is None or self._gather.buf.shape[0] < len(part):
+            self._gather = _Gather(self.n_sel, self.batch_frames, self.cache.device)
+        return self._gather(self.cache.data_ptr(), 3 * self.n_atoms, part, self.sel_dev, stream)
 
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
         ahead = self.decoder.n_slots - 1 if self.decode_on == "gpu" else 0
@@ -605,7 +608,13 @@ class XtcSource:
         if self.decode_on == "gpu" and _scattered(frames, b0, b1, nb):
             idx = frames.idx[b0:b1]
             for i in range(0, len(idx), nb):
-                queue.extend(self._list_batch(idx[i:i + nb], stream))
+                part = idx[i:i + nb]
+                if self.cache is not None and self._cached[part].all():
+                    while queue:  # decodes in flight first; a gathered batch is never queued ahead
+                        yield queue.pop(0)
+                    yield self._cached_list(part, stream)
+                    continue
+                queue.append(self._list_batch(part, stream))
                 while len(queue) > ahead:
                     yield queue.pop(0)
         else:
