@@ -259,6 +259,35 @@ SkPlan sweep_plan(int64_t lanes, int64_t nf, int mode, int per_cu, int *k_out, i
 
 namespace ub {
 
+// k_welford_flat_sk with the round-1 plain partial stores (A/B of the store kind)
+__global__ __launch_bounds__(kBlock) void flat_plain(const float *__restrict__ xyz, int64_t stride4, SkPlan pl,
+                                                    int64_t *__restrict__ hdr, double *__restrict__ parts0,
+                                                    double *__restrict__ parts1) {
+  const int b = sk_range(pl, blockIdx.x);
+  if (blockIdx.x == 0 && threadIdx.x == 0) sk_write_header(hdr, pl);
+  int64_t lo = sk_lo(pl, b);
+  const int64_t hi = sk_lo(pl, b + 1);
+  int64_t slot = (int64_t)b * pl.P;
+  while (lo < hi) {
+    int64_t c, f0;
+    const int len = (int)sk_seg_len(pl, lo, hi, &c, &f0);
+    const int64_t i4 = c * kBlock + threadIdx.x;
+    if (i4 < pl.lanes) {
+      double m[4], q[4];
+      wel_flat_run<4>(reinterpret_cast<const f32x4 *>(xyz) + f0 * stride4 + i4, stride4, len, m, q);
+      const int64_t o = slot * (kBlock * 4) + 4 * threadIdx.x;
+      f64x2 *a = reinterpret_cast<f64x2 *>(parts0 + o);
+      f64x2 *bb = reinterpret_cast<f64x2 *>(parts1 + o);
+      a[0] = f64x2{m[0], m[1]};
+      a[1] = f64x2{m[2], m[3]};
+      bb[0] = f64x2{q[0], q[1]};
+      bb[1] = f64x2{q[2], q[3]};
+    }
+    lo += len;
+    ++slot;
+  }
+}
+
 // tile = 64 frames x W floats (W/4 float4 per row), staged HBM -> regs -> LDS
 // (next tile in flight); thread t owns coordinate c = t % W of frame half
 // h = t / W (W = 128: 2 halves of 32 frames; W = 256: 1 half of 64 frames)
@@ -429,6 +458,23 @@ int main() {
       rmsf_fold_balanced(acc, fs, RMSF_MODE_WELFORD, 0, out, part, nullptr);
     });
     char nm[96];
+    {
+      const SkPlan pl = sk_plan(n4, 4, nf, 0, RMSF_MODE_WELFORD, kSkPerCuFlat);
+      for (int ab_rep = 0; ab_rep < 2; ++ab_rep) {
+        run("A/B: flat, nontemporal partial stores", [&] {
+          int64_t *hdr = static_cast<int64_t *>(acc);
+          double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
+          double *p1 = p0 + (size_t)pl.G * pl.P * kBlock * 4;
+          hipLaunchKernelGGL((k_welford_flat_sk<4>), dim3(pl.G), dim3(kBlock), 0, 0, x, fs / 4, pl, hdr, p0, p1);
+        });
+        run("A/B: flat, plain partial stores", [&] {
+          int64_t *hdr = static_cast<int64_t *>(acc);
+          double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
+          double *p1 = p0 + (size_t)pl.G * pl.P * kBlock * 4;
+          hipLaunchKernelGGL(ub::flat_plain, dim3(pl.G), dim3(kBlock), 0, 0, x, fs / 4, pl, hdr, p0, p1);
+        });
+      }
+    }
     for (int S : {5, 16, 32}) {
       snprintf(nm, sizeof nm, "probe W=64 splits=%d no epilogue", S);
       run(nm, [&] {
