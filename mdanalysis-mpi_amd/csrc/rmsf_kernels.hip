@@ -1492,11 +1492,8 @@ int cu_count() {
 // split grid on the same box); one atom per lane without the transform at 1-2;
 // the aligned (transform) kernels are VALU-heavy (~48 fp64 ops per
 // atom-frame, 99 VGPRs) and want many short ranges: 3.90 vs 4.06 ms (Welford),
-// 3.73 vs 3.77 ms (sum) at 32/CU.  The aligned Welford then gains ~1 % from
-// 8 frames in flight per lane at 16/CU (3.81-3.82 vs 3.85-3.86 ms,
-// tools/ubench_accum2.hip); the sum does not.
-constexpr int kSkPerCuFlat = 3, kSkPerCuAtoms = 2, kSkPerCuAligned = 32, kSkPerCuAlignedWel = 16;
-constexpr int kUAligned = 4, kUAlignedWel = 8;
+// 3.73 vs 3.77 ms (sum) at 32/CU.
+constexpr int kSkPerCuFlat = 3, kSkPerCuAtoms = 2, kSkPerCuAligned = 32;
 
 
 // Balanced-grid plan for `lanes` lanes (cpl coordinates each) over nf frames.
@@ -1555,7 +1552,7 @@ RMSF_EXPORT size_t rmsf_accumulate_balanced_workspace_bytes(int64_t n_sel, int64
   if (n_sel < 1 || n_frames < 1) return 0;
   // the larger of the two layouts (float4 columns / one atom per lane), WELFORD
   size_t m = 0;
-  for (int per_cu : {kSkPerCuFlat, kSkPerCuAtoms, kSkPerCuAligned, kSkPerCuAlignedWel}) {
+  for (int per_cu : {kSkPerCuFlat, kSkPerCuAtoms, kSkPerCuAligned}) {
     m = std::max(m, sk_bytes(sk_plan((3 * n_sel + 3) / 4, 4, n_frames, n_groups, RMSF_MODE_WELFORD, per_cu), true));
     m = std::max(m, sk_bytes(sk_plan(n_sel, 3, n_frames, n_groups, RMSF_MODE_WELFORD, per_cu), true));
   }
@@ -1582,24 +1579,23 @@ RMSF_EXPORT int rmsf_accumulate_balanced(const float *d_xyz, int64_t fstride, in
     hipLaunchKernelGGL((k_welford_flat_sk<4>), dim3(pl.G), dim3(kBlock), 0, s, d_xyz, fstride / 4, pl, hdr, p0, p1);
     return after_launch("k_welford_flat_sk");
   }
-  const int per_cu = !d_xform ? kSkPerCuAtoms : two ? kSkPerCuAlignedWel : kSkPerCuAligned;
-  const SkPlan pl = sk_plan(n_sel, 3, n_frames, n_groups, mode, per_cu);
+  const SkPlan pl = sk_plan(n_sel, 3, n_frames, n_groups, mode, d_xform ? kSkPerCuAligned : kSkPerCuAtoms);
   if (work_bytes < sk_bytes(pl, two)) return fail(RMSF_ENOMEM, "rmsf_accumulate_balanced: workspace too small");
   double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
   double *p1 = two ? p0 + (size_t)pl.G * pl.P * kBlock * 3 : nullptr;
   const bool g = d_sel != nullptr, al = d_xform != nullptr;
-#define SK_LAUNCH(M_, A_, G_, U_) \
-  hipLaunchKernelGGL((k_accum_atoms_sk<M_, A_, G_, U_>), dim3(pl.G), dim3(kBlock), 0, s, d_xyz, fstride, d_sel, d_xform, d_refinfo, pl, hdr, p0, p1)
+#define SK_LAUNCH(M_, A_, G_) \
+  hipLaunchKernelGGL((k_accum_atoms_sk<M_, A_, G_, 4>), dim3(pl.G), dim3(kBlock), 0, s, d_xyz, fstride, d_sel, d_xform, d_refinfo, pl, hdr, p0, p1)
   if (two) {
-    if (al && g) SK_LAUNCH(0, true, true, kUAlignedWel);
-    else if (al) SK_LAUNCH(0, true, false, kUAlignedWel);
-    else if (g) SK_LAUNCH(0, false, true, 4);
-    else SK_LAUNCH(0, false, false, 4);
+    if (al && g) SK_LAUNCH(0, true, true);
+    else if (al) SK_LAUNCH(0, true, false);
+    else if (g) SK_LAUNCH(0, false, true);
+    else SK_LAUNCH(0, false, false);
   } else {
-    if (al && g) SK_LAUNCH(1, true, true, kUAligned);
-    else if (al) SK_LAUNCH(1, true, false, kUAligned);
-    else if (g) SK_LAUNCH(1, false, true, 4);
-    else SK_LAUNCH(1, false, false, 4);
+    if (al && g) SK_LAUNCH(1, true, true);
+    else if (al) SK_LAUNCH(1, true, false);
+    else if (g) SK_LAUNCH(1, false, true);
+    else SK_LAUNCH(1, false, false);
   }
 #undef SK_LAUNCH
   return after_launch("k_accum_atoms_sk");
