@@ -1492,8 +1492,12 @@ int cu_count() {
 // split grid on the same box); one atom per lane without the transform at 1-2;
 // the aligned (transform) kernels are VALU-heavy (~48 fp64 ops per
 // atom-frame, 99 VGPRs) and want many short ranges: 3.90 vs 4.06 ms (Welford),
-// 3.73 vs 3.77 ms (sum) at 32/CU.
-constexpr int kSkPerCuFlat = 3, kSkPerCuAtoms = 2, kSkPerCuAligned = 32;
+// 3.73 vs 3.77 ms (sum) at 32/CU.  Round 2 (tools/ubench_short.hip, five
+// boxes, the strong-scaling shares 100k x 20k/N): the float4 Welford at
+// 2/CU = 512 workgroups is the fastest count at every share -- 8 % under
+// 3/CU at 2,500 frames (0.444-0.454 vs 0.480-0.494 ms), 2 % at 5,000, within
+// +0.4/-1 % at 10,000-20,000 -- so 2/CU, not 3.
+constexpr int kSkPerCuFlat = 2, kSkPerCuAtoms = 2, kSkPerCuAligned = 32;
 
 
 // Balanced-grid plan for `lanes` lanes (cpl coordinates each) over nf frames.
