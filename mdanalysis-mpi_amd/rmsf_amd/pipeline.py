@@ -94,15 +94,25 @@ class Accumulator:
             # the bound grows with the batch, so size it for the largest one
             nbytes = eng.balanced_workspace_bytes(n_sel, max_batch)
             self.work = eng.empty(max(2, (nbytes + 7) // 8))
-        # only slot 0 (the running result) must start at zero: split slots are
-        # fully written by the accumulate kernel before they are read
+        # Slot 0 is the running result.  The balanced fold overwrites it on the
+        # first batch (acc_n = 0), so it is zeroed only if it is read with no
+        # frames folded in (an empty block); the split grid's Chan merge reads
+        # it from the start.  Split slots are written before they are read.
         self.parts0 = eng.empty(1 + self.s_max, self.n_coord)
-        self.parts0[0].zero_()
         self.parts1 = None
         if mode == RMSF_MODE_WELFORD:
             self.parts1 = eng.empty(1 + self.s_max, self.n_coord)
-            self.parts1[0].zero_()
         self.n = 0
+        self._zeroed = False
+        if n_splits:
+            self._zero()
+
+    def _zero(self) -> None:
+        if not self._zeroed:
+            self.parts0[0].zero_()
+            if self.parts1 is not None:
+                self.parts1[0].zero_()
+            self._zeroed = True
 
     def add(self, b: Batch, xform: torch.Tensor | None = None, refinfo: torch.Tensor | None = None) -> None:
         eng = self.eng
@@ -130,10 +140,14 @@ class Accumulator:
 
     @property
     def result0(self) -> torch.Tensor:
+        if self.n == 0:
+            self._zero()
         return self.parts0[0]
 
     @property
     def result1(self) -> torch.Tensor:
+        if self.n == 0:
+            self._zero()
         return self.parts1[0]
 
 
