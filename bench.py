@@ -343,7 +343,7 @@ def main_single_process(a, wl, cpu) -> None:
     out = base_line(a, wl, n, dt, par)
     out["devices"] = devs
     out["rehearsal"] = rehearsal
-    kname = ("k_accum_atoms_sk" if align else "k_welford_flat_sk")
+    kname = ("k_accum_split_sk" if align else "k_welford_flat_sk")
     out["roofline"] = roofline(kname, sum(x[0] for x in acc), sum(x[1] for x in acc), sum(x[2] for x in acc))
     out["roofline"]["per_device_gbs"] = [B_PER_ATOM_FRAME * x[2] / (x[1] / 1e3) / 1e9 if x[1] else None for x in acc]
     if align:
@@ -486,7 +486,7 @@ def main():
     launches, acc_ms, acc_af = timer.totals("accumulate")
     traffic = load_traffic(a.workload, n_atoms, n_local) if launches == a.steps else None
     kname = (("k_accum_atoms" if wl["align"] else "k_welford_flat") if a.splits
-             else ("k_accum_atoms_sk" if wl["align"] else "k_welford_flat_sk"))
+             else ("k_accum_split_sk" if wl["align"] else "k_welford_flat_sk"))
     out["roofline"] = roofline(kname, launches, acc_ms, acc_af, traffic,
                                f"profiles/pmc_{a.workload}.json" if traffic else None)
     out["cpu_baseline"] = cpu

@@ -454,6 +454,120 @@ __global__ __launch_bounds__(kBlock) void k_accum_atoms_sk(const float *__restri
   }
 }
 
+// accum_span: frames [0, nf) from p (one selected atom per lane), adding to
+// m/q: WELFORD shifted sums (S1 += d, S2 += d^2, d = x - sh), SUM plain sums.
+// xf = frame 0's transform record.
+template <int MODE, bool ALIGN, int U>
+__device__ __forceinline__ void accum_span(const float *__restrict__ p, int64_t fstride, int nf,
+                                           const double *__restrict__ xf, double rc0, double rc1, double rc2,
+                                           const double (&sh)[3], double (&m)[3], double (&q)[3]) {
+  auto consume = [&](float x, float y, float z, int k) {
+    if (ALIGN) apply_xform(x, y, z, xf + (int64_t)k * kXform, rc0, rc1, rc2);
+    if (MODE == RMSF_MODE_WELFORD) {
+      const double d0 = (double)x - sh[0], d1 = (double)y - sh[1], d2 = (double)z - sh[2];
+      m[0] += d0, m[1] += d1, m[2] += d2;
+      q[0] = fma(d0, d0, q[0]), q[1] = fma(d1, d1, q[1]), q[2] = fma(d2, d2, q[2]);
+    } else {
+      m[0] += (double)x, m[1] += (double)y, m[2] += (double)z;
+    }
+  };
+  int k = 0;
+  for (; k + U <= nf; k += U) {
+    float vx[U], vy[U], vz[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float *r = p + (int64_t)(k + u) * fstride;
+      vx[u] = __builtin_nontemporal_load(r);
+      vy[u] = __builtin_nontemporal_load(r + 1);
+      vz[u] = __builtin_nontemporal_load(r + 2);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) consume(vx[u], vy[u], vz[u], k + u);
+  }
+  for (; k < nf; ++k) {
+    const float *r = p + (int64_t)k * fstride;
+    consume(r[0], r[1], r[2], k);
+  }
+}
+
+// k_accum_split_sk: the balanced grid of k_accum_atoms_sk with the frames of
+// every segment split over Q sub-blocks of Q*256 threads (each sub-block the
+// chunk's 256 atoms, a contiguous Q-th of the segment's frames).  The
+// sub-blocks share one shift (the segment's first frame after the
+// transform), so their shifted sums add: sub-blocks 1..Q-1 leave theirs in
+// LDS and sub-block 0 adds them in that order (deterministic) and stores ONE
+// partial per segment.  Q x fewer partials at the same wave count: at 8,192
+// ranges x 2 segments the partials are 196 MB per launch, which the fold
+// reads back -- 6 % of a 2,500-frame share (tools/ubench_accum3.hip).
+template <int MODE, bool ALIGN, bool GATHER, int U, int Q>
+__global__ __launch_bounds__(kBlock *Q) void k_accum_split_sk(const float *__restrict__ xyz, int64_t fstride,
+                                                              const int32_t *__restrict__ sel,
+                                                              const double *__restrict__ xform,
+                                                              const double *__restrict__ refinfo, SkPlan pl,
+                                                              int64_t *__restrict__ hdr,
+                                                              double *__restrict__ parts0,
+                                                              double *__restrict__ parts1) {
+  static_assert(Q > 1 && RMSF_SHIFTED_SUMS, "k_accum_split_sk combines shifted sums of Q > 1 sub-blocks");
+  constexpr int NV = MODE == RMSF_MODE_WELFORD ? 6 : 3;  // doubles per lane handed over
+  __shared__ double red[(Q - 1) * NV * kBlock];
+  const int b = sk_range(pl, blockIdx.x);
+  if (blockIdx.x == 0 && threadIdx.x == 0) sk_write_header(hdr, pl);
+  const int li = threadIdx.x % kBlock;
+  const int qd = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kBlock));
+  const double rc0 = ALIGN ? refinfo[0] : 0.0, rc1 = ALIGN ? refinfo[1] : 0.0, rc2 = ALIGN ? refinfo[2] : 0.0;
+  int64_t lo = uni64(sk_lo(pl, b));
+  const int64_t hi = uni64(sk_lo(pl, b + 1));
+  int64_t slot = (int64_t)b * pl.P;
+  while (lo < hi) {
+    int64_t c, f0;
+    const int len = __builtin_amdgcn_readfirstlane((int)sk_seg_len(pl, lo, hi, &c, &f0));
+    c = uni64(c);
+    f0 = uni64(f0);
+    const int64_t a = c * kBlock + li;
+    const bool live = a < pl.lanes;  // no early exit: every thread meets the barriers
+    const int s0 = (int)((int64_t)len * qd / Q), s1 = (int)((int64_t)len * (qd + 1) / Q);
+    double m[3] = {0.0, 0.0, 0.0}, q[3] = {0.0, 0.0, 0.0}, sh[3] = {0.0, 0.0, 0.0};
+    if (live) {
+      const float *p = xyz + f0 * fstride + (GATHER ? 3 * (int64_t)sel[a] : 3 * a);
+      if (MODE == RMSF_MODE_WELFORD) {
+        float x = p[0], y = p[1], z = p[2];
+        if (ALIGN) apply_xform(x, y, z, xform + f0 * kXform, rc0, rc1, rc2);
+        sh[0] = (double)x, sh[1] = (double)y, sh[2] = (double)z;
+      }
+      accum_span<MODE, ALIGN, U>(p + (int64_t)s0 * fstride, fstride, s1 - s0,
+                                 ALIGN ? xform + (f0 + s0) * kXform : nullptr, rc0, rc1, rc2, sh, m, q);
+    }
+    if (qd > 0) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        red[((qd - 1) * NV + j) * kBlock + li] = m[j];
+        if (MODE == RMSF_MODE_WELFORD) red[((qd - 1) * NV + 3 + j) * kBlock + li] = q[j];
+      }
+    }
+    __syncthreads();
+    if (qd == 0 && live) {
+#pragma unroll
+      for (int v = 1; v < Q; ++v) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          m[j] += red[((v - 1) * NV + j) * kBlock + li];
+          if (MODE == RMSF_MODE_WELFORD) q[j] += red[((v - 1) * NV + 3 + j) * kBlock + li];
+        }
+      }
+      if (MODE == RMSF_MODE_WELFORD) {
+        const double inv = g_coef.v[len - 1].b;  // 1/len
+#pragma unroll
+        for (int j = 0; j < 3; ++j) shifted_to_moments(m[j], q[j], sh[j], inv);
+      }
+      const int64_t o = slot * (kBlock * 3) + 3 * li;
+      store3<MODE>(parts0 + o, parts1 + o, m, q);
+    }
+    __syncthreads();  // red is rewritten by the next segment
+    lo += len;
+    ++slot;
+  }
+}
+
 // Fold the balanced partials of one batch, in frame order, into the running
 // result (acc_n frames already in acc0/acc1; 0 = overwrite): Chan's merge
 // (second_order_moments, RMSF.py:36-41) for WELFORD, a sum for SUM.  One
@@ -1492,12 +1606,18 @@ int cu_count() {
 // split grid on the same box); one atom per lane without the transform at 1-2;
 // the aligned (transform) kernels are VALU-heavy (~48 fp64 ops per
 // atom-frame, 99 VGPRs) and want many short ranges: 3.90 vs 4.06 ms (Welford),
-// 3.73 vs 3.77 ms (sum) at 32/CU.  Round 2 (tools/ubench_short.hip, five
+// 3.73 vs 3.77 ms (sum) at 32/CU -- round 2 replaced them by the frame-split
+// kernel (k_accum_split_sk) below.  Round 2 (tools/ubench_short.hip, five
 // boxes, the strong-scaling shares 100k x 20k/N): the float4 Welford at
 // 2/CU = 512 workgroups is the fastest count at every share -- 8 % under
 // 3/CU at 2,500 frames (0.444-0.454 vs 0.480-0.494 ms), 2 % at 5,000, within
 // +0.4/-1 % at 10,000-20,000 -- so 2/CU, not 3.
 constexpr int kSkPerCuFlat = 2, kSkPerCuAtoms = 2, kSkPerCuAligned = 32;
+// Aligned accumulate, frame-split (k_accum_split_sk; tools/ubench_accum3.hip,
+// accumulate + fold at 100k atoms): Welford Q = 2 at 8 workgroups/CU, sum
+// Q = 4 at 4/CU -- against the one-sub-block kernel at 32/CU, 17-20 % less
+// time at 2,500 frames, 11-12 % at 5,000, 2-3 % at 20,000.
+constexpr int kQWel = 2, kSkPerCuSplitWel = 8, kQSum = 4, kSkPerCuSplitSum = 4;
 
 
 // Balanced-grid plan for `lanes` lanes (cpl coordinates each) over nf frames.
@@ -1556,7 +1676,7 @@ RMSF_EXPORT size_t rmsf_accumulate_balanced_workspace_bytes(int64_t n_sel, int64
   if (n_sel < 1 || n_frames < 1) return 0;
   // the larger of the two layouts (float4 columns / one atom per lane), WELFORD
   size_t m = 0;
-  for (int per_cu : {kSkPerCuFlat, kSkPerCuAtoms, kSkPerCuAligned}) {
+  for (int per_cu : {kSkPerCuFlat, kSkPerCuAtoms, kSkPerCuAligned, kSkPerCuSplitWel, kSkPerCuSplitSum}) {
     m = std::max(m, sk_bytes(sk_plan((3 * n_sel + 3) / 4, 4, n_frames, n_groups, RMSF_MODE_WELFORD, per_cu), true));
     m = std::max(m, sk_bytes(sk_plan(n_sel, 3, n_frames, n_groups, RMSF_MODE_WELFORD, per_cu), true));
   }
@@ -1583,11 +1703,28 @@ RMSF_EXPORT int rmsf_accumulate_balanced(const float *d_xyz, int64_t fstride, in
     hipLaunchKernelGGL((k_welford_flat_sk<4>), dim3(pl.G), dim3(kBlock), 0, s, d_xyz, fstride / 4, pl, hdr, p0, p1);
     return after_launch("k_welford_flat_sk");
   }
-  const SkPlan pl = sk_plan(n_sel, 3, n_frames, n_groups, mode, d_xform ? kSkPerCuAligned : kSkPerCuAtoms);
+  const bool g = d_sel != nullptr, al = d_xform != nullptr;
+  const bool split = al && RMSF_SHIFTED_SUMS;  // aligned: the frame-split kernel
+  const int per_cu = !al ? kSkPerCuAtoms : !split ? kSkPerCuAligned : two ? kSkPerCuSplitWel : kSkPerCuSplitSum;
+  const SkPlan pl = sk_plan(n_sel, 3, n_frames, n_groups, mode, per_cu);
   if (work_bytes < sk_bytes(pl, two)) return fail(RMSF_ENOMEM, "rmsf_accumulate_balanced: workspace too small");
   double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
   double *p1 = two ? p0 + (size_t)pl.G * pl.P * kBlock * 3 : nullptr;
-  const bool g = d_sel != nullptr, al = d_xform != nullptr;
+#if RMSF_SHIFTED_SUMS
+  if (split) {
+#define SPLIT_LAUNCH(M_, G_, Q_) \
+  hipLaunchKernelGGL((k_accum_split_sk<M_, true, G_, 4, Q_>), dim3(pl.G), dim3(kBlock * Q_), 0, s, d_xyz, fstride, d_sel, d_xform, d_refinfo, pl, hdr, p0, p1)
+    if (two) {
+      if (g) SPLIT_LAUNCH(0, true, kQWel);
+      else SPLIT_LAUNCH(0, false, kQWel);
+    } else {
+      if (g) SPLIT_LAUNCH(1, true, kQSum);
+      else SPLIT_LAUNCH(1, false, kQSum);
+    }
+#undef SPLIT_LAUNCH
+    return after_launch("k_accum_split_sk");
+  }
+#endif
 #define SK_LAUNCH(M_, A_, G_) \
   hipLaunchKernelGGL((k_accum_atoms_sk<M_, A_, G_, 4>), dim3(pl.G), dim3(kBlock), 0, s, d_xyz, fstride, d_sel, d_xform, d_refinfo, pl, hdr, p0, p1)
   if (two) {

@@ -224,24 +224,39 @@ int main() {
              dq);
     }
   }
+  // accumulate + fold (the fold reads every partial: its cost grows with G*P)
+  auto libg = [&](int mode, int64_t nf, int groups) {
+    SkPlan pl = sk_plan(n, 3, nf, groups, mode, kSkPerCuAligned);
+    int64_t *hdr = static_cast<int64_t *>(acc);
+    double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
+    double *p1 = p0 + (size_t)pl.G * pl.P * kBlock * 3;
+    if (mode == RMSF_MODE_WELFORD)
+      hipLaunchKernelGGL((k_accum_atoms_sk<RMSF_MODE_WELFORD, true, false, 4>), dim3(pl.G), dim3(kBlock), 0, 0, x, fs,
+                         nullptr, xf, info, pl, hdr, p0, p1);
+    else
+      hipLaunchKernelGGL((k_accum_atoms_sk<RMSF_MODE_SUM, true, false, 4>), dim3(pl.G), dim3(kBlock), 0, 0, x, fs,
+                         nullptr, xf, info, pl, hdr, p0, p1);
+  };
+  auto fold = [&](int mode) { rmsf_fold_balanced(acc, fs, mode, 0, out0, out1, nullptr); };
   char nm[96];
   for (int rep = 0; rep < 2; ++rep) {
-    for (int64_t nf : {2500, 20000}) {
-      run("lib WELFORD (32/CU x 256)", nf, [&] { lib(RMSF_MODE_WELFORD, nf); });
-      for (int per_cu : {2, 4, 8}) {
-        int G = qsplit(RMSF_MODE_WELFORD, nf, per_cu, Q4{});
-        snprintf(nm, sizeof nm, "Q=4 WELFORD %d/CU x 1024 (G %d)", per_cu, G);
-        run(nm, nf, [&] { qsplit(RMSF_MODE_WELFORD, nf, per_cu, Q4{}); });
-      }
-      for (int per_cu : {8, 16}) {
-        int G = qsplit(RMSF_MODE_WELFORD, nf, per_cu, Q2{});
-        snprintf(nm, sizeof nm, "Q=2 WELFORD %d/CU x 512 (G %d)", per_cu, G);
-        run(nm, nf, [&] { qsplit(RMSF_MODE_WELFORD, nf, per_cu, Q2{}); });
-      }
-      run("lib SUM (32/CU x 256)", nf, [&] { lib(RMSF_MODE_SUM, nf); });
-      for (int per_cu : {4, 8}) {
-        snprintf(nm, sizeof nm, "Q=4 SUM %d/CU x 1024", per_cu);
-        run(nm, nf, [&] { qsplit(RMSF_MODE_SUM, nf, per_cu, Q4{}); });
+    for (int64_t nf : {2500, 5000, 20000}) {
+      for (int mode : {RMSF_MODE_WELFORD, RMSF_MODE_SUM}) {
+        const char *mn = mode == RMSF_MODE_WELFORD ? "WEL" : "SUM";
+        snprintf(nm, sizeof nm, "%s lib 32/CU x256 +fold", mn);
+        run(nm, nf, [&] { lib(mode, nf); fold(mode); });
+        for (int groups : {2048, 4096}) {
+          snprintf(nm, sizeof nm, "%s lib G=%d x256 +fold", mn, groups);
+          run(nm, nf, [&] { libg(mode, nf, groups); fold(mode); });
+        }
+        for (int per_cu : {8, 16, 32}) {
+          snprintf(nm, sizeof nm, "%s Q=2 %d/CU x512 +fold", mn, per_cu);
+          run(nm, nf, [&] { qsplit(mode, nf, per_cu, Q2{}); fold(mode); });
+        }
+        for (int per_cu : {4, 8}) {
+          snprintf(nm, sizeof nm, "%s Q=4 %d/CU x1024 +fold", mn, per_cu);
+          run(nm, nf, [&] { qsplit(mode, nf, per_cu, Q4{}); fold(mode); });
+        }
       }
     }
   }
