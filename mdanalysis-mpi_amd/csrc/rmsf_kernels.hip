@@ -65,8 +65,10 @@ constexpr int kXform = RMSF_XFORM_DOUBLES;
 constexpr int kStats = 16;       // doubles per (frame, chunk) partial
 constexpr int64_t kAccumBlocks = 3584;       // target workgroups, k_welford_flat
 constexpr int64_t kAccumBlocksAtom = 4608;   // target workgroups, k_accum_atoms
-constexpr int64_t kStatsGroups = 3072;  // k_frame_stats workgroups (balanced grid; 4 rounds of 3 per CU on MI355X)
-constexpr int64_t kStatsMinUnits = 1;   // ... at least this many (64-frame, 32-atom) units each
+constexpr int64_t kStatsGroups = 3072;  // k_frame_stats workgroups at most (balanced grid; 4 rounds of 3 per CU on MI355X)
+constexpr int64_t kStatsRound = 768;    // ... in whole rounds of this many (3 resident per CU x 256 CUs)
+constexpr int64_t kStatsRoundUnits = 768 * 160;  // ... one round per this many (64-frame, 32-atom) units
+constexpr int64_t kStatsMinUnits = 1;   // ... at least this many units each
 
 // ---------------------------------------------------------------------------
 // Welford coefficients a_k = k/(k+1), b_k = 1/(k+1) (RMSF.py:137-138), folded
@@ -1353,16 +1355,23 @@ __global__ __launch_bounds__(kBlock) void k_synth(float *__restrict__ out, int64
 
 inline unsigned grid1(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
-// Balanced grid of k_frame_stats: kStatsGroups workgroups (a fixed count,
-// so the summation order -- hence the bits -- does not depend on the device),
-// fewer when the batch has fewer than kStatsMinUnits units per workgroup.
+// Balanced grid of k_frame_stats: whole rounds of kStatsRound workgroups, up
+// to kStatsGroups, by the batch's unit count -- a function of the shape only,
+// so the summation order (hence the bits) does not depend on the device.
 // P = the most segments any workgroup's range can cross: ceil(len/ntiles)+1.
 StatsPlan stats_plan(int64_t n_sel, int64_t n_frames) {
   StatsPlan p;
   p.ntiles = (n_sel + kTA - 1) / kTA;
   p.ngroups = std::max<int64_t>(1, (n_frames + kTF - 1) / kTF);
   p.T = p.ntiles * p.ngroups;
-  p.G = (int)std::max<int64_t>(1, std::min<int64_t>(kStatsGroups, p.T / kStatsMinUnits));
+  // whole rounds, ~160 units per workgroup, at most kStatsGroups: fewer
+  // workgroups at short batches cut both the per-workgroup fixed cost and the
+  // partials k_qcp_frames folds (tools/ubench_stats3.hip, 100k atoms: 2,500
+  // frames 0.478 vs 0.516 ms for stats + QCP at 768 vs 3,072 workgroups;
+  // 5,000 frames 0.945 vs 0.988 at 1,536; 20,000 frames best at 3,072)
+  const int64_t rounds = std::min<int64_t>(kStatsGroups / kStatsRound,
+                                           std::max<int64_t>(1, (p.T + kStatsRoundUnits / 2) / kStatsRoundUnits));
+  p.G = (int)std::max<int64_t>(1, std::min<int64_t>(kStatsRound * rounds, p.T / kStatsMinUnits));
   const int64_t len = (p.T + p.G - 1) / p.G;
   p.P = (int)((len + p.ntiles - 1) / p.ntiles + 1);
   return p;
