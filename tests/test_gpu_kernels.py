@@ -195,6 +195,68 @@ def test_balanced_welford_and_sum(eng, n_sel, nf, groups, gather):
     np.testing.assert_allclose(rmsf.cpu().numpy(), O.rmsf_two_pass(x), rtol=0, atol=1e-9)
 
 
+@pytest.mark.parametrize("n_sel,nf,groups,gather", [
+    (4096, 1000, 0, False), (1001, 333, 7, True), (3, 5, 0, False), (3, 5, 2, True), (257, 4097, 2, False),
+    (300, 9000, 0, True), (1000, 1, 0, False), (1000, 2, 0, False), (5000, 3, 1, False), (70_000, 40, 0, False)])
+def test_balanced_aligned_vs_split_grid(eng, n_sel, nf, groups, gather):
+    """The aligned accumulate on the balanced grid -- k_accum_split_sk: each
+    segment's frames split over Q sub-blocks that share one shift (1-3 frame
+    segments leave sub-blocks empty) -- against the split grid's one-atom-per-
+    lane kernel (k_accum_atoms) on the same device transforms: the f32
+    transformed coordinates are the same values, only the f64 summation order
+    differs (1e-10).  Both against RMSF.py:133-138 restated in numpy with the
+    device's R / COM and the three f32 rounding points (1e-6 A, the north
+    star's bound: an FMA-order flip moves one coordinate by one f32 ulp)."""
+    from rmsf_amd.synth import generate, motion_table
+    from rmsf_amd._lib import RMSF_MODE_SUM, RMSF_MODE_WELFORD
+    n_atoms = n_sel + 11 if gather else n_sel
+    traj = generate(eng, n_atoms, 0, nf, seed=31, motion=motion_table(2, nf))
+    sel = np.sort(np.random.default_rng(4).choice(n_atoms, n_sel, replace=False)) if gather else np.arange(n_sel)
+    sdev = torch.tensor(sel.astype(np.int32), device=eng.device) if gather else None
+    ref, info = eng.reference_setup(n_sel, frame_ptr=traj.data_ptr(), sel=sdev)
+    xf = eng.empty(nf, 16)
+    sw = eng.empty(eng.workspace_bytes(n_sel, nf) // 8 + 1)
+    eng.superpose(traj.data_ptr(), 3 * n_atoms, nf, n_sel, sdev, None, ref, info, xf, sw)
+    nc = 3 * n_sel
+    # balanced grid, two batches folded in order
+    mean, m2, s = eng.empty(nc), eng.empty(nc), eng.empty(nc)
+    acc, cut = 0, nf // 3
+    for f0, f1 in ((0, cut), (cut, nf)):
+        if f1 <= f0:
+            continue
+        n = f1 - f0
+        work = eng.empty(eng.balanced_workspace_bytes(n_sel, n, groups) // 8 + 2)
+        ptr = traj.data_ptr() + f0 * 3 * n_atoms * 4
+        eng.accumulate_balanced(ptr, 3 * n_atoms, n, n_sel, sdev, xf[f0:], info, RMSF_MODE_WELFORD, work, groups)
+        eng.fold_balanced(work, nc, RMSF_MODE_WELFORD, acc, mean, m2)
+        eng.accumulate_balanced(ptr, 3 * n_atoms, n, n_sel, sdev, xf[f0:], info, RMSF_MODE_SUM, work, groups)
+        eng.fold_balanced(work, nc, RMSF_MODE_SUM, acc, s, None)
+        acc += n
+    # split grid
+    k = eng.splits(n_sel, nf, True)
+    mp, qp, sp = eng.empty(k, nc), eng.empty(k, nc), eng.empty(k, nc)
+    eng.accumulate(traj.data_ptr(), 3 * n_atoms, nf, n_sel, sdev, xf, info, RMSF_MODE_WELFORD, k, mp, qp)
+    mean_s, m2_s, s_s = eng.empty(nc), eng.empty(nc), eng.empty(nc)
+    eng.chan_merge(mp, qp, eng.split_counts(nf, k), nc, mean_s, m2_s)
+    eng.accumulate(traj.data_ptr(), 3 * n_atoms, nf, n_sel, sdev, xf, info, RMSF_MODE_SUM, k, sp, None)
+    eng.sum_splits(sp, k, nc, s_s)
+    _sync()
+    M, Q2, S = mean.cpu().numpy(), m2.cpu().numpy(), s.cpu().numpy()
+    np.testing.assert_allclose(M, mean_s.cpu().numpy(), rtol=0, atol=1e-10)
+    np.testing.assert_allclose(S, s_s.cpu().numpy(), rtol=1e-13, atol=1e-9)
+    np.testing.assert_allclose(Q2 / nf, m2_s.cpu().numpy() / nf, rtol=0, atol=1e-10)
+    # RMSF.py:133-138 with the device's transforms
+    X, I = xf.cpu().numpy(), info.cpu().numpy()
+    host = traj.cpu().numpy()[:, sel].astype(np.float64)
+    al = np.empty_like(host)
+    for f in range(nf):
+        p = (host[f] - X[f, 9:12]).astype(np.float32).astype(np.float64)
+        p = (p @ X[f, :9].reshape(3, 3)).astype(np.float32).astype(np.float64)
+        al[f] = (p + I[:3]).astype(np.float32)
+    np.testing.assert_allclose(M.reshape(-1, 3), al.mean(0), rtol=0, atol=1e-6)
+    np.testing.assert_allclose(np.sqrt(Q2.reshape(-1, 3).sum(1) / nf), O.rmsf_two_pass(al), rtol=0, atol=1e-6)
+
+
 def test_balanced_bad_arguments(eng):
     from rmsf_amd import RmsfError
     from rmsf_amd._lib import RMSF_MODE_WELFORD
