@@ -7,6 +7,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #define CK(x)                                                                        \
   do {                                                                               \
@@ -17,8 +18,15 @@
     }                                                                                \
   } while (0)
 
-int main() {
-  const int64_t n = 100000, nf_max = 20000, fs = 3 * n;
+int main(int argc, char **argv) {
+  // ubench_short [n_atoms [frames...]]: default 100k atoms at 2,500-20,000 frames
+  const int64_t n = argc > 1 ? atoll(argv[1]) : 100000;
+  std::vector<int64_t> frames_list;
+  for (int i = 2; i < argc; ++i) frames_list.push_back(atoll(argv[i]));
+  if (frames_list.empty()) frames_list = {2500, 5000, 10000, 20000};
+  int64_t nf_max = 0;
+  for (int64_t f : frames_list) nf_max = std::max(nf_max, f);
+  const int64_t fs = 3 * n;
   float *x;
   CK(hipMalloc(&x, sizeof(float) * fs * nf_max));
   if (rmsf_synth_frames(x, fs, n, 0, nf_max, 0, nullptr, nullptr)) return 1;
@@ -41,6 +49,10 @@ int main() {
   };
   auto launch = [&](int64_t nf, int per_cu, int groups, int S = 0) {
     const SkPlan pl = S > 0 ? plan_s(nf, S) : sk_plan(3 * n / 4, 4, nf, groups, RMSF_MODE_WELFORD, per_cu);
+    if (sk_bytes(pl, true) > ab) {  // never launch past the workspace
+      printf("skip: G %d needs %zu B of partials (> %zu)\n", pl.G, sk_bytes(pl, true), ab);
+      return -1;
+    }
     int64_t *hdr = static_cast<int64_t *>(acc);
     double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
     double *p1 = p0 + (size_t)pl.G * pl.P * kBlock * 4;
@@ -48,13 +60,14 @@ int main() {
     return pl.G;
   };
   for (int rep = 0; rep < 2; ++rep) {
-    for (int64_t nf : {2500, 5000, 10000, 20000}) {
+    for (int64_t nf : frames_list) {
       for (int v = 0; v < 12; ++v) {
         static const int kG[] = {512, 768, 1024, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         static const int kS[] = {0, 0, 0, 1, 2, 3, 4, 5, 7, 10, 13, 20};
         const int groups = kG[v], S = kS[v];
         int G = 0;
         for (int i = 0; i < 3; ++i) G = launch(nf, 3, groups, S);
+        if (G < 0) continue;
         CK(hipDeviceSynchronize());
         float best = 1e9, sum = 0;
         const int R = 20;
@@ -75,8 +88,8 @@ int main() {
     }
   }
   // back-to-back launches (a step loop): the gap between dependent launches
-  for (int64_t nf : {2500, 20000}) {
-    const int K = 50;
+  for (int64_t nf : frames_list) {
+    const int K = 20;
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(a));
     for (int i = 0; i < K; ++i) launch(nf, 3, 0);
