@@ -178,6 +178,22 @@ int rmsf_chan_deviation(const double *d_mean_k, const double *d_m2_k,
                         const double *d_mean, double n_k, int64_t n,
                         double *d_out, void *stream);
 
+/* One-collective form of the same merge (RMSF.py:140-143 + 146): moments
+ * about a shift c held by every rank (c[j] = shift[j] + off3[j % 3]; shift
+ * f64, or f32 when shift_is_f32; off3 may be NULL):
+ *   pack:   d_t[0:n] = n_k (mean_k - c),  d_t[n:2n] = M2_k + n_k (mean_k - c)^2
+ *   -- one all-reduce(SUM) of d_t[0:2n] over the ranks --
+ *   finish: mean = c + T1/n,  M2 = max(T2 - T1^2/n, 0),  rmsf = sqrt(sum M2 / n)
+ * (d_rmsf may be NULL; n = 3 n_sel coordinates).                           */
+int rmsf_chan_shift_pack(const double *d_mean_k, const double *d_m2_k,
+                         const void *d_shift, int shift_is_f32,
+                         const double *d_off3, double n_k, int64_t n,
+                         double *d_t, void *stream);
+int rmsf_chan_shift_finish(const double *d_t, const void *d_shift,
+                           int shift_is_f32, const double *d_off3,
+                           int64_t n_sel, int64_t n_frames, double *d_mean,
+                           double *d_m2, double *d_rmsf, void *stream);
+
 /* ---- finalise: RMSF.py:146  rmsf = sqrt(M2.sum(axis=1) / n) ---------------*/
 int rmsf_finalize(const double *d_m2, int64_t n_sel, int64_t n_frames,
                   double *d_rmsf, void *stream);

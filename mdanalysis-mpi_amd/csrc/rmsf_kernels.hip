@@ -1237,6 +1237,53 @@ __global__ __launch_bounds__(kBlock) void k_chan_deviation(const double *__restr
   y[j] = qk[j] + nk * (d * d);
 }
 
+// One-collective cross-rank merge (RMSF.py:140-143 + 146): moments about a
+// shift c that every rank holds (the reference structure, the sweep-1
+// average, or trajectory frame 0 broadcast during the sweep).  Per rank
+//   T1 = n_k (mean_k - c),   T2 = M2_k + n_k (mean_k - c)^2
+// summed over ranks in ONE all-reduce; then mean = c + T1/n and
+// M2 = T2 - T1^2/n -- Chan's k-way formula in exact arithmetic, and with c
+// near the data (|mean - c| ~ the fluctuation) free of cancellation.
+template <typename ShiftT>
+__global__ __launch_bounds__(kBlock) void k_chan_shift_pack(const double *__restrict__ mk,
+                                                            const double *__restrict__ qk,
+                                                            const ShiftT *__restrict__ shift,
+                                                            const double *__restrict__ off3, double nk, int64_t n,
+                                                            double *__restrict__ t) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  double c = (double)shift[j];
+  if (off3) c += off3[j % 3];
+  const double d = mk[j] - c;
+  t[j] = nk * d;
+  t[n + j] = qk[j] + nk * (d * d);
+}
+
+template <typename ShiftT>
+__global__ __launch_bounds__(kBlock) void k_chan_shift_finish(const double *__restrict__ t,
+                                                              const ShiftT *__restrict__ shift,
+                                                              const double *__restrict__ off3, int64_t n_sel,
+                                                              double nf, double *__restrict__ mean,
+                                                              double *__restrict__ m2, double *__restrict__ rmsf) {
+  const int64_t a = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (a >= n_sel) return;
+  const int64_t n = 3 * n_sel;
+  double q[3];
+#pragma unroll
+  for (int x = 0; x < 3; ++x) {
+    const int64_t j = 3 * a + x;
+    double c = (double)shift[j];
+    if (off3) c += off3[x];
+    const double t1 = t[j];
+    mean[j] = c + t1 / nf;
+    // the two sums are of non-negative terms whose difference rounds to
+    // >= -eps * T2: clamp so that sqrt below never sees a negative zero-sum
+    q[x] = fmax(t[n + j] - t1 * (t1 / nf), 0.0);
+    m2[j] = q[x];
+  }
+  if (rmsf) rmsf[a] = sqrt((q[0] + q[1] + q[2]) / nf);
+}
+
 __global__ __launch_bounds__(kBlock) void k_finalize(const double *__restrict__ m2, int64_t n_sel, double nf,
                                                      double *__restrict__ out) {
   const int64_t a = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1817,6 +1864,34 @@ RMSF_EXPORT int rmsf_chan_deviation(const double *d_mean_k, const double *d_m2_k
   hipLaunchKernelGGL(k_chan_deviation, dim3(grid1(n)), dim3(kBlock), 0, S(stream), d_mean_k, d_m2_k, d_mean, n_k, n,
                      d_out);
   return after_launch("k_chan_deviation");
+}
+
+RMSF_EXPORT int rmsf_chan_shift_pack(const double *d_mean_k, const double *d_m2_k, const void *d_shift,
+                                     int shift_is_f32, const double *d_off3, double n_k, int64_t n, double *d_t,
+                                     void *stream) {
+  if (!d_mean_k || !d_m2_k || !d_shift || !d_t || n < 1 || n_k < 0)
+    return fail(RMSF_EINVAL, "rmsf_chan_shift_pack: bad arguments");
+  if (shift_is_f32)
+    hipLaunchKernelGGL(k_chan_shift_pack<float>, dim3(grid1(n)), dim3(kBlock), 0, S(stream), d_mean_k, d_m2_k,
+                       static_cast<const float *>(d_shift), d_off3, n_k, n, d_t);
+  else
+    hipLaunchKernelGGL(k_chan_shift_pack<double>, dim3(grid1(n)), dim3(kBlock), 0, S(stream), d_mean_k, d_m2_k,
+                       static_cast<const double *>(d_shift), d_off3, n_k, n, d_t);
+  return after_launch("k_chan_shift_pack");
+}
+
+RMSF_EXPORT int rmsf_chan_shift_finish(const double *d_t, const void *d_shift, int shift_is_f32, const double *d_off3,
+                                       int64_t n_sel, int64_t n_frames, double *d_mean, double *d_m2,
+                                       double *d_rmsf, void *stream) {
+  if (!d_t || !d_shift || !d_mean || !d_m2 || n_sel < 1) return fail(RMSF_EINVAL, "rmsf_chan_shift_finish: bad arguments");
+  if (n_frames < 1) return fail(RMSF_EEMPTY, "rmsf_chan_shift_finish: no frames");
+  if (shift_is_f32)
+    hipLaunchKernelGGL(k_chan_shift_finish<float>, dim3(grid1(n_sel)), dim3(kBlock), 0, S(stream), d_t,
+                       static_cast<const float *>(d_shift), d_off3, n_sel, (double)n_frames, d_mean, d_m2, d_rmsf);
+  else
+    hipLaunchKernelGGL(k_chan_shift_finish<double>, dim3(grid1(n_sel)), dim3(kBlock), 0, S(stream), d_t,
+                       static_cast<const double *>(d_shift), d_off3, n_sel, (double)n_frames, d_mean, d_m2, d_rmsf);
+  return after_launch("k_chan_shift_finish");
 }
 
 RMSF_EXPORT int rmsf_finalize(const double *d_m2, int64_t n_sel, int64_t n_frames, double *d_rmsf, void *stream) {

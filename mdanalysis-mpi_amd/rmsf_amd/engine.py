@@ -120,6 +120,35 @@ class Engine:
         call("rmsf_chan_deviation", mean_k.data_ptr(), m2_k.data_ptr(), mean.data_ptr(), float(n_k), mean_k.numel(),
              out.data_ptr(), self.stream)
 
+    def chan_shift_pack(self, mean_k, m2_k, shift, off3, n_k: float, out) -> None:
+        """out[0:n] = n_k (mean_k - c), out[n:2n] = M2_k + n_k (mean_k - c)^2,
+        c = shift + off3 (per xyz); shift f64 or f32."""
+        n = mean_k.numel()
+        if out.numel() < 2 * n or shift.numel() < n:
+            raise ValueError("chan_shift_pack: buffer sizes")
+        call("rmsf_chan_shift_pack", mean_k.data_ptr(), m2_k.data_ptr(), shift.data_ptr(),
+             int(shift.dtype == torch.float32), _ptr(off3), float(n_k), n, out.data_ptr(), self.stream)
+
+    def chan_shift_finish(self, t, shift, off3, n_sel: int, n_frames: int, mean, m2, rmsf) -> None:
+        if t.numel() < 6 * n_sel or shift.numel() < 3 * n_sel or mean.numel() < 3 * n_sel or m2.numel() < 3 * n_sel:
+            raise ValueError("chan_shift_finish: buffer sizes")
+        call("rmsf_chan_shift_finish", t.data_ptr(), shift.data_ptr(), int(shift.dtype == torch.float32), _ptr(off3),
+             n_sel, n_frames, mean.data_ptr(), m2.data_ptr(), _ptr(rmsf), self.stream)
+
+    def zero_index(self) -> torch.Tensor:
+        """A resident int64 [0] (row index for gathering one frame); made once."""
+        if getattr(self, "_zero_idx", None) is None:
+            self._zero_idx = torch.zeros(1, dtype=torch.int64, device=self.device)
+        return self._zero_idx
+
+    def gather_frames(self, base_ptr: int, fstride: int, rows: torch.Tensor, n: int, n_sel: int, sel,
+                      out: torch.Tensor) -> None:
+        """out[i] = frame base + rows[i]*fstride, selected (rmsf_gather_frames)."""
+        if out.dtype != F32 or out.numel() < 3 * n_sel * n or rows.numel() < n:
+            raise ValueError("gather_frames: buffer sizes")
+        call("rmsf_gather_frames", base_ptr, fstride, rows.data_ptr(), n, n_sel, _ptr(sel), out.data_ptr(),
+             self.stream)
+
     def finalize(self, m2: torch.Tensor, n_sel: int, n_frames: int, out: torch.Tensor) -> None:
         """RMSF.py:146: sqrt(M2.sum(axis=1)/n)."""
         call("rmsf_finalize", m2.data_ptr(), n_sel, n_frames, out.data_ptr(), self.stream)

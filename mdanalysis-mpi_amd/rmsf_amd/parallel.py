@@ -4,13 +4,16 @@ Replaces the mpi4py layer of RMSF.py:
   * RMSF.py:59-72  rank/size + contiguous frame blocks   -> ``blocks()``
   * RMSF.py:107-111 Barrier + Allreduce(SUM) of positions -> ``allreduce_sum_``
   * RMSF.py:141-143 Barrier + pickle comm.reduce(second_order_moments)
-        -> ``global_chan``: an exact k-way Chan merge as two all-reduce(SUM)
-           passes over RCCL (torch.distributed "nccl" backend = RCCL on ROCm).
+        -> ``global_chan_shifted``: the k-way Chan merge as ONE all-reduce(SUM)
+           of moments about a shift every rank holds (the pipeline's form), or
+           ``global_chan``: the same merge as two all-reduce(SUM) passes
+           (mean, then deviations) -- over RCCL (torch.distributed "nccl"
+           backend = RCCL on ROCm).
 
 One process per GPU (torch.distributed.run); the frames shard with no data
-path collective except these two exchange steps.  ``global_chan`` takes an
-``ops`` object for its two element-wise steps: on the GPU that is the
-``Engine`` (HIP kernels); the CPU gloo tests pass the oracle's restatement.
+path collective except these exchange steps.  The merges take an ``ops``
+object for their element-wise steps: on the GPU that is the ``Engine`` (HIP
+kernels); the CPU gloo tests pass the oracle's restatement.
 """
 from __future__ import annotations
 
@@ -70,6 +73,43 @@ def global_chan(ops, mean_k: torch.Tensor, m2_k: torch.Tensor, n_k: int, n_total
     ops.chan_deviation(mean_k, m2_k, mean, float(n_k), m2)
     allreduce_sum_(m2)
     return mean, m2
+
+
+def broadcast_async(t: torch.Tensor, src: int):
+    """Start an in-place broadcast from ``src``; returns the work (wait() orders
+    the then-current stream after it), or None for a single process."""
+    _, size = world()
+    if size > 1:
+        return dist.broadcast(t, src=src, async_op=True)
+    return None
+
+
+def global_chan_shifted(ops, mean_k: torch.Tensor, m2_k: torch.Tensor, n_k: int, n_total: int, shift: torch.Tensor,
+                        off3: torch.Tensor | None = None, shift_work=None):
+    """The k-way Chan merge in ONE all-reduce: moments about a shift c that
+    every rank already holds (c = shift + off3 per xyz: the sweep's reference
+    structure, the sweep-1 average, or frame 0 broadcast during the sweep).
+
+    T1 = sum_k n_k (mean_k - c),  T2 = sum_k [M2_k + n_k (mean_k - c)^2]
+    mean = c + T1/n,  M2 = T2 - T1^2/n   (= Chan's k-way merge in exact
+    arithmetic; c within the fluctuation of the data keeps it free of
+    cancellation).  Returns (mean, M2, rmsf) -- the finalise of RMSF.py:146 is
+    fused into the unpacking.  ``shift_work``: the pending broadcast that
+    fills ``shift``, waited for here (it ran beside the sweep)."""
+    _, size = world()
+    if n_total <= 0:
+        raise ZeroDivisionError("global_chan_shifted: no frames on any rank")
+    n = mean_k.numel()
+    t = torch.empty(2 * n, dtype=mean_k.dtype, device=mean_k.device)
+    if shift_work is not None:
+        shift_work.wait()
+    ops.chan_shift_pack(mean_k, m2_k, shift, off3, float(n_k), t)
+    if size > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    mean, m2 = torch.empty_like(mean_k), torch.empty_like(m2_k)
+    rmsf = torch.empty(n // 3, dtype=mean_k.dtype, device=mean_k.device)
+    ops.chan_shift_finish(t, shift, off3, n // 3, n_total, mean, m2, rmsf)
+    return mean, m2, rmsf
 
 
 def barrier() -> None:

@@ -7,8 +7,8 @@ Per rank (one process per GPU):
                   and sums (RMSF.py:89-105); all-reduce + divide gives the
                   average structure (RMSF.py:107-111); sweep 2 superposes on
                   the centred average and runs Welford (RMSF.py:113-140).
-then the exact cross-rank Chan merge (RMSF.py:141-143) and the finalise
-(RMSF.py:145-146).  Every launch is asynchronous on the current stream; the
+then the cross-rank Chan merge (RMSF.py:141-143: one all-reduce of moments
+about a shift every rank holds) and the finalise (RMSF.py:145-146).  Every launch is asynchronous on the current stream; the
 only host synchronisation is the final copy of the result.
 """
 from __future__ import annotations
@@ -220,6 +220,19 @@ def reference_from_frame(eng: Engine, source, frame: int, n_sel: int, masses, ow
     return r, i
 
 
+def _frame_shift(eng: Engine, source, frames: FrameList, n_total: int, size: int, rank: int):
+    """Frame 0 of the list, selected, as f32 on every rank: gathered by the
+    rank whose RMSF.py:65-69 block starts with it and broadcast asynchronously
+    (the broadcast runs beside the sweep; the merge waits for it)."""
+    owner = next(r for r, (a, b) in enumerate(parallel.blocks(n_total, size)) if b > a)
+    buf = torch.empty(3 * source.n_sel, dtype=torch.float32, device=eng.device)
+    if rank == owner:
+        b = source.reference(frames[0], eng.stream)
+        eng.gather_frames(b.ptr, b.fstride, eng.zero_index(), 1, source.n_sel, b.sel, buf)
+        b.done()
+    return buf, parallel.broadcast_async(buf, owner)
+
+
 def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=None, ref_frame: int = 0,
                  max_batch: int | None = None, n_splits: int | None = None, collect_rmsd: bool = False,
                  ref_owner: int | None = None, block: tuple[int, int] | None = None,
@@ -272,12 +285,29 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     else:
         ref = info = None
 
+    # The merge's shift (parallel.global_chan_shifted): something every rank
+    # holds near the data -- the last sweep's reference structure, or (no
+    # alignment) frame 0 of the list, broadcast by its owner while the sweep
+    # streams.
+    shift = off3 = shift_work = None
+    if size > 1:
+        if align == "average":
+            shift = average
+        elif align == "frame0":
+            shift, off3 = ref, info[:3]
+        else:
+            shift, shift_work = _frame_shift(eng, source, frames, n_total, size, rank)
+
     acc = Accumulator(eng, n_sel, RMSF_MODE_WELFORD, max_batch, aligned, n_splits, timer)
     if n_local:
         sweep(acc, ref, info)
-    mean, m2 = parallel.global_chan(eng, acc.result0, acc.result1, acc.n, n_total)  # RMSF.py:141-143
-    rmsf = eng.empty(n_sel)
-    eng.finalize(m2, n_sel, n_total, rmsf)                   # RMSF.py:146
+    if size > 1:                                             # RMSF.py:141-143 + 146: one all-reduce
+        mean, m2, rmsf = parallel.global_chan_shifted(eng, acc.result0, acc.result1, acc.n, n_total,
+                                                      shift, off3, shift_work)
+    else:
+        mean, m2 = acc.result0, acc.result1
+        rmsf = eng.empty(n_sel)
+        eng.finalize(m2, n_sel, n_total, rmsf)               # RMSF.py:146
     return PipelineResult(rmsf=rmsf, mean=mean.view(n_sel, 3), m2=m2.view(n_sel, 3), n_frames=n_total,
                           n_local=n_local, block=(b0, b1),
                           average=None if average is None else average.view(n_sel, 3), rmsd=rmsd)

@@ -18,3 +18,42 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); run with -m gpu")
+
+
+def spawn_ranks(target, size: int, args_fn, timeout: float = 120.0) -> list:
+    """Run ``target`` in ``size`` spawned processes (one torch.distributed
+    rank each) and return what they put on the queue.  Ranks rendezvous
+    through a fresh file (``init`` = file:// URL: no TCP port to collide
+    with), and every child still alive when this returns -- a rank stuck in a
+    collective after its peer failed -- is terminated, so a failing case can
+    never leave the test run waiting on a hung child.
+    ``args_fn(rank, init, q)`` builds each process's arguments."""
+    import tempfile
+
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    d = tempfile.mkdtemp(prefix="rmsf_rdv_")
+    init = "file://" + os.path.join(d, "store")
+    procs = [ctx.Process(target=target, args=args_fn(r, init, q), daemon=True) for r in range(size)]
+    try:
+        for p in procs:
+            p.start()
+        return [q.get(timeout=timeout) for _ in range(size)]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+
+
+def init_gloo(init: str, rank: int, size: int) -> None:
+    """gloo process group over a file rendezvous (see spawn_ranks)."""
+    from datetime import timedelta
+
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=size, timeout=timedelta(seconds=120))

@@ -7,14 +7,12 @@ HIP kernels, which need a GPU) and then runs the *product's* cross-rank code
 Chan merge.  The element-wise steps of the merge are injected through an
 ``ops`` object -- here the oracle's numpy restatement of the two kernels."""
 import os
-import socket
 import sys
 
 import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
-import torch.multiprocessing as mp
 
 from conftest import PKG, ROOT
 
@@ -31,19 +29,32 @@ class OracleOps:
         d = mean_k.numpy() - mean.numpy()
         out.copy_(torch.from_numpy(m2_k.numpy() + n_k * (d * d)))
 
+    # k_chan_shift_pack / k_chan_shift_finish (the one-all-reduce merge)
+    @staticmethod
+    def _c(shift, off3, n):
+        c = shift.numpy().astype(np.float64)[:n]
+        return c + np.tile(off3.numpy(), n // 3) if off3 is not None else c
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    @staticmethod
+    def chan_shift_pack(mean_k, m2_k, shift, off3, n_k, out):
+        n = mean_k.numel()
+        d = mean_k.numpy() - OracleOps._c(shift, off3, n)
+        out.copy_(torch.from_numpy(np.concatenate([n_k * d, m2_k.numpy() + n_k * (d * d)])))
+
+    @staticmethod
+    def chan_shift_finish(t, shift, off3, n_sel, n, mean, m2, rmsf):
+        c = OracleOps._c(shift, off3, 3 * n_sel)
+        t1, t2 = t.numpy()[:3 * n_sel], t.numpy()[3 * n_sel:6 * n_sel]
+        q = np.maximum(t2 - t1 * (t1 / n), 0.0)
+        mean.copy_(torch.from_numpy(c + t1 / n))
+        m2.copy_(torch.from_numpy(q))
+        rmsf.copy_(torch.from_numpy(np.sqrt(q.reshape(-1, 3).sum(axis=1) / n)))
 
 
-def _worker(rank, size, port, n_frames, q):
+def _worker(rank, size, port, n_frames, q, merge="two"):
     sys.path[:0] = [ROOT, PKG]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=size)
+    from conftest import init_gloo
+    init_gloo(port, rank, size)
     try:
         from oracle import rmsf_oracle as O
         from oracle import synth as SY
@@ -62,31 +73,46 @@ def _worker(rank, size, port, n_frames, q):
         ref_com2, ref_c2 = O.centred_reference(avg)
         # sweep 2 (RMSF.py:120-140) + product k-way Chan (replaces :143)
         n_k, mean_k, m2_k = O.rank_sweep2(traj, sel, None, b0, b1, ref_c2, ref_com2)
-        mean, m2 = parallel.global_chan(OracleOps, torch.from_numpy(mean_k.reshape(-1).copy()),
-                                        torch.from_numpy(m2_k.reshape(-1).copy()), n_k, n_frames)
-        rmsf = np.sqrt(m2.numpy().reshape(-1, 3).sum(axis=1) / n_frames)
+        mean_k = torch.from_numpy(mean_k.reshape(-1).copy())
+        m2_k = torch.from_numpy(m2_k.reshape(-1).copy())
+        if merge == "two":
+            mean, m2 = parallel.global_chan(OracleOps, mean_k, m2_k, n_k, n_frames)
+            rmsf = np.sqrt(m2.numpy().reshape(-1, 3).sum(axis=1) / n_frames)
+        else:
+            # the pipeline's one-all-reduce merge, shifted by the sweep-2
+            # reference (f64 centred + COM: align="frame0"'s form), by the
+            # sweep-1 average (f64: align="average"), or by frame 0 (f32,
+            # broadcast by the owner of block 0: no alignment)
+            if merge == "ref":
+                shift, off3, work = torch.from_numpy(ref_c2.reshape(-1).copy()), torch.from_numpy(ref_com2), None
+            elif merge == "average":
+                shift, off3, work = torch.from_numpy(avg.reshape(-1).copy()), None, None
+            else:
+                owner = next(r for r, (a, b) in enumerate(parallel.blocks(n_frames, size)) if b > a)
+                shift = torch.zeros(3 * len(sel), dtype=torch.float32)
+                if rank == owner:
+                    shift.copy_(torch.from_numpy(traj[0][sel].reshape(-1)))
+                off3, work = None, parallel.broadcast_async(shift, owner)
+            mean, m2, rmsf_t = parallel.global_chan_shifted(OracleOps, mean_k, m2_k, n_k, n_frames, shift, off3,
+                                                            work)
+            rmsf = rmsf_t.numpy()
         q.put((rank, rmsf, avg))
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("merge", ["two", "ref", "average", "frame0"])
 @pytest.mark.parametrize("size,n_frames", [(2, 40), (3, 40), (2, 1), (3, 2)])
-def test_gloo_two_sweep_merge(size, n_frames):
-    """world_size 2/3, including ranks with empty blocks (n_frames < size)."""
+def test_gloo_two_sweep_merge(size, n_frames, merge):
+    """world_size 2/3, including ranks with empty blocks (n_frames < size);
+    the two-all-reduce Chan merge and the one-all-reduce shifted form with
+    each of the pipeline's shifts."""
     from oracle import rmsf_oracle as O
     from oracle import synth as SY
     from rmsf_amd.synth import motion_table
 
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, size, port, n_frames, q)) for r in range(size)]
-    for p in procs:
-        p.start()
-    out = [q.get(timeout=120) for _ in range(size)]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    from conftest import spawn_ranks
+    out = spawn_ranks(_worker, size, lambda r, init, q: (r, size, init, n_frames, q, merge))
     traj = SY.frames(8, 60, 0, n_frames, motion_table(9, n_frames))
     ref = O.rmsf_script(traj, np.arange(0, 60, 3), None, size=1, align="average")
     for rank, rmsf, avg in out:

@@ -10,7 +10,6 @@ merged on the host and over RCCL (ncclCommInitAll on one device), the
 callback transport across two processes (gloo), the plain-C host program,
 and the error contract."""
 import os
-import socket
 import subprocess
 import sys
 
@@ -224,19 +223,12 @@ def test_plain_c_host_program(c1, tmp_path):
 
 
 # ---- callback transport across processes (gloo on cuda:0) -------------------
-def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def _cb_worker(rank, size, port, q):
     sys.path[:0] = [ROOT, PKG]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=size)
+
+    from conftest import init_gloo
+    init_gloo(port, rank, size)
     try:
         from oracle import synth as SY2
         from rmsf_amd.context import PUSH_ALIGN_SUM, PUSH_ALIGN_WELFORD, Context
@@ -261,17 +253,9 @@ def _cb_worker(rank, size, port, q):
 
 @pytest.mark.parametrize("size", [2, 3])
 def test_context_callback_transport_processes(size):
-    import torch.multiprocessing as mp
+    from conftest import spawn_ranks
     from rmsf_amd.synth import motion_table
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _port()
-    procs = [ctx.Process(target=_cb_worker, args=(r, size, port, q)) for r in range(size)]
-    for p in procs:
-        p.start()
-    out = [q.get(timeout=100) for _ in range(size)]
-    for p in procs:
-        p.join(timeout=60)
+    out = spawn_ranks(_cb_worker, size, lambda r, init, q: (r, size, init, q), timeout=100)
     traj = SY.frames(2, 700, 0, 41, motion_table(3, 41))
     exp = O.rmsf_script(traj, np.arange(5, 700, 3), None, size=size, align="average")["rmsf"]
     for rank, rmsf, n in out:

@@ -290,6 +290,54 @@ def test_chan_merge_kernel_many_groups(eng):
     assert issubclass(RmsfEmptyError, ZeroDivisionError)
 
 
+@pytest.mark.parametrize("shift_kind", ["f64", "f64+off3", "f32"])
+def test_chan_shift_merge_kernels(eng, shift_kind):
+    """k_chan_shift_pack / k_chan_shift_finish: the one-all-reduce merge
+    (parallel.global_chan_shifted) of P rank partials -- the packed sums
+    added as the all-reduce would -- against the pooled mean / M2 / RMSF
+    (RMSF.py:140-146) and against the two-collective Chan kernels; identical
+    frames give exactly 0 when the shift is the data."""
+    rng = np.random.default_rng(5)
+    n_sel, counts = 211, [7, 0, 13, 1]
+    n = 3 * n_sel
+    base = rng.uniform(0, 100, n)
+    data = [base + rng.normal(scale=1.5, size=(c, n)) for c in counts]
+    mp = [d.mean(0) if len(d) else np.zeros(n) for d in data]
+    qp = [((d - d.mean(0)) ** 2).sum(0) if len(d) else np.zeros(n) for d in data]
+    nt = sum(counts)
+    f0 = data[0][0].astype(np.float32)
+    if shift_kind == "f32":
+        shift, off3 = torch.tensor(f0, device=eng.device), None
+    elif shift_kind == "f64":
+        shift, off3 = torch.tensor(f0.astype(np.float64), device=eng.device), None
+    else:
+        com = f0.reshape(-1, 3).astype(np.float64).mean(0)
+        shift = torch.tensor(f0.reshape(-1, 3) - com, device=eng.device).reshape(-1)
+        off3 = torch.tensor(com, device=eng.device)
+    t = torch.zeros(2 * n, dtype=torch.float64, device=eng.device)
+    for m, q, c in zip(mp, qp, counts):
+        tk = eng.empty(2 * n)
+        eng.chan_shift_pack(torch.tensor(m, device=eng.device), torch.tensor(q, device=eng.device), shift, off3, c, tk)
+        t += tk  # the all-reduce's sum
+    mean, m2, rmsf = eng.empty(n), eng.empty(n), eng.empty(n_sel)
+    eng.chan_shift_finish(t, shift, off3, n_sel, nt, mean, m2, rmsf)
+    _sync()
+    allx = np.concatenate([d for d in data if len(d)])
+    q_all = ((allx - allx.mean(0)) ** 2).sum(0)
+    np.testing.assert_allclose(mean.cpu().numpy(), allx.mean(0), rtol=0, atol=1e-12)
+    np.testing.assert_allclose(m2.cpu().numpy(), q_all, rtol=1e-11)
+    np.testing.assert_allclose(rmsf.cpu().numpy(), np.sqrt(q_all.reshape(-1, 3).sum(1) / nt), rtol=0, atol=1e-12)
+    # identical frames about the same frame: exactly zero
+    same = torch.tensor(np.tile(f0.astype(np.float64), 1), device=eng.device)
+    tk = eng.empty(2 * n)
+    eng.chan_shift_pack(same, torch.zeros(n, dtype=torch.float64, device=eng.device),
+                        torch.tensor(f0, device=eng.device), None, 5, tk)
+    eng.chan_shift_finish(tk, torch.tensor(f0, device=eng.device), None, n_sel, 5, mean, m2, rmsf)
+    _sync()
+    assert float(rmsf.abs().max()) == 0.0 and float(m2.abs().max()) == 0.0
+    np.testing.assert_array_equal(mean.cpu().numpy(), f0.astype(np.float64))
+
+
 def test_second_order_moments_api(eng):
     from rmsf_amd import second_order_moments
     rng = np.random.default_rng(1)

@@ -7,7 +7,6 @@ only its own frame shard in HBM (RMSF.py:65-69 blocks), the reference frame's
 owner computes and broadcasts it, sweep 1 is all-reduced, and the exact k-way
 Chan merge runs through the HIP kernels."""
 import os
-import socket
 import sys
 
 import numpy as np
@@ -18,20 +17,13 @@ from conftest import PKG, ROOT
 pytestmark = pytest.mark.gpu
 
 
-def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def _worker(rank, size, port, align, n_frames, q):
     sys.path[:0] = [ROOT, PKG]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=size)
+
+    from conftest import init_gloo
+    init_gloo(port, rank, size)
     try:
         from rmsf_amd import parallel
         from rmsf_amd.engine import Engine
@@ -55,22 +47,14 @@ def _worker(rank, size, port, align, n_frames, q):
 
 
 @pytest.mark.parametrize("size,n_frames,align", [(2, 41, "average"), (2, 41, "frame0"), (2, 30, None),
-                                                 (3, 2, "average")])
+                                                 (3, 2, "average"), (3, 2, None), (3, 40, None), (3, 40, "frame0")])
 def test_sharded_pipeline_two_processes(size, n_frames, align):
-    import torch.multiprocessing as mp
     from oracle import rmsf_oracle as O
     from oracle import synth as SY
     from rmsf_amd.synth import motion_table
 
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, size, port, align, n_frames, q)) for r in range(size)]
-    for p in procs:
-        p.start()
-    out = [q.get(timeout=100) for _ in range(size)]
-    for p in procs:
-        p.join(timeout=60)
+    from conftest import spawn_ranks
+    out = spawn_ranks(_worker, size, lambda r, init, q: (r, size, init, align, n_frames, q), timeout=100)
     for rank, r, n_local in out:
         assert n_local >= 0, r
     traj = SY.frames(2, 700, 0, n_frames, motion_table(3, n_frames))
