@@ -573,14 +573,19 @@ __global__ __launch_bounds__(kBlock *Q) void k_accum_split_sk(const float *__res
 // Fold the balanced partials of one batch, in frame order, into the running
 // result (acc_n frames already in acc0/acc1; 0 = overwrite): Chan's merge
 // (second_order_moments, RMSF.py:36-41) for WELFORD, a sum for SUM.  One
-// thread per coordinate; it replays the segment walk of the workgroups that
-// cover its chunk (fixed order: bitwise reproducible).
+// thread per lane (its cpl = 3 or 4 coordinates, which share the segment
+// walk); it replays the walk of the workgroups that cover its chunk in a
+// fixed order (bitwise reproducible) and loads the partials of up to
+// kFoldBatch segments before folding any of them, so a chunk covered by a
+// few ranges costs one memory round trip, not one per segment.  The walk is
+// uniform per wave (a chunk is 256 lanes), its divisions stay off the
+// critical path of the loads.
+constexpr int kFoldBatch = 4;
 __global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ hdr,
                                                     const double *__restrict__ parts0, int64_t n_coord,
                                                     double acc_n, double *__restrict__ acc0,
                                                     double *__restrict__ acc1) {
-  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (j >= n_coord) return;
+  const int64_t l = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   SkPlan pl;
   pl.lanes = hdr[0];
   pl.C = hdr[1];
@@ -592,55 +597,100 @@ __global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ 
   pl.mode = (int)hdr[7];
   pl.S = (int)hdr[8];
   pl.cw = (int)hdr[9];
-  const int64_t lane = j / pl.cpl;
-  const int64_t c = lane / pl.cw;
+  if (l >= pl.lanes) return;
+  const int cpl = pl.cpl;
+  const int64_t j0 = l * cpl;  // first coordinate of the lane
+  const int nx = (int)(n_coord - j0 < cpl ? n_coord - j0 : cpl);
+  const int64_t c = l / pl.cw;
   const int64_t slot_d = (int64_t)pl.cw * pl.cpl;
-  const int64_t off = j - c * slot_d;
+  const int64_t off = j0 - c * slot_d;
   const int64_t clo = c * pl.nf, chi = clo + pl.nf;
   const double *__restrict__ parts1 = parts0 + (int64_t)pl.G * pl.P * slot_d;
-  // first workgroup whose range ends after the chunk starts
+  const bool wel = pl.mode == RMSF_MODE_WELFORD;
+  double n1 = acc_n, mu[4] = {0.0, 0.0, 0.0, 0.0}, M[4] = {0.0, 0.0, 0.0, 0.0};
+  if (acc_n > 0) {
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      if (x < nx) {
+        mu[x] = acc0[j0 + x];
+        if (wel) M[x] = acc1[j0 + x];
+      }
+    }
+  }
+  // first range whose end is past the chunk's start, walked from its start
   int64_t b = clo * pl.G / pl.T;
   while (b > 0 && sk_lo(pl, b) > clo) --b;
   while (sk_lo(pl, b + 1) <= clo) ++b;
-  const bool wel = pl.mode == RMSF_MODE_WELFORD;
-  double n1 = acc_n, mu = 0.0, M = 0.0;
-  if (acc_n > 0) {
-    mu = acc0[j];
-    if (wel) M = acc1[j];
+  int64_t lo = sk_lo(pl, b), hi = sk_lo(pl, b + 1), slot = b * pl.P;
+  while (lo < clo) {
+    int64_t cc, f0;
+    lo += sk_seg_len(pl, lo, hi, &cc, &f0);
+    ++slot;
   }
-  for (; b < pl.G; ++b) {
-    int64_t lo = sk_lo(pl, b);
-    if (lo >= chi) break;
-    const int64_t hi = sk_lo(pl, b + 1);
-    int64_t slot = b * pl.P;
-    while (lo < hi) {
+  for (;;) {
+    int64_t sl[kFoldBatch];
+    double ln[kFoldBatch];
+    int n = 0;
+    while (n < kFoldBatch) {
+      if (lo >= hi) {
+        if (++b >= pl.G) break;
+        lo = sk_lo(pl, b);
+        hi = sk_lo(pl, b + 1);
+        slot = b * pl.P;
+      }
+      if (lo >= chi) break;
       int64_t cc, f0;
       const int64_t len = sk_seg_len(pl, lo, hi, &cc, &f0);
-      if (cc > c) break;
-      if (cc == c) {
-        const int64_t o = slot * slot_d + off;
-        if (!wel) {
-          mu += parts0[o];
-        } else if (n1 <= 0) {
-          n1 = (double)len;
-          mu = parts0[o];
-          M = parts1[o];
-        } else {
-          const double n2 = (double)len, mu2 = parts0[o], M2 = parts1[o];
-          const double T = n1 + n2;
-          const double d = mu2 - mu;
-          const double mun = (n1 * mu + n2 * mu2) / T;
-          M = M + M2 + (n1 * n2 / T) * (d * d);
-          mu = mun;
-          n1 = T;
-        }
-      }
+      sl[n] = slot;
+      ln[n] = (double)len;
+      ++n;
       lo += len;
       ++slot;
     }
+    double pm[kFoldBatch][4], pq[kFoldBatch][4];
+#pragma unroll
+    for (int k = 0; k < kFoldBatch; ++k) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        if (k < n && x < nx) {
+          const int64_t o = sl[k] * slot_d + off + x;
+          pm[k][x] = parts0[o];
+          pq[k][x] = wel ? parts1[o] : 0.0;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kFoldBatch; ++k) {
+      if (k < n) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          if (x >= nx) continue;
+          if (!wel) {
+            mu[x] += pm[k][x];
+          } else if (n1 <= 0) {
+            mu[x] = pm[k][x];
+            M[x] = pq[k][x];
+          } else {
+            const double n2 = ln[k], mu2 = pm[k][x], M2 = pq[k][x];
+            const double T = n1 + n2;
+            const double d = mu2 - mu[x];
+            const double mun = (n1 * mu[x] + n2 * mu2) / T;
+            M[x] = M[x] + M2 + (n1 * n2 / T) * (d * d);
+            mu[x] = mun;
+          }
+        }
+        if (wel) n1 = n1 <= 0 ? ln[k] : n1 + ln[k];
+      }
+    }
+    if (n < kFoldBatch) break;
   }
-  acc0[j] = mu;
-  if (wel) acc1[j] = M;
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    if (x < nx) {
+      acc0[j0 + x] = mu[x];
+      if (wel) acc1[j0 + x] = M[x];
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1807,7 +1857,8 @@ RMSF_EXPORT int rmsf_fold_balanced(const void *d_work, int64_t n_coord, int mode
   const double *p0 = reinterpret_cast<const double *>(hdr + kSkHdr);
   // the plan (and where parts1 starts) is read from the header the
   // accumulate kernel wrote
-  hipLaunchKernelGGL(k_fold_sk, dim3(grid1(n_coord)), dim3(kBlock), 0, S(stream), hdr, p0, n_coord, (double)acc_n,
+  // one thread per lane of >= 3 coordinates (the plan's cpl is on the device)
+  hipLaunchKernelGGL(k_fold_sk, dim3(grid1((n_coord + 2) / 3)), dim3(kBlock), 0, S(stream), hdr, p0, n_coord, (double)acc_n,
                      d_acc0, d_acc1);
   return after_launch("k_fold_sk");
 }
