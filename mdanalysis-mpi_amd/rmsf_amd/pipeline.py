@@ -8,8 +8,9 @@ Per rank (one process per GPU):
                   average structure (RMSF.py:107-111); sweep 2 superposes on
                   the centred average and runs Welford (RMSF.py:113-140).
 then the cross-rank Chan merge (RMSF.py:141-143: one all-reduce of moments
-about a shift every rank holds) and the finalise (RMSF.py:145-146).  Every launch is asynchronous on the current stream; the
-only host synchronisation is the final copy of the result.
+about a shift every rank holds) and the finalise (RMSF.py:145-146).  Every
+launch is asynchronous on the current stream; the only host synchronisation
+is the final copy of the result.
 """
 from __future__ import annotations
 
