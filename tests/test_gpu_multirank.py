@@ -87,6 +87,64 @@ class _FakeTrajectory:
         return self.ts
 
 
+def _api_worker(rank, size, init, q, kind, path, align, run_kw):
+    """rmsf_amd.RMSF(...).run() on one torch.distributed rank (the script-mode
+    shape: every rank holds the whole input, run() takes its RMSF.py:65-69
+    block; the cross-rank merge is the one-all-reduce form, its shift frame
+    staged from the host or decoded from the XTC by the owner)."""
+    sys.path[:0] = [ROOT, PKG]
+    import torch.distributed as dist
+
+    from conftest import init_gloo
+    init_gloo(init, rank, size)
+    try:
+        from oracle import synth as SY
+        from rmsf_amd import RMSF
+        from rmsf_amd.synth import motion_table
+        sel = np.arange(3, 500, 4)
+        inp = path if kind == "xtc" else SY.frames(4, 500, 0, 37, motion_table(5, 37))
+        r = RMSF(inp, select=sel, align=align, batch_frames=7).run(**run_kw)
+        q.put((rank, r.results.rmsf, r.results.n_frames))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), -1))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["host", "xtc"])
+@pytest.mark.parametrize("align,run_kw", [(None, {}), ("frame0", dict(step=2)), ("average", {}),
+                                          (None, dict(frames=[1, 4, 5, 9, 10, 11, 20, 30, 36])),
+                                          ("average", dict(start=30, stop=2, step=-3))])
+def test_api_under_torch_distributed(tmp_path, kind, align, run_kw):
+    """RMSF(host array | .xtc path).run() on 3 ranks (gloo, one GPU) against
+    the oracle's mpirun -n 3 emulation of the same frame list: staged and
+    XTC-decoded batches, strided / explicit / reversed frame lists, every
+    alignment mode -- each through the one-all-reduce Chan merge."""
+    from conftest import spawn_ranks
+    from oracle import rmsf_oracle as O
+    from oracle import synth as SY
+    from oracle import xtc_py
+    from rmsf_amd.sources import FrameList
+    from rmsf_amd.synth import motion_table
+    from rmsf_amd.xtc import write_xtc
+
+    traj = SY.frames(4, 500, 0, 37, motion_table(5, 37))
+    path = str(tmp_path / "r.xtc")
+    if kind == "xtc":
+        write_xtc(path, traj)
+        traj = xtc_py.read_xtc(path)
+    size = 3
+    out = spawn_ranks(_api_worker, size, lambda r, init, q: (r, size, init, q, kind, path, align, run_kw))
+    fl = FrameList(37, **run_kw)
+    frames = np.array([fl[i] for i in range(len(fl))])
+    sel = np.arange(3, 500, 4)
+    # trajectory frame 0 stays the reference (RMSF.py:80-87) whatever the list
+    exp = O.rmsf_script(traj[np.concatenate([[0], frames])], sel, None, size=size, align=align, start=1)["rmsf"]
+    for rank, rmsf, n in sorted(out, key=lambda o: o[0]):
+        assert n == len(frames), rmsf
+        np.testing.assert_allclose(rmsf, exp, rtol=0, atol=1e-6)
+
+
 class _FakeUniverse:
     def __init__(self, traj):
         self.trajectory = _FakeTrajectory(traj)
