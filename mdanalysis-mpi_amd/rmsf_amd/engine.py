@@ -41,6 +41,14 @@ class Engine:
     def stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 
+    @property
+    def side_stream(self) -> torch.cuda.Stream:
+        """A second stream on the device, for work that must not queue ahead
+        of the launching stream's kernels (the merge shift's gather)."""
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        return self._side
+
     def empty(self, *shape, dtype=F64) -> torch.Tensor:
         return torch.empty(*shape, dtype=dtype, device=self.device)
 

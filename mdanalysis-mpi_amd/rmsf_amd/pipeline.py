@@ -225,13 +225,29 @@ def _frame_shift(eng: Engine, source, frames: FrameList, n_total: int, size: int
     """Frame 0 of the list, selected, as f32 on every rank: gathered by the
     rank whose RMSF.py:65-69 block starts with it and broadcast asynchronously
     (the broadcast runs beside the sweep; the merge waits for it)."""
+    from .sources import DeviceSource
+
     owner = next(r for r, (a, b) in enumerate(parallel.blocks(n_total, size)) if b > a)
     buf = torch.empty(3 * source.n_sel, dtype=torch.float32, device=eng.device)
-    if rank == owner:
-        b = source.reference(frames[0], eng.stream)
-        eng.gather_frames(b.ptr, b.fstride, eng.zero_index(), 1, source.n_sel, b.sel, buf)
-        b.done()
-    return buf, parallel.broadcast_async(buf, owner)
+    idx = eng.zero_index()
+    if not isinstance(source, DeviceSource):  # staged / decoded on the launching stream
+        if rank == owner:
+            b = source.reference(frames[0], eng.stream)
+            eng.gather_frames(b.ptr, b.fstride, idx, 1, source.n_sel, b.sel, buf)
+            b.done()
+        return buf, parallel.broadcast_async(buf, owner)
+    # HBM-resident frames: gather and broadcast from a side stream, so the
+    # owner's sweep is not queued behind them
+    main = torch.cuda.current_stream(eng.device)
+    side = eng.side_stream
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        if rank == owner:
+            b = source.reference(frames[0], eng.stream)
+            eng.gather_frames(b.ptr, b.fstride, idx, 1, source.n_sel, b.sel, buf)
+        work = parallel.broadcast_async(buf, owner)
+    buf.record_stream(side)
+    return buf, work
 
 
 def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=None, ref_frame: int = 0,
