@@ -245,6 +245,7 @@ def _frame_shift(eng: Engine, source, frames: FrameList, n_total: int, size: int
         if rank == owner:
             b = source.reference(frames[0], eng.stream)
             eng.gather_frames(b.ptr, b.fstride, idx, 1, source.n_sel, b.sel, buf)
+            b.done()
         work = parallel.broadcast_async(buf, owner)
     buf.record_stream(side)
     return buf, work
