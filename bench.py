@@ -490,6 +490,7 @@ def main():
     out["roofline"] = roofline(kname, launches, acc_ms, acc_af, traffic,
                                f"profiles/pmc_{a.workload}.json" if traffic else None)
     out["cpu_baseline"] = cpu
+    out["rmsf_checksum"] = float(res.rmsf.sum())  # the merged result, identical on every rank
     # whole-step rate in algorithmic bytes (incl. merges, finalise, launch gaps)
     out["pipeline_hbm_gbs"] = B_PER_ATOM_FRAME * n_atoms * n_local * a.steps / dt / 1e9
     if wl["align"]:

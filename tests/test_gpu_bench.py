@@ -75,3 +75,32 @@ def test_single_process_refuses_missing_devices():
     with pytest.raises(SystemExit, match="visible"):
         bench.device_plan(n, torch.cuda.device_count(), False)
     np.testing.assert_equal(bench.device_plan(n, torch.cuda.device_count(), True)[0], [0] * n)
+
+
+@pytest.mark.parametrize("align", ["none", "frame0", "average"])
+def test_torchrun_two_ranks_same_result_as_one_gpu(align):
+    """The driver's multi-GPU form (torch.distributed.run, one process per
+    rank; gloo ranks sharing the one GPU here, RCCL on a node): strong
+    scaling of one trajectory over 2 ranks gives the 1-GPU run's RMSF (the
+    one-all-reduce merge vs the single-device fold), and the oracle's."""
+    common = ["--n-atoms", "6000", "--frames", "301", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+              "--no-modes", "--align", align]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    one = subprocess.run([sys.executable, "bench.py"] + common, cwd=ROOT, capture_output=True, text=True,
+                         timeout=300, env=env)
+    assert one.returncode == 0, one.stderr[-2000:]
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", "29533", "bench.py", "--gpus", "2",
+                          "--backend", "gloo"] + common, cwd=ROOT, capture_output=True, text=True, timeout=300,
+                         env=env)
+    assert two.returncode == 0, two.stderr[-2000:]
+    l1 = json.loads(one.stdout.strip().splitlines()[-1])
+    l2 = json.loads(two.stdout.strip().splitlines()[-1])
+    assert l2["n_gpus"] == 2 and l2["config"]["n_frames_per_gpu"] == 150
+    assert l1["rmsf_checksum"] == pytest.approx(l2["rmsf_checksum"], rel=1e-12)
+    from rmsf_amd.synth import motion_table
+
+    mt = motion_table(1, 301) if align != "none" else None
+    traj = SY.frames(0, 6000, 0, 301, mt)
+    exp = O.rmsf_script(traj, None, None, size=2, align=None if align == "none" else align)["rmsf"]
+    assert abs(l2["rmsf_checksum"] - float(exp.sum())) < 1e-6 * len(exp)
