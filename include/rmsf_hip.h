@@ -477,6 +477,15 @@ typedef int (*rmsf_allreduce_fn)(double *d_buf, int64_t count, void *stream,
                                  void *user);
 int rmsf_ctx_allreduce_sum(rmsf_ctx *ctx, rmsf_allreduce_fn fn, void *user);
 int rmsf_ctx_chan_merge(rmsf_ctx *ctx, rmsf_allreduce_fn fn, void *user);
+/* The same merge with ONE data all-reduce (2*3*n_sel doubles, plus the
+ * frame-count exchange): moments about the context's reference structure
+ * (rmsf_chan_shift_pack / _finish).  Precondition, as in RMSF.py: every rank
+ * holds the SAME reference (rmsf_ctx_set_reference_frame on the same frame,
+ * or rmsf_ctx_set_reference_average after rmsf_ctx_allreduce_sum); every rank
+ * must call this form (the buffer sizes differ from the two-pass form).
+ * rmsf_multi_chan_merge uses it by itself when all ranks are contexts of the
+ * calling process and each holds a reference.                              */
+int rmsf_ctx_chan_merge_shifted(rmsf_ctx *ctx, rmsf_allreduce_fn fn, void *user);
 
 /* RCCL (librccl.so.1, loaded on first use).  One process per GPU:
  * rank 0 calls rmsf_multi_unique_id, the host broadcasts the 128 bytes, each

@@ -400,6 +400,45 @@ int exchange_chan(rmsf_ctx **cs, int n, const Reduce &red, bool host_counts) {
   return RMSF_OK;
 }
 
+// The same merge in ONE data all-reduce (rmsf_chan_shift_pack/_finish):
+// moments about the contexts' common reference structure (centred reference
+// + its COM), which every rank of RMSF.py holds identically (the frame-0
+// reference, RMSF.py:80-87, or the average, :113-118).  The caller
+// guarantees that every context of the exchange holds the same reference.
+int exchange_chan_shifted(rmsf_ctx **cs, int n, const Reduce &red, bool host_counts) {
+  std::vector<int64_t> local(n);
+  for (int i = 0; i < n; ++i) {
+    if (!cs[i]->ref_set) return fail(RMSF_EINVAL, "rmsf shifted chan merge: a context holds no reference");
+    if (cs[i]->wel.parts0.bytes == 0) {
+      DeviceScope ds(cs[i]->dev);
+      CX_OK(zero_running(cs[i], cs[i]->wel, true));
+    }
+    local[i] = cs[i]->wel.n;
+  }
+  int64_t total = 0;
+  CX_OK(count_exchange(cs, n, red, local, &total, host_counts));
+  if (total == 0) return fail(RMSF_EEMPTY, "rmsf chan merge: no frames on any rank (RMSF.py:39 ZeroDivisionError)");
+  const int64_t nc = cs[0]->n_coord;
+  std::vector<double *> t(n);
+  for (int i = 0; i < n; ++i) {
+    rmsf_ctx *c = cs[i];
+    DeviceScope ds(c->dev);
+    CX_OK(c->xa.ensure(sizeof(double) * 2 * nc, c->stream));
+    CX_OK(rmsf_chan_shift_pack(c->wel.parts0.d(), c->wel.parts1.d(), c->ref.d(), 0, c->refinfo.d(),
+                               (double)local[i], nc, c->xa.d(), c->stream));
+    t[i] = c->xa.d();
+  }
+  CX_OK(red(2 * nc, t.data()));
+  for (int i = 0; i < n; ++i) {
+    rmsf_ctx *c = cs[i];
+    DeviceScope ds(c->dev);
+    CX_OK(rmsf_chan_shift_finish(c->xa.d(), c->ref.d(), 0, c->refinfo.d(), c->n_sel, total, c->wel.parts0.d(),
+                                 c->wel.parts1.d(), nullptr, c->stream));
+    c->wel.n = total;
+  }
+  return RMSF_OK;
+}
+
 Reduce callback_reduce(rmsf_ctx *c, rmsf_allreduce_fn fn, void *user) {
   return [c, fn, user](int64_t count, double *const *bufs) -> int {
     DeviceScope ds(c->dev);
@@ -882,6 +921,12 @@ RMSF_EXPORT int rmsf_ctx_chan_merge(rmsf_ctx *c, rmsf_allreduce_fn fn, void *use
   return exchange_chan(&c, 1, callback_reduce(c, fn, user), false);
 }
 
+RMSF_EXPORT int rmsf_ctx_chan_merge_shifted(rmsf_ctx *c, rmsf_allreduce_fn fn, void *user) {
+  CX_OK(check_ctx(c, "rmsf_ctx_chan_merge_shifted"));
+  if (!fn) return fail(RMSF_EINVAL, "rmsf_ctx_chan_merge_shifted: NULL callback");
+  return exchange_chan_shifted(&c, 1, callback_reduce(c, fn, user), false);
+}
+
 RMSF_EXPORT int rmsf_multi_unique_id(void *id_out) {
   if (!id_out) return fail(RMSF_EINVAL, "rmsf_multi_unique_id: NULL output");
   const Rccl &r = rccl();
@@ -941,6 +986,15 @@ RMSF_EXPORT int rmsf_multi_allreduce_sum(rmsf_ctx **cs, int n) {
 RMSF_EXPORT int rmsf_multi_chan_merge(rmsf_ctx **cs, int n) {
   Reduce red;
   CX_OK(multi_reduce(cs, n, "rmsf_multi_chan_merge", &red));
+  // every rank of the exchange is a context of this process and each holds
+  // a reference (aligned sweeps: the same one, as RMSF.py's ranks hold it):
+  // one data all-reduce instead of two.  Ranks in other processes could
+  // decide differently, so a communicator spanning processes keeps the
+  // two-pass form (rmsf_ctx_chan_merge_shifted is the explicit choice there).
+  const bool here = whole_group_here(cs, n);
+  bool all_ref = here;
+  for (int i = 0; i < n; ++i) all_ref = all_ref && cs[i]->ref_set;
+  if (all_ref) return exchange_chan_shifted(cs, n, red, here);
   return exchange_chan(cs, n, red, whole_group_here(cs, n));
 }
 

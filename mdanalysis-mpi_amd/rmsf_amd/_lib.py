@@ -121,6 +121,7 @@ SIGNATURES = {
     "rmsf_set_partial": (c_int, [P, c_int64, P, P]),
     "rmsf_ctx_allreduce_sum": (c_int, [P, P, P]),
     "rmsf_ctx_chan_merge": (c_int, [P, P, P]),
+    "rmsf_ctx_chan_merge_shifted": (c_int, [P, P, P]),
     "rmsf_multi_unique_id": (c_int, [P]),
     "rmsf_multi_init": (c_int, [P, P, c_int, c_int]),
     "rmsf_multi_init_all": (c_int, [P, c_int]),

@@ -257,14 +257,18 @@ class Context:
         else:
             call("rmsf_ctx_allreduce_sum", self._h, ctypes.cast(fn, ctypes.c_void_p), None)
 
-    def chan_merge(self, fn=None) -> None:
-        """Exact k-way Chan merge over ranks (RMSF.py:140-143)."""
+    def chan_merge(self, fn=None, shifted: bool = False) -> None:
+        """Exact k-way Chan merge over ranks (RMSF.py:140-143).  ``shifted``:
+        one data all-reduce of moments about the reference every rank holds
+        (rmsf_ctx_chan_merge_shifted; all ranks must pass the same choice)
+        instead of two."""
         if fn is None and _dist_world() > 1:
             fn = _DIST_FN
         if fn is None:
             Context.multi_chan_merge([self])
         else:
-            call("rmsf_ctx_chan_merge", self._h, ctypes.cast(fn, ctypes.c_void_p), None)
+            name = "rmsf_ctx_chan_merge_shifted" if shifted else "rmsf_ctx_chan_merge"
+            call(name, self._h, ctypes.cast(fn, ctypes.c_void_p), None)
 
     # -- RCCL / in-process groups ---------------------------------------------
     @staticmethod

@@ -223,7 +223,7 @@ def test_plain_c_host_program(c1, tmp_path):
 
 
 # ---- callback transport across processes (gloo on cuda:0) -------------------
-def _cb_worker(rank, size, port, q):
+def _cb_worker(rank, size, port, q, shifted=False):
     sys.path[:0] = [ROOT, PKG]
     import torch.distributed as dist
 
@@ -243,7 +243,7 @@ def _cb_worker(rank, size, port, q):
             c.allreduce_sum()          # rmsf_ctx_allreduce_sum + torch.distributed callback
             c.set_reference_average()
             c.push(traj[b0:b1], PUSH_ALIGN_WELFORD)
-            c.chan_merge()             # rmsf_ctx_chan_merge + callback
+            c.chan_merge(shifted=shifted)  # rmsf_ctx_chan_merge[_shifted] + callback
             q.put((rank, c.rmsf(), c.partial()[0]))
     except Exception as e:  # noqa: BLE001
         q.put((rank, repr(e), -1))
@@ -251,13 +251,41 @@ def _cb_worker(rank, size, port, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("shifted", [False, True])
 @pytest.mark.parametrize("size", [2, 3])
-def test_context_callback_transport_processes(size):
+def test_context_callback_transport_processes(size, shifted):
     from conftest import spawn_ranks
     from rmsf_amd.synth import motion_table
-    out = spawn_ranks(_cb_worker, size, lambda r, init, q: (r, size, init, q), timeout=100)
+    out = spawn_ranks(_cb_worker, size, lambda r, init, q: (r, size, init, q, shifted), timeout=100)
     traj = SY.frames(2, 700, 0, 41, motion_table(3, 41))
     exp = O.rmsf_script(traj, np.arange(5, 700, 3), None, size=size, align="average")["rmsf"]
     for rank, rmsf, n in out:
         assert n == 41, rmsf
         np.testing.assert_allclose(rmsf, exp, rtol=0, atol=TOL)
+
+
+def test_shifted_merge_needs_a_reference():
+    """rmsf_ctx_chan_merge_shifted refuses a context that holds no reference
+    (its shift); the in-process rmsf_multi_chan_merge then keeps the
+    two-pass form by itself."""
+    import ctypes
+
+    from rmsf_amd import RmsfError
+    from rmsf_amd.context import PUSH_WELFORD, Context
+    from rmsf_amd._lib import call
+    traj = SY.frames(3, 200, 0, 9)
+
+    @ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p)
+    def noop(buf, count, stream, user):  # a one-rank "all-reduce"
+        return 0
+
+    with Context(200) as c:
+        c.push(traj, PUSH_WELFORD)
+        with pytest.raises(RmsfError):
+            call("rmsf_ctx_chan_merge_shifted", c._h, ctypes.cast(noop, ctypes.c_void_p), None)
+    with Context(200) as a, Context(200) as b:
+        a.push(traj[:4], PUSH_WELFORD)
+        b.push(traj[4:], PUSH_WELFORD)
+        Context.multi_chan_merge([a, b])
+        exp = O.rmsf_script(traj, None, None, size=2, align=None)["rmsf"]
+        np.testing.assert_allclose(a.rmsf(), exp, rtol=0, atol=TOL)
