@@ -261,7 +261,12 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     n_total = len(frames)
     if n_total == 0:
         raise RmsfEmptyError(-4, "RMSF.run", "no frames selected")
-    b0, b1 = block if block is not None else parallel.blocks(n_total, size)[rank]
+    std = parallel.blocks(n_total, size)[rank]
+    if block is not None and size > 1 and tuple(block) != std:
+        # the merge's shift frame (and RMSF.py's decomposition) is defined by
+        # the RMSF.py:65-69 blocks: every rank must run its own
+        raise ValueError(f"rank {rank}: block {tuple(block)} is not the RMSF.py:65-69 block {std}")
+    b0, b1 = block if block is not None else std
     n_local = b1 - b0
     n_sel = source.n_sel
     if max_batch is None:
