@@ -145,6 +145,63 @@ def test_api_under_torch_distributed(tmp_path, kind, align, run_kw):
         np.testing.assert_allclose(rmsf, exp, rtol=0, atol=1e-6)
 
 
+def _array_worker(rank, size, init, q, traj, align):
+    sys.path[:0] = [ROOT, PKG]
+    import torch
+    import torch.distributed as dist
+
+    from conftest import init_gloo
+    init_gloo(init, rank, size)
+    try:
+        from rmsf_amd import parallel
+        from rmsf_amd.engine import Engine
+        from rmsf_amd.pipeline import run_pipeline
+        from rmsf_amd.sources import DeviceSource, FrameList
+        eng = Engine(torch.device("cuda", 0))
+        n = traj.shape[0]
+        b0, b1 = parallel.blocks(n, size)[rank]
+        shard = torch.tensor(traj[b0:max(b1, b0 + 1)], device=eng.device)[: b1 - b0]
+        res = run_pipeline(eng, DeviceSource(shard, offset=b0, n_traj=n), FrameList(n), align=align)
+        torch.cuda.synchronize()
+        q.put((rank, res.rmsf.cpu().numpy(), res.mean.cpu().numpy()))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["outlier_frame0", "drift", "frozen"])
+def test_shifted_merge_conditioning(case):
+    """The one-all-reduce merge shifts by frame 0 (no alignment).  Because
+    that shift is one of the data points, M2 >= (x_0 - mean)^2, so
+    T2 <= (n+1) M2 and the subtraction T2 - T1^2/n loses at most log2(n+1)
+    bits -- checked where it is hardest: frame 0 an outlier 500 A away from
+    frames that move by 0.01 A, a trajectory drifting 80 A per frame, and
+    frozen atoms (every frame identical: exactly 0).  3 ranks, against a
+    two-pass f64 variance."""
+    from conftest import spawn_ranks
+    rng = np.random.default_rng(9)
+    n, na = 40, 4096
+    base = rng.uniform(0, 100, (na, 3))
+    if case == "outlier_frame0":
+        traj = base + 0.01 * rng.standard_normal((n, na, 3))
+        traj[0] += 500.0
+    elif case == "drift":
+        traj = base + 80.0 * np.arange(n)[:, None, None] + 0.3 * rng.standard_normal((n, na, 3))
+    else:
+        traj = np.broadcast_to(base, (n, na, 3)).copy()
+    traj = traj.astype(np.float32)
+    out = spawn_ranks(_array_worker, 3, lambda r, init, q: (r, 3, init, q, traj, None))
+    x = traj.astype(np.float64)
+    exp = np.sqrt(((x - x.mean(0)) ** 2).sum(0).sum(1) / n)
+    for rank, rmsf, mean in out:
+        assert mean is not None, rmsf
+        np.testing.assert_allclose(rmsf, exp, rtol=0, atol=1e-9 * max(1.0, float(exp.max())))
+        np.testing.assert_allclose(mean.reshape(-1, 3), x.mean(0), rtol=0, atol=1e-9 * float(np.abs(x).max()))
+        if case == "frozen":
+            assert float(np.abs(rmsf).max()) == 0.0
+
+
 class _FakeUniverse:
     def __init__(self, traj):
         self.trajectory = _FakeTrajectory(traj)
