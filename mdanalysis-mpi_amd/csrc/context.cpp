@@ -146,6 +146,34 @@ struct Running {
   int64_t n = 0;
 };
 
+// Order-independent 64-bit digest of a reference structure: the bit patterns
+// of the centred reference ref[0..n) and of its COM info[0..3) (what the
+// shifted merge uses as its shift, k_chan_shift_pack), each word mixed with
+// its position and summed mod 2^64.  Two contexts whose digests differ hold
+// different references; equal digests mean identical bits up to a 2^-64
+// collision.  rmsf_multi_chan_merge takes the one-all-reduce shifted merge
+// only when every context's digest is equal.
+__host__ __device__ inline uint64_t dig_mix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_ref_digest(const uint64_t *__restrict__ ref, int64_t n,
+                                                    const uint64_t *__restrict__ info,
+                                                    unsigned long long *__restrict__ out) {
+  uint64_t acc = 0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n + 3; j += stride) {
+    const uint64_t w = j < n ? ref[j] : info[j - n];
+    acc += dig_mix(w ^ dig_mix((uint64_t)j));
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) acc += (uint64_t)__shfl_xor((unsigned long long)acc, off, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)acc);
+}
+
 }  // namespace
 
 struct rmsf_ctx {
@@ -155,7 +183,7 @@ struct rmsf_ctx {
   bool has_masses = false;
   std::vector<double> h_masses;
   hipStream_t stream = nullptr;
-  DevBuf sel, masses, ref, refinfo, xform, work, accwork, frame, avg, rmsf, xa, xb, cnt;
+  DevBuf sel, masses, ref, refinfo, xform, work, accwork, frame, avg, rmsf, xa, xb, cnt, refdig;
   bool ref_set = false;
   Running wel, sum;
   rmsf_stager *stager = nullptr;
@@ -251,7 +279,10 @@ int process(rmsf_ctx *c, const float *d_xyz, int64_t stride, int64_t n_frames, c
   }
   if (aligned && welford && c->collect_rmsd) {
     // the rmsd RMSF.py:48 discards: element 12 of each frame's transform record
-    CX_OK(c->rmsd.ensure(sizeof(double) * (size_t)(c->n_rmsd + n_frames), c->stream, true));
+    // grown geometrically: one reallocation (and stream sync) per doubling,
+    // not per batch
+    const size_t need = sizeof(double) * (size_t)(c->n_rmsd + n_frames);
+    CX_OK(c->rmsd.ensure(need > c->rmsd.bytes ? std::max(need, 2 * c->rmsd.bytes) : need, c->stream, true));
     CX_HIP(hipMemcpy2DAsync(c->rmsd.d() + c->n_rmsd, sizeof(double), c->xform.d() + 12,
                             sizeof(double) * RMSF_XFORM_DOUBLES, sizeof(double), (size_t)n_frames,
                             hipMemcpyDeviceToDevice, c->stream));
@@ -271,6 +302,37 @@ int process(rmsf_ctx *c, const float *d_xyz, int64_t stride, int64_t n_frames, c
   CX_OK(rmsf_fold_balanced(c->accwork.p, c->n_coord, mode_k, r.n, r.parts0.d(), welford ? r.parts1.d() : nullptr,
                            c->stream));
   r.n += n_frames;
+  return RMSF_OK;
+}
+
+// queue the digest of the context's current reference (after every setter)
+int digest_reference(rmsf_ctx *c) {
+  CX_OK(c->refdig.ensure(sizeof(unsigned long long), c->stream));
+  CX_HIP(hipMemsetAsync(c->refdig.p, 0, sizeof(unsigned long long), c->stream));
+  const int64_t n = c->n_coord;
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (n + 3 + 1023) / 1024));
+  hipLaunchKernelGGL(k_ref_digest, dim3(blocks), dim3(256), 0, c->stream, static_cast<const uint64_t *>(c->ref.p), n,
+                     static_cast<const uint64_t *>(c->refinfo.p), static_cast<unsigned long long *>(c->refdig.p));
+  CX_HIP(hipGetLastError());
+  return RMSF_OK;
+}
+
+// true when every context holds a reference with the same digest
+int same_references(rmsf_ctx **cs, int n, bool *same) {
+  *same = true;
+  unsigned long long d0 = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!cs[i]->ref_set || !cs[i]->refdig.p) {
+      *same = false;
+      return RMSF_OK;
+    }
+    DeviceScope ds(cs[i]->dev);
+    unsigned long long d = 0;
+    CX_HIP(hipMemcpyAsync(&d, cs[i]->refdig.p, sizeof d, hipMemcpyDeviceToHost, cs[i]->stream));
+    CX_HIP(hipStreamSynchronize(cs[i]->stream));
+    if (i == 0) d0 = d;
+    else if (d != d0) *same = false;
+  }
   return RMSF_OK;
 }
 
@@ -683,7 +745,7 @@ RMSF_EXPORT int rmsf_set_reference(rmsf_ctx *c, const double *h_ref, const doubl
   CX_HIP(hipMemcpyAsync(c->refinfo.p, info, sizeof(info), hipMemcpyHostToDevice, c->stream));
   CX_HIP(hipStreamSynchronize(c->stream));  // the host sources are the caller's / on this stack
   c->ref_set = true;
-  return RMSF_OK;
+  return digest_reference(c);
 }
 
 RMSF_EXPORT int rmsf_set_reference_frame(rmsf_ctx *c, const float *xyz, int is_device_ptr) {
@@ -700,7 +762,7 @@ RMSF_EXPORT int rmsf_set_reference_frame(rmsf_ctx *c, const float *xyz, int is_d
   }
   CX_OK(rmsf_reference_setup(d, nullptr, c->n_sel, c->d_sel(), c->d_masses(), c->ref.d(), c->refinfo.d(), c->stream));
   c->ref_set = true;
-  return RMSF_OK;
+  return digest_reference(c);
 }
 
 RMSF_EXPORT int rmsf_set_reference_average(rmsf_ctx *c) {
@@ -712,7 +774,7 @@ RMSF_EXPORT int rmsf_set_reference_average(rmsf_ctx *c) {
   CX_OK(rmsf_reference_setup(nullptr, c->avg.d(), c->n_sel, nullptr, c->d_masses(), c->ref.d(), c->refinfo.d(),
                              c->stream));
   c->ref_set = true;
-  return RMSF_OK;
+  return digest_reference(c);
 }
 
 RMSF_EXPORT int rmsf_push_frames(rmsf_ctx *c, const float *xyz, int64_t n_frames, int64_t stride, int mode,
@@ -991,9 +1053,14 @@ RMSF_EXPORT int rmsf_multi_chan_merge(rmsf_ctx **cs, int n) {
   // one data all-reduce instead of two.  Ranks in other processes could
   // decide differently, so a communicator spanning processes keeps the
   // two-pass form (rmsf_ctx_chan_merge_shifted is the explicit choice there).
+  // The shifted form is exact only when every context holds the SAME
+  // reference (T1 = sum n_k (mean_k - c) needs one c): contexts aligned to
+  // references of their own keep the two-pass merge (reference digests,
+  // k_ref_digest, compared here).
   const bool here = whole_group_here(cs, n);
   bool all_ref = here;
   for (int i = 0; i < n; ++i) all_ref = all_ref && cs[i]->ref_set;
+  if (all_ref) CX_OK(same_references(cs, n, &all_ref));
   if (all_ref) return exchange_chan_shifted(cs, n, red, here);
   return exchange_chan(cs, n, red, whole_group_here(cs, n));
 }

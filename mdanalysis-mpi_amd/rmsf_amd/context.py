@@ -160,6 +160,11 @@ class Context:
     def set_reference_frame(self, frame) -> None:
         ptr, dev, keep = self._frames_ptr(frame, 1)
         call("rmsf_set_reference_frame", self._h, ptr, dev)
+        if dev:
+            # the setup kernels read the frame asynchronously on the context
+            # stream: a temporary (e.g. a copy from another device) must
+            # outlive them
+            self.synchronize()
         del keep
 
     def set_reference_average(self) -> None:
@@ -174,11 +179,23 @@ class Context:
                 raise ValueError("device frames must be contiguous float32")
             if frames.numel() % (3 * self.n_atoms):
                 raise ValueError(f"device frames: not a whole number of {self.n_atoms}-atom frames")
+            self._after_torch(frames)
             return frames.data_ptr(), 1, frames
         a = np.ascontiguousarray(frames, dtype=np.float32)
         if a.size % (3 * self.n_atoms):
             raise ValueError(f"host frames: not a whole number of {self.n_atoms}-atom frames")
         return a.ctypes.data, 0, a
+
+    def _after_torch(self, t) -> None:
+        """Order the context stream after the work torch has queued on the
+        tensor's device (a copy or kernel that produces ``t``): the context
+        reads device frames on its own non-blocking stream, which nothing else
+        orders behind torch's current stream.  An event wait, no host sync."""
+        import torch
+
+        with torch.cuda.device(self.device):
+            ext = torch.cuda.ExternalStream(self.stream, device=torch.device("cuda", self.device))
+        ext.wait_stream(torch.cuda.current_stream(t.device))
 
     def push(self, frames, mode: int = PUSH_WELFORD, step: int = 1) -> None:
         """Push frames [n, n_atoms, 3] (every ``step``-th one)."""

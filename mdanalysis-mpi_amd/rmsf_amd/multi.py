@@ -378,7 +378,11 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
             for c in ctxs:  # every rank reads the reference frame (RMSF.py:80-87)
                 if hasattr(ref, "is_cuda") and ref.device.index != c.device:
                     import torch
-                    c.set_reference_frame(ref.to(torch.device("cuda", c.device)))  # one frame over xGMI
+                    # one frame over xGMI, copied on torch's stream of c's
+                    # device; set_reference_frame orders the context stream
+                    # after it and keeps the copy alive until the setup ran
+                    with torch.cuda.device(c.device):
+                        c.set_reference_frame(ref.to(torch.device("cuda", c.device)))
                 else:
                     c.set_reference_frame(ref)
         cached = {}

@@ -164,6 +164,9 @@ class Superposer:
 
     def run(self, b: Batch, ref: torch.Tensor, refinfo: torch.Tensor) -> torch.Tensor:
         xf = self.xform[: b.n_frames]
+        need = self.eng.workspace_bytes(self.n_sel, b.n_frames)
+        if need > self.work.numel() * 8:  # stats_plan's bytes are not monotone in the batch size
+            self.work = self.eng.empty((need + 7) // 8)
         with _span(self.timer, "superpose", b.n_frames * self.n_sel):
             self.eng.superpose(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, self.masses, ref, refinfo, xf,
                                self.work)

@@ -77,6 +77,15 @@ def test_single_process_refuses_missing_devices():
     np.testing.assert_equal(bench.device_plan(n, torch.cuda.device_count(), True)[0], [0] * n)
 
 
+def _free_port() -> int:
+    """A TCP port on 127.0.0.1 that was free a moment ago (bind to port 0)."""
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 @pytest.mark.parametrize("align", ["none", "frame0", "average"])
 def test_torchrun_two_ranks_same_result_as_one_gpu(align):
     """The driver's multi-GPU form (torch.distributed.run, one process per
@@ -89,10 +98,13 @@ def test_torchrun_two_ranks_same_result_as_one_gpu(align):
     one = subprocess.run([sys.executable, "bench.py"] + common, cwd=ROOT, capture_output=True, text=True,
                          timeout=300, env=env)
     assert one.returncode == 0, one.stderr[-2000:]
-    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                          "--master-addr", "127.0.0.1", "--master-port", "29533", "bench.py", "--gpus", "2",
-                          "--backend", "gloo"] + common, cwd=ROOT, capture_output=True, text=True, timeout=300,
-                         env=env)
+    for _ in range(3):  # a port the kernel just handed out; retried if taken meanwhile
+        two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                              "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+                              "--gpus", "2", "--backend", "gloo"] + common, cwd=ROOT, capture_output=True, text=True,
+                             timeout=300, env=env)
+        if two.returncode == 0 or "EADDRINUSE" not in two.stderr:
+            break
     assert two.returncode == 0, two.stderr[-2000:]
     l1 = json.loads(one.stdout.strip().splitlines()[-1])
     l2 = json.loads(two.stdout.strip().splitlines()[-1])

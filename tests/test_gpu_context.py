@@ -264,6 +264,36 @@ def test_context_callback_transport_processes(size, shifted):
         np.testing.assert_allclose(rmsf, exp, rtol=0, atol=TOL)
 
 
+def test_multi_merge_contexts_with_different_references():
+    """rmsf_multi_chan_merge over contexts aligned to DIFFERENT references
+    (each to a frame of its own block): the one-all-reduce shifted merge
+    would use one context's shift for all of them, so the reference digests
+    differ and the exact two-pass Chan merge runs (RMSF.py:36-41 over the
+    contexts' own partials); with equal references the shifted form runs and
+    agrees with the same fold."""
+    from rmsf_amd.context import PUSH_ALIGN_WELFORD, Context
+    from rmsf_amd.synth import motion_table
+    traj = SY.frames(6, 400, 0, 30, motion_table(7, 30))
+    sel = np.arange(1, 400, 3)
+    for refs in ([0, 10, 20], [4, 4, 4]):
+        ctxs = [Context(400, sel=sel) for _ in range(3)]
+        parts = []
+        for c, r, (b0, b1) in zip(ctxs, refs, [(0, 10), (10, 20), (20, 30)]):
+            c.set_reference_frame(traj[r])
+            c.push(traj[b0:b1], PUSH_ALIGN_WELFORD)
+            n, mean, m2 = c.partial()
+            parts.append([n, mean, m2])
+        Context.multi_chan_merge(ctxs)
+        T, mu, M = O.chan_fold(parts)
+        exp = np.sqrt(M.sum(axis=1) / T)
+        for c in ctxs:
+            np.testing.assert_allclose(c.rmsf(), exp, rtol=0, atol=1e-9)
+            n, mean, _ = c.partial()
+            assert n == 30
+            np.testing.assert_allclose(mean, mu, rtol=0, atol=1e-9)
+            c.close()
+
+
 def test_shifted_merge_needs_a_reference():
     """rmsf_ctx_chan_merge_shifted refuses a context that holds no reference
     (its shift); the in-process rmsf_multi_chan_merge then keeps the

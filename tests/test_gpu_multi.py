@@ -127,6 +127,22 @@ def test_multi_device_shards(traj, align, run):
         np.testing.assert_allclose(r.rmsd, one.results.rmsd, rtol=0, atol=1e-9)
 
 
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two visible GPUs (the cross-device branch)")
+@pytest.mark.parametrize("align", ["frame0", "average"])
+def test_multi_device_shards_two_devices(traj, align):
+    """Shards on two distinct devices: the reference frame lives on device 0
+    and is copied to device 1 (the cross-device branch of run_multi), each
+    shard produced by torch's stream and read on the context stream."""
+    from rmsf_amd import RMSF
+    sel = np.arange(3, 700, 4)
+    t = torch.tensor(traj, device="cuda:0")
+    parts = [t[:20].contiguous(), t[20:].to("cuda:1")]
+    r = RMSF(parts, select=sel, align=align).run().results
+    exp = O.rmsf_script(traj, sel, None, size=1, align=align)
+    np.testing.assert_allclose(r.rmsf, exp["rmsf"], rtol=0, atol=TOL)
+    assert r.devices == [0, 1] and r.n_frames == len(traj)
+
+
 @pytest.mark.parametrize("align", ["frame0", "average"])
 def test_multi_collect_rmsd_host(traj, align):
     """The per-frame QCP rmsd (RMSF.py:48's discarded by-product) under gpus=,
