@@ -183,6 +183,10 @@ class PipelineResult:
     block: tuple[int, int]
     average: torch.Tensor | None = None   # f64 [n_sel, 3] (align="average")
     rmsd: torch.Tensor | None = None      # f64 [n_local] last-sweep QCP rmsd
+    # f64 [n_local, 16] per-frame transform records (R row-major 0..8, mobile
+    # COM 9..11, rmsd 12) of the last sweep / of RMSF.py's first sweep
+    transforms: torch.Tensor | None = None
+    transforms_sweep1: torch.Tensor | None = None
     extras: dict = field(default_factory=dict)
 
 
@@ -257,7 +261,7 @@ def _frame_shift(eng: Engine, source, frames: FrameList, n_total: int, size: int
 def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=None, ref_frame: int = 0,
                  max_batch: int | None = None, n_splits: int | None = None, collect_rmsd: bool = False,
                  ref_owner: int | None = None, block: tuple[int, int] | None = None,
-                 timer: KernelTimer | None = None) -> PipelineResult:
+                 timer: KernelTimer | None = None, collect_transforms: bool = False) -> PipelineResult:
     if align not in ALIGN_MODES:
         raise ValueError(f"align must be one of {ALIGN_MODES}, got {align!r}")
     rank, size = parallel.world()
@@ -283,9 +287,12 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     aligned = align is not None
     sup = Superposer(eng, n_sel, max_batch, m_dev, timer) if aligned else None
     rmsd = eng.empty(n_local) if (aligned and collect_rmsd) else None
+    keep = aligned and collect_transforms
+    xf_last = eng.empty(n_local, RMSF_XFORM_DOUBLES) if keep else None
+    xf_first = eng.empty(n_local, RMSF_XFORM_DOUBLES) if (keep and align == "average") else None
     average = None
 
-    def sweep(acc: Accumulator, ref=None, info=None):
+    def sweep(acc: Accumulator, ref=None, info=None, xf_out=None):
         done = 0
         for b in source.batches(frames, b0, b1, max_batch, eng.stream):
             xf = None
@@ -293,6 +300,8 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                 xf = sup.run(b, ref, info)
                 if rmsd is not None:
                     rmsd[done:done + b.n_frames].copy_(xf[:, 12])
+                if xf_out is not None:
+                    xf_out[done:done + b.n_frames].copy_(xf)
             acc.add(b, xf, info)
             done += b.n_frames
             b.done()
@@ -301,7 +310,7 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
         ref0, info0 = reference_from_frame(eng, source, ref_frame, n_sel, m_dev, ref_owner)
         acc1 = Accumulator(eng, n_sel, RMSF_MODE_SUM, max_batch, True, n_splits, timer)
         if n_local:
-            sweep(acc1, ref0, info0)
+            sweep(acc1, ref0, info0, xf_first)
         total = parallel.allreduce_sum_(acc1.result0)       # RMSF.py:110
         average = eng.empty(3 * n_sel)
         eng.divide(total, float(n_total), average)          # RMSF.py:111
@@ -326,7 +335,7 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
 
     acc = Accumulator(eng, n_sel, RMSF_MODE_WELFORD, max_batch, aligned, n_splits, timer)
     if n_local:
-        sweep(acc, ref, info)
+        sweep(acc, ref, info, xf_last)
     if size > 1:                                             # RMSF.py:141-143 + 146: one all-reduce
         mean, m2, rmsf = parallel.global_chan_shifted(eng, acc.result0, acc.result1, acc.n, n_total,
                                                       shift, off3, shift_work)
@@ -336,7 +345,8 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
         eng.finalize(m2, n_sel, n_total, rmsf)               # RMSF.py:146
     return PipelineResult(rmsf=rmsf, mean=mean.view(n_sel, 3), m2=m2.view(n_sel, 3), n_frames=n_total,
                           n_local=n_local, block=(b0, b1),
-                          average=None if average is None else average.view(n_sel, 3), rmsd=rmsd)
+                          average=None if average is None else average.view(n_sel, 3), rmsd=rmsd,
+                          transforms=xf_last, transforms_sweep1=xf_first)
 
 
 class CapturedPipeline:

@@ -21,6 +21,12 @@ selection by ``select``).
 ``run(start, stop, step)`` or ``run(frames=...)`` (indices or a boolean mask,
 as ``AnalysisBase.run``; taken in ascending order, so ``results.rmsd`` with
 ``collect_rmsd=True`` follows the sorted frames).
+
+``collect_transforms=True`` (aligned runs, one device per process) adds
+``results.transforms`` -- f64 [n_local, 16] per-frame records of the last
+sweep: the rotation of RMSF.py:48-51 row-major in 0..8, the mobile centre of
+mass of RMSF.py:94 in 9..11, the QCP rmsd in 12 -- and, for
+``align="average"``, ``results.transforms_sweep1`` for RMSF.py's first sweep.
 """
 from __future__ import annotations
 
@@ -75,7 +81,8 @@ class RMSF:
 
     def __init__(self, atomgroup, *, select=None, align=None, masses=None, ref_frame: int = 0,
                  device=None, batch_frames: int | None = None, n_splits: int | None = None,
-                 collect_rmsd: bool = False, verbose: bool = False, gpus=None, **kwargs):
+                 collect_rmsd: bool = False, verbose: bool = False, gpus=None,
+                 collect_transforms: bool = False, **kwargs):
         self._input = atomgroup
         self.select = select
         self.align = align
@@ -85,6 +92,7 @@ class RMSF:
         self.batch_frames = batch_frames
         self.n_splits = n_splits
         self.collect_rmsd = collect_rmsd
+        self.collect_transforms = collect_transforms
         self.verbose = verbose
         self.gpus = gpus
         self.results = Results()
@@ -93,6 +101,8 @@ class RMSF:
     # MDAnalysis AnalysisBase compatible signature
     def run(self, start=None, stop=None, step=None, frames=None, verbose=None, **kwargs):
         if self.gpus is not None or isinstance(self._input, (list, tuple)):
+            if self.collect_transforms:
+                raise NotImplementedError("collect_transforms is for one device per process")
             return self._run_multi(start, stop, step, frames)  # several devices, or HBM shards per device
         eng = Engine(self.device)
         # torch's current device = the engine's, so the buffers sources and
@@ -106,7 +116,8 @@ class RMSF:
                 b0, b1 = parallel.blocks(len(fl), size)[rank]
                 print("Process:%3d --> Frames: %10d -- %10d" % (rank, b0, b1))  # RMSF.py:74
             res = run_pipeline(eng, src, fl, align=self.align, masses=masses, ref_frame=self.ref_frame,
-                               max_batch=self.batch_frames, n_splits=self.n_splits, collect_rmsd=self.collect_rmsd)
+                               max_batch=self.batch_frames, n_splits=self.n_splits, collect_rmsd=self.collect_rmsd,
+                               collect_transforms=self.collect_transforms)
             torch.cuda.current_stream(eng.device).synchronize()
             r = self.results
             r.rmsf = res.rmsf.cpu().numpy()
@@ -120,6 +131,10 @@ class RMSF:
                 r.average = res.average.cpu().numpy()
             if res.rmsd is not None:
                 r.rmsd = res.rmsd.cpu().numpy()
+            if res.transforms is not None:
+                r.transforms = res.transforms.cpu().numpy()
+            if res.transforms_sweep1 is not None:
+                r.transforms_sweep1 = res.transforms_sweep1.cpu().numpy()
         self.n_frames = res.n_frames
         return self
 

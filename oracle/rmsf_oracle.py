@@ -234,8 +234,15 @@ def align_frame_(positions: np.ndarray, masses, ref_coordinates, ref_com) -> np.
     mobile_com = center_of_mass(positions, masses).astype(np.float64)
     mobile_coordinates = positions.astype(np.float64) - mobile_com
     reshaped_matrix = get_rotation_matrix(ref_coordinates, mobile_coordinates, len(positions))
+    return apply_transform_(positions, reshaped_matrix, mobile_com, ref_com)
+
+
+def apply_transform_(positions: np.ndarray, R: np.ndarray, mobile_com, ref_com) -> np.ndarray:
+    """RMSF.py:99-101 (= 133-135) with a given rotation (3x3, row-major) and
+    mobile centre of mass: float32 ``positions`` rewritten in place, rounded
+    to float32 after each of the three steps as ts.positions is."""
     positions[:] -= mobile_com
-    positions[:] = np.dot(positions, reshaped_matrix)
+    positions[:] = np.dot(positions, R)
     positions += ref_com
     return positions
 
@@ -270,10 +277,13 @@ def _frame_list(n_traj, start, stop, step):
 
 
 def rmsf_script(traj, sel=None, masses=None, size: int = 1, ref_frame: int = 0, align: str | None = "average",
-                start=None, stop=None, step=None):
+                start=None, stop=None, step=None, average_f32: bool = False):
     """RMSF.py end to end, emulating ``mpirun -n size`` by running the ranks
     one after another.  align="average" is the script itself; "frame0" skips
     sweep 1 and aligns on frame ``ref_frame``; None is the bare Welford.
+    ``average_f32``: RMSF.py:113's MemoryReader taken to store the average
+    as float32 (the other reading of an unpinned upstream detail; default
+    f64, the build's choice) before the pass-2 reference of :116-118.
 
     Returns dict(rmsf, mean, m2, n, parts, average)."""
     traj = np.asarray(traj)
@@ -292,7 +302,7 @@ def rmsf_script(traj, sel=None, masses=None, size: int = 1, ref_frame: int = 0, 
             total += rank_sweep1(sub, sel, masses, b.start, b.stop, ref_coordinates, ref_com)
         positions = total.reshape(-1) / float(n_frames)
         average = positions.reshape(-1, 3)
-        ref_com, ref_coordinates = centred_reference(average, masses)
+        ref_com, ref_coordinates = centred_reference(average.astype(np.float32) if average_f32 else average, masses)
     parts = [rank_sweep2(sub, sel, masses, b.start, b.stop, ref_coordinates, ref_com) for b in blocks]
     Data = chan_fold(parts)
     RMSF = np.sqrt(Data[2].sum(axis=1) / Data[0])

@@ -36,6 +36,12 @@ Every atom of the frame is transformed (RMSF.py:99-101 acts on all atoms), so
 these vectors also check that restricting the work to the selection (the
 build's SURVEY Q3 disposition) is exact.
 
+RMSF.py:113 wraps the f64 average in a MemoryReader Universe; whether that
+reader keeps f64 or casts to float32 is an upstream detail not pinned here
+(MDAnalysis is absent).  Every end-to-end case is therefore run under both
+readings: the f64 one (keys without suffix) and the float32 one (``_avg32``:
+the average cast to float32 before lines 116-118).
+
 Output: tests/golden/reference_exec.npz (inputs as generator parameters, the
 reference's outputs).  Run from the repo root:
     python tests/golden/make_reference_vectors.py
@@ -125,8 +131,9 @@ def com_upstream(x, m):
     return np.einsum("ij,ij->j", x, m[:, None]) / m.sum()
 
 
-def run_reference(fns, code, traj, sel, masses, size):
-    """RMSF.py for ``mpirun -n size`` on a synthetic trajectory (all atoms)."""
+def run_reference(fns, code, traj, sel, masses, size, avg_f32=False):
+    """RMSF.py for ``mpirun -n size`` on a synthetic trajectory (all atoms).
+    ``avg_f32``: the MemoryReader of RMSF.py:113 taken to store float32."""
     n_frames, n_all = traj.shape[:2]
     ns = dict(np=np, n_frames=n_frames, size=size)
     exec(code["blocks"], ns)
@@ -158,8 +165,9 @@ def run_reference(fns, code, traj, sel, masses, size):
     exec(code["divide"], g)
     average = g["positions"].reshape(-1, 3)
 
-    # pass-2 reference (RMSF.py:113-118): the f64 MemoryReader rows of the CA
-    g["ref_positions"] = average[sel]
+    # pass-2 reference (RMSF.py:113-118): the MemoryReader rows of the CA
+    # (f64, or float32 under the other reading of :113)
+    g["ref_positions"] = average[sel].astype(np.float32) if avg_f32 else average[sel]
     g["ref_com"] = com_upstream(g["ref_positions"], masses).astype(np.float64)
     exec(code["ref2"], g)
     ref_coordinates, ref_com = g["ref_coordinates"], g["ref_com"]
@@ -231,8 +239,29 @@ def main():
                 out[f"mean_{tag}"] = r["mean"]
                 out[f"m2_{tag}"] = r["m2"]
                 out[f"average_{tag}"] = r["average"]
+            r32 = run_reference(fns, code, traj, sel, m, P, avg_f32=True)
+            out[f"rmsf_{tag}_P{P}_avg32"] = r32["rmsf"]
+            if P == 1:
+                out[f"mean_{tag}_avg32"] = r32["mean"]
             print(f"masses={tag} P={P}: n={r['n']} blocks={r['blocks'].tolist()} "
-                  f"rmsf[:3]={r['rmsf'][:3]}")
+                  f"rmsf[:3]={r['rmsf'][:3]} |f64 - f32 reading| max {np.abs(r['rmsf'] - r32['rmsf']).max():.3e}")
+
+    # 100k atoms x 256 frames (all atoms selected, uniform masses), both
+    # readings of RMSF.py:113; 2,048 sampled rows stored (each atom's RMSF
+    # depends on the others only through the per-frame rotations)
+    bseed, bn, bf = 21, 100_000, 256
+    bmotion = motion_table(22, bf)
+    btraj = SY.frames(bseed, bn, 0, bf, bmotion)
+    bsel = np.arange(bn)
+    bm = np.full(bn, 12.011)
+    rows = np.sort(np.random.default_rng(23).choice(bn, 2048, replace=False))
+    b64 = run_reference(fns, code, btraj, bsel, bm, 1)
+    b32 = run_reference(fns, code, btraj, bsel, bm, 1, avg_f32=True)
+    gap = np.abs(b64["rmsf"] - b32["rmsf"])
+    out.update(big_seed=bseed, big_n_atoms=bn, big_n_frames=bf, big_motion=bmotion, big_rows=rows,
+               big_rmsf=b64["rmsf"][rows], big_rmsf_avg32=b32["rmsf"][rows], big_average=b64["average"][rows],
+               big_gap_max=gap.max(), big_gap_mean=gap.mean())
+    print(f"100k x 256: |f64 - f32 reading| max {gap.max():.3e} mean {gap.mean():.3e}")
     np.savez_compressed(OUT, **out)
     print("wrote", OUT)
 

@@ -199,3 +199,39 @@ def test_oracle_edges_golden():
     assert np.all(d["one_frame"] == 0.0)
     assert np.all(d["identical"] == 0.0)
     np.testing.assert_allclose(d["p8_of_3"], d["p1_of_3"], atol=1e-12)
+
+
+def test_rebuild_from_transforms_equals_script():
+    """The full-size GPU tests rebuild sampled atoms from per-frame (R, mobile
+    COM) records: RMSF.py's loop with the records of align_frame_ must give
+    rmsf_script's answer bit for bit, on a subset of rows too (every atom is
+    transformed independently, RMSF.py:99-101)."""
+    rng = np.random.default_rng(5)
+    nf, n = 40, 30
+    base = rng.normal(scale=8.0, size=(n, 3))
+    traj = np.empty((nf, n, 3), dtype=np.float32)
+    for f in range(nf):
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        a, b, c, d = q
+        R = np.array([[a*a+b*b-c*c-d*d, 2*(b*c-a*d), 2*(b*d+a*c)],
+                      [2*(b*c+a*d), a*a-b*b+c*c-d*d, 2*(c*d-a*b)],
+                      [2*(b*d-a*c), 2*(c*d+a*b), a*a-b*b-c*c+d*d]])
+        traj[f] = (base + rng.normal(scale=0.5, size=(n, 3))) @ R + rng.uniform(-5, 5, 3)
+    exp = O.rmsf_script(traj, align="frame0")
+    ref_com, ref_c = O.centred_reference(traj[0])
+    T = np.zeros((nf, 16))
+    for f in range(nf):
+        mob = traj[f]
+        com = O.center_of_mass(mob).astype(np.float64)
+        T[f, :9] = O.get_rotation_matrix(ref_c, mob.astype(np.float64) - com, n).reshape(-1)
+        T[f, 9:12] = com
+    rows = np.array([3, 7, 8, 20, 29])
+    aligned = np.empty((nf, len(rows), 3), dtype=np.float32)
+    for f in range(nf):
+        p = traj[f][rows].copy()
+        O.apply_transform_(p, T[f, :9].reshape(3, 3), T[f, 9:12], ref_com)
+        aligned[f] = p
+    S = O.rank_sweep2(aligned, np.arange(len(rows)), None, 0, nf)
+    np.testing.assert_array_equal(S[1], exp["mean"][rows])
+    np.testing.assert_array_equal(np.sqrt(S[2].sum(axis=1) / S[0]), exp["rmsf"][rows])

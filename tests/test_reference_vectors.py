@@ -65,6 +65,47 @@ def test_oracle_bitwise_vs_reference(ref, traj, tag, P):
         np.testing.assert_array_equal(r["average"], ref[f"average_{tag}"])
 
 
+@pytest.mark.parametrize("tag", ["ca", "het"])
+@pytest.mark.parametrize("P", [1, 2, 3])
+def test_oracle_bitwise_vs_reference_avg32(ref, traj, tag, P):
+    """The other reading of RMSF.py:113 (MemoryReader storing float32): the
+    restatement's ``average_f32`` equals the reference statements run that
+    way, bit for bit."""
+    r = O.rmsf_script(traj, ref["sel"], ref[f"masses_{tag}"], size=P, align="average", average_f32=True)
+    np.testing.assert_array_equal(r["rmsf"], ref[f"rmsf_{tag}_P{P}_avg32"])
+    if P == 1:
+        np.testing.assert_array_equal(r["mean"], ref[f"mean_{tag}_avg32"])
+
+
+def test_memoryreader_readings_gap(ref):
+    """RMSF.py:113's two readings (f64 / float32 MemoryReader) stay inside the
+    north star's 1e-6 A of each other: C1 shape (both mass sets, all P) and
+    100k atoms x 256 frames (max over all atoms, recorded at generation)."""
+    gaps = {}
+    for tag in ("ca", "het"):
+        for P in (1, 2, 3):
+            gaps[tag, P] = np.abs(ref[f"rmsf_{tag}_P{P}"] - ref[f"rmsf_{tag}_P{P}_avg32"]).max()
+    print(f"\nC1 shape |f64 - f32 reading| max: {max(gaps.values()):.3e} A; "
+          f"100k x 256: max {float(ref['big_gap_max']):.3e} mean {float(ref['big_gap_mean']):.3e} A")
+    assert max(gaps.values()) < 0.5 * TOL
+    assert float(ref["big_gap_max"]) < 0.5 * TOL
+    assert np.abs(ref["big_rmsf"] - ref["big_rmsf_avg32"]).max() <= float(ref["big_gap_max"])
+
+
+def test_oracle_100k_rows_vs_reference(ref):
+    """At 100k x 256 the restatement's rows equal the reference statements'
+    (both readings; every atom selected, so the reference's all-atom
+    transform and the restatement's coincide)."""
+    n, nf = int(ref["big_n_atoms"]), int(ref["big_n_frames"])
+    t = SY.frames(int(ref["big_seed"]), n, 0, nf, ref["big_motion"])
+    m = np.full(n, 12.011)
+    rows = ref["big_rows"]
+    r64 = O.rmsf_script(t, None, m, size=1, align="average")
+    np.testing.assert_array_equal(r64["rmsf"][rows], ref["big_rmsf"])
+    r32 = O.rmsf_script(t, None, m, size=1, align="average", average_f32=True)
+    np.testing.assert_array_equal(r32["rmsf"][rows], ref["big_rmsf_avg32"])
+
+
 def test_uniform_default_vs_ca_masses(ref, traj):
     """masses=None (centroid) vs the reference's CA masses: COM rounding moves
     a few f32 rounding points, far inside the tolerance."""
@@ -88,9 +129,34 @@ def test_hip_rmsf_vs_reference(ref, traj, tag, where):
     # summation order) moves one coordinate by ulp/n_frames (3.9e-8 A seen)
     np.testing.assert_allclose(r.results.average, ref[f"average_{tag}"], rtol=0, atol=TOL)
     assert r.results.n_frames == int(ref["n_frames"])
+    # the other reading of RMSF.py:113 (float32 MemoryReader)
+    np.testing.assert_allclose(r.results.rmsf, ref[f"rmsf_{tag}_P1_avg32"], rtol=0, atol=TOL)
     # default (uniform masses) against the reference's CA masses
     r = RMSF(x, select=ref["sel"], align="average").run()
     np.testing.assert_allclose(r.results.rmsf, ref["rmsf_ca_P1"], rtol=0, atol=TOL)
+
+
+@pytest.mark.gpu
+def test_hip_rmsf_100k_vs_both_readings(ref):
+    """100k atoms x 256 frames, RMSF.py's two sweeps on the device: the
+    sampled rows within 1e-6 A of the reference statements under both
+    readings of RMSF.py:113."""
+    import torch
+
+    from rmsf_amd import RMSF
+    from rmsf_amd.engine import Engine
+    from rmsf_amd.synth import generate
+    n, nf = int(ref["big_n_atoms"]), int(ref["big_n_frames"])
+    t = generate(Engine(), n, 0, nf, seed=int(ref["big_seed"]), motion=ref["big_motion"])
+    r = RMSF(t, align="average", masses=np.full(n, 12.011)).run().results
+    rows = ref["big_rows"]
+    d64 = np.abs(r.rmsf[rows] - ref["big_rmsf"]).max()
+    d32 = np.abs(r.rmsf[rows] - ref["big_rmsf_avg32"]).max()
+    print(f"\n100k x 256: build vs f64 reading {d64:.3e} A, vs f32 reading {d32:.3e} A")
+    assert d64 < TOL and d32 < TOL
+    np.testing.assert_allclose(r.average[rows], ref["big_average"], rtol=0, atol=TOL)
+    del t
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.gpu
