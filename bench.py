@@ -172,6 +172,42 @@ def roofline(kernel: str, launches: int, ms: float, atom_frames: float, traffic=
                           "sum(HIP-event launch time)"}
 
 
+def rank_roofline(kernel: str, rows, traffic=None, traffic_source=None) -> dict:
+    """``roofline`` for every rank's timed launches: ``rows`` = one
+    (launches, ms, atom_frames) triple per rank (rank order).  achieved =
+    sum(bytes) / sum(launch time) over all ranks; ``per_device_gbs`` each
+    rank's own rate, ``slowest_rank_gbs`` / ``slowest_rank`` the minimum."""
+    rows = [tuple(float(v) for v in r) for r in rows]
+    rf = roofline(kernel, int(sum(r[0] for r in rows)), sum(r[1] for r in rows), sum(r[2] for r in rows),
+                  traffic, traffic_source)
+    per = [B_PER_ATOM_FRAME * r[2] / (r[1] / 1e3) / 1e9 if r[1] > 0 else None for r in rows]
+    live = [(g, i) for i, g in enumerate(per) if g is not None]
+    rf["ranks"] = len(rows)
+    rf["per_device_gbs"] = per
+    rf["per_device_launches"] = [int(r[0]) for r in rows]
+    rf["slowest_rank_gbs"], rf["slowest_rank"] = min(live) if live else (None, None)
+    rf["slowest_rank_frac"] = rf["slowest_rank_gbs"] / HBM_PEAK_GBS if live else None
+    if len(rows) > 1:
+        rf["bytes_rule"] += "; summed over every rank's launches (all-reduced before rank 0 prints)"
+    return rf
+
+
+def gather_rank_rows(vals, device=None) -> list:
+    """Every rank's ``vals`` (a short list of numbers), in rank order, on
+    every rank: each rank fills its row of a zero [world, k] f64 tensor and
+    one SUM all-reduce assembles them (works over RCCL and gloo)."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [list(vals)]
+    w, r = dist.get_world_size(), dist.get_rank()
+    t = torch.zeros(w, len(vals), dtype=torch.float64, device=device)
+    t[r] = torch.tensor([float(v) for v in vals], dtype=torch.float64)
+    dist.all_reduce(t)
+    return t.cpu().tolist()
+
+
 def c1_latency(eng, no_cpu: bool) -> dict:
     """Config C1 shape (BASELINE configs[0]): 3341 atoms, 214 selected, 98
     frames, RMSF.py's two-sweep average alignment -- latency of one full
@@ -344,8 +380,7 @@ def main_single_process(a, wl, cpu) -> None:
     out["devices"] = devs
     out["rehearsal"] = rehearsal
     kname = ("k_accum_split_sk" if align else "k_welford_flat_sk")
-    out["roofline"] = roofline(kname, sum(x[0] for x in acc), sum(x[1] for x in acc), sum(x[2] for x in acc))
-    out["roofline"]["per_device_gbs"] = [B_PER_ATOM_FRAME * x[2] / (x[1] / 1e3) / 1e9 if x[1] else None for x in acc]
+    out["roofline"] = rank_roofline(kname, acc)
     if align:
         ms, af = sum(x[1] for x in sup), sum(x[2] for x in sup)
         out["superpose"] = {"launches": sum(x[0] for x in sup), "avg_launch_ms": ms / max(1, sum(x[0] for x in sup)),
@@ -487,19 +522,24 @@ def main():
     traffic = load_traffic(a.workload, n_atoms, n_local) if launches == a.steps else None
     kname = (("k_accum_atoms" if wl["align"] else "k_welford_flat") if a.splits
              else ("k_accum_split_sk" if wl["align"] else "k_welford_flat_sk"))
-    out["roofline"] = roofline(kname, launches, acc_ms, acc_af, traffic,
-                               f"profiles/pmc_{a.workload}.json" if traffic else None)
+    # every rank's launches (one all-reduce, after the timed region)
+    coll_dev = eng.device if a.backend == "nccl" else None
+    rows = gather_rank_rows([launches, acc_ms, acc_af], coll_dev)
+    out["roofline"] = rank_roofline(kname, rows, traffic, f"profiles/pmc_{a.workload}.json" if traffic else None)
     out["cpu_baseline"] = cpu
     out["rmsf_checksum"] = float(res.rmsf.sum())  # the merged result, identical on every rank
     # whole-step rate in algorithmic bytes (incl. merges, finalise, launch gaps)
     out["pipeline_hbm_gbs"] = B_PER_ATOM_FRAME * n_atoms * n_local * a.steps / dt / 1e9
     if wl["align"]:
-        k, s_ms, s_af = timer.totals("superpose")
+        srows = gather_rank_rows(list(timer.totals("superpose")), coll_dev)
+        k, s_ms, s_af = (sum(r[i] for r in srows) for i in range(3))
         if k:
-            out["superpose"] = {"launches": k, "avg_launch_ms": s_ms / k,
+            out["superpose"] = {"launches": int(k), "avg_launch_ms": s_ms / k,
                                 "gflops": FLOP_PER_ATOM_FRAME_SUPERPOSE * s_af / (s_ms / 1e3) / 1e9,
                                 "fp64_peak_tflops_spec": FP64_PEAK_TFS,
-                                "hbm_gbs": B_PER_ATOM_FRAME * s_af / (s_ms / 1e3) / 1e9}
+                                "hbm_gbs": B_PER_ATOM_FRAME * s_af / (s_ms / 1e3) / 1e9,
+                                "per_device_hbm_gbs": [B_PER_ATOM_FRAME * r[2] / (r[1] / 1e3) / 1e9 if r[1] else None
+                                                       for r in srows]}
 
     if wl.get("host"):
         # bytes that actually cross PCIe per step: the staged selection rows of

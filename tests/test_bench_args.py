@@ -45,3 +45,38 @@ def test_roofline_sums_bytes_over_launch_time():
     assert r["achieved"] == pytest.approx(12 * 3.0e8 / 3.0e-3 / 1e9)
     assert r["frac"] == pytest.approx(r["achieved"] / 8000.0)
     assert r["algorithmic_bytes_per_launch"] == pytest.approx(12 * 1.0e8)
+
+
+def test_rank_roofline_describes_every_rank():
+    # rank 1 is slower: the line keeps sum(bytes)/sum(time) and names it
+    rows = [(2, 1.0, 2.0e8), (2, 1.25, 2.0e8), (2, 1.0, 2.0e8)]
+    r = bench.rank_roofline("k_welford_flat_sk", rows)
+    assert r["ranks"] == 3 and r["launches"] == 6
+    assert r["achieved"] == pytest.approx(12 * 6.0e8 / 3.25e-3 / 1e9)
+    assert r["per_device_gbs"] == pytest.approx([2400.0, 1920.0, 2400.0])
+    assert r["per_device_launches"] == [2, 2, 2]
+    assert r["slowest_rank"] == 1 and r["slowest_rank_gbs"] == pytest.approx(1920.0)
+    assert r["slowest_rank_frac"] == pytest.approx(1920.0 / 8000.0)
+    one = bench.rank_roofline("k", [(3, 3.0, 3.0e8)])
+    assert one["ranks"] == 1 and one["slowest_rank"] == 0 and one["achieved"] == pytest.approx(1200.0)
+
+
+def _gather_worker(rank, size, init, q):
+    from conftest import init_gloo
+    import torch.distributed as dist
+
+    init_gloo(init, rank, size)
+    rows = bench.gather_rank_rows([rank + 1, 0.5 * (rank + 1), 1.0e6 * (rank + 1)])
+    r = bench.rank_roofline("k", rows)
+    q.put((rank, rows, r["slowest_rank"], r["launches"]))
+    dist.destroy_process_group()
+
+
+def test_gather_rank_rows_gloo_two_ranks():
+    """The N>1 bench line is built from every rank's KernelTimer totals,
+    all-reduced in rank order before rank 0 prints (gloo, world size 2)."""
+    from conftest import spawn_ranks
+    out = sorted(spawn_ranks(_gather_worker, 2, lambda r, init, q: (r, 2, init, q)))
+    for rank, rows, slow, launches in out:
+        assert rows == [[1.0, 0.5, 1.0e6], [2.0, 1.0, 2.0e6]]
+        assert launches == 3 and slow in (0, 1)

@@ -109,6 +109,15 @@ def test_torchrun_two_ranks_same_result_as_one_gpu(align):
     l1 = json.loads(one.stdout.strip().splitlines()[-1])
     l2 = json.loads(two.stdout.strip().splitlines()[-1])
     assert l2["n_gpus"] == 2 and l2["config"]["n_frames_per_gpu"] == 150
+    # the roofline describes both ranks (KernelTimer totals all-reduced)
+    rf = l2["roofline"]
+    sweeps = 2 if align == "average" else 1
+    assert rf["ranks"] == 2 and rf["launches"] == 2 * 2 * sweeps and rf["per_device_launches"] == [2 * sweeps] * 2
+    assert len(rf["per_device_gbs"]) == 2 and all(0 < g < 8000 for g in rf["per_device_gbs"])
+    assert rf["slowest_rank"] in (0, 1) and rf["slowest_rank_gbs"] == min(rf["per_device_gbs"])
+    assert min(rf["per_device_gbs"]) <= rf["achieved"] <= max(rf["per_device_gbs"])
+    if align != "none":
+        assert len(l2["superpose"]["per_device_hbm_gbs"]) == 2
     assert l1["rmsf_checksum"] == pytest.approx(l2["rmsf_checksum"], rel=1e-12)
     from rmsf_amd.synth import motion_table
 
