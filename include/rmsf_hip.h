@@ -194,6 +194,15 @@ int rmsf_chan_shift_finish(const double *d_t, const void *d_shift,
                            int64_t n_sel, int64_t n_frames, double *d_mean,
                            double *d_m2, double *d_rmsf, void *stream);
 
+/* rmsf_fold_balanced (WELFORD) and rmsf_chan_shift_pack in ONE launch, for a
+ * rank's last batch before the cross-rank merge: the fold as above, then
+ * d_t as the pack writes it, with n_k = acc_n + the batch's frames --
+ * bit-identical to the two calls (RMSF.py:36-41 + 140-143).                */
+int rmsf_fold_balanced_shift(const void *d_work, int64_t n_coord,
+                             int64_t acc_n, double *d_acc0, double *d_acc1,
+                             const void *d_shift, int shift_is_f32,
+                             const double *d_off3, double *d_t, void *stream);
+
 /* ---- finalise: RMSF.py:146  rmsf = sqrt(M2.sum(axis=1) / n) ---------------*/
 int rmsf_finalize(const double *d_m2, int64_t n_sel, int64_t n_frames,
                   double *d_rmsf, void *stream);

@@ -559,11 +559,27 @@ __global__ __launch_bounds__(kBlock *Q) void k_accum_split_sk(const float *__res
 // few ranges costs one memory round trip, not one per segment.  The walk is
 // uniform per wave (a chunk is 256 lanes), its divisions stay off the
 // critical path of the loads.
+//
+// PACK (N > 1, WELFORD only): the fold also writes the moments about the
+// merge's shift c that the one-all-reduce merge sums (k_chan_shift_pack's
+// T1/T2, same arithmetic: shift_moments), so the pack needs no launch of its
+// own.  PACK = 1: float32 shift, 2: float64 shift; c = shift[j] (+ off3[j % 3]).
 constexpr int kFoldBatch = 4;
+
+// T1 = n (mean - c), T2 = M2 + n (mean - c)^2, the rounding fixed by explicit
+// operations (the standalone pack and the fused fold must agree bit for bit)
+__device__ __forceinline__ void shift_moments(double mu, double M2, double c, double nk, double *t1, double *t2) {
+  const double d = mu - c;
+  *t1 = nk * d;
+  *t2 = __builtin_fma(nk, d * d, M2);
+}
+
+template <int PACK>
 __global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ hdr,
                                                     const double *__restrict__ parts0, int64_t n_coord,
                                                     double acc_n, double *__restrict__ acc0,
-                                                    double *__restrict__ acc1) {
+                                                    double *__restrict__ acc1, const void *__restrict__ shift,
+                                                    const double *__restrict__ off3, double *__restrict__ t) {
   const int64_t l = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   SkPlan pl;
   pl.lanes = hdr[0];
@@ -586,6 +602,19 @@ __global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ 
   const int64_t clo = c * pl.nf, chi = clo + pl.nf;
   const double *__restrict__ parts1 = parts0 + (int64_t)pl.G * pl.P * slot_d;
   const bool wel = pl.mode == RMSF_MODE_WELFORD;
+  // the merge's shift, loaded before the walk so its latency hides behind it
+  double cs[4] = {0.0, 0.0, 0.0, 0.0};
+  if (PACK) {
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      if (x < nx) {
+        const int64_t j = j0 + x;
+        double c = PACK == 1 ? (double)static_cast<const float *>(shift)[j] : static_cast<const double *>(shift)[j];
+        if (off3) c += off3[j % 3];
+        cs[x] = c;
+      }
+    }
+  }
   double n1 = acc_n, mu[4] = {0.0, 0.0, 0.0, 0.0}, M[4] = {0.0, 0.0, 0.0, 0.0};
   if (acc_n > 0) {
 #pragma unroll
@@ -669,6 +698,12 @@ __global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ 
       acc0[j0 + x] = mu[x];
       if (wel) acc1[j0 + x] = M[x];
     }
+  }
+  if (PACK) {
+    const double nk = acc_n + (double)pl.nf;  // frames folded in: this rank's n_k
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+      if (x < nx) shift_moments(mu[x], M[x], cs[x], nk, t + j0 + x, t + n_coord + j0 + x);
   }
 }
 
@@ -1169,9 +1204,7 @@ __global__ __launch_bounds__(kBlock) void k_chan_shift_pack(const double *__rest
   if (j >= n) return;
   double c = (double)shift[j];
   if (off3) c += off3[j % 3];
-  const double d = mk[j] - c;
-  t[j] = nk * d;
-  t[n + j] = qk[j] + nk * (d * d);
+  shift_moments(mk[j], qk[j], c, nk, t + j, t + n + j);
 }
 
 template <typename ShiftT>
@@ -1723,8 +1756,24 @@ RMSF_EXPORT int rmsf_fold_balanced(const void *d_work, int64_t n_coord, int mode
   // the plan (and where parts1 starts) is read from the header the
   // accumulate kernel wrote
   // one thread per lane of >= 3 coordinates (the plan's cpl is on the device)
-  hipLaunchKernelGGL(k_fold_sk, dim3(grid1((n_coord + 2) / 3)), dim3(kBlock), 0, S(stream), hdr, p0, n_coord, (double)acc_n,
-                     d_acc0, d_acc1);
+  hipLaunchKernelGGL(k_fold_sk<0>, dim3(grid1((n_coord + 2) / 3)), dim3(kBlock), 0, S(stream), hdr, p0, n_coord,
+                     (double)acc_n, d_acc0, d_acc1, nullptr, nullptr, nullptr);
+  return after_launch("k_fold_sk");
+}
+
+RMSF_EXPORT int rmsf_fold_balanced_shift(const void *d_work, int64_t n_coord, int64_t acc_n, double *d_acc0,
+                                         double *d_acc1, const void *d_shift, int shift_is_f32, const double *d_off3,
+                                         double *d_t, void *stream) {
+  if (!d_work || !d_acc0 || !d_acc1 || !d_shift || !d_t || n_coord < 1 || acc_n < 0)
+    return fail(RMSF_EINVAL, "rmsf_fold_balanced_shift: bad arguments");
+  const int64_t *hdr = static_cast<const int64_t *>(d_work);
+  const double *p0 = reinterpret_cast<const double *>(hdr + kSkHdr);
+  if (shift_is_f32)
+    hipLaunchKernelGGL(k_fold_sk<1>, dim3(grid1((n_coord + 2) / 3)), dim3(kBlock), 0, S(stream), hdr, p0, n_coord,
+                       (double)acc_n, d_acc0, d_acc1, d_shift, d_off3, d_t);
+  else
+    hipLaunchKernelGGL(k_fold_sk<2>, dim3(grid1((n_coord + 2) / 3)), dim3(kBlock), 0, S(stream), hdr, p0, n_coord,
+                       (double)acc_n, d_acc0, d_acc1, d_shift, d_off3, d_t);
   return after_launch("k_fold_sk");
 }
 

@@ -69,6 +69,7 @@ SIGNATURES = {
     "rmsf_chan_deviation": (c_int, [P, P, P, c_double, c_int64, P, P]),
     "rmsf_finalize": (c_int, [P, c_int64, c_int64, P, P]),
     "rmsf_chan_shift_pack": (c_int, [P, P, P, c_int, P, c_double, c_int64, P, P]),
+    "rmsf_fold_balanced_shift": (c_int, [P, c_int64, c_int64, P, P, P, c_int, P, P, P]),
     "rmsf_chan_shift_finish": (c_int, [P, P, c_int, P, c_int64, c_int64, P, P, P, P]),
     "rmsf_qcp_batch": (c_int, [P, P, P, c_int64, P, P, P]),
     "rmsf_calc_rmsd_rotational_matrix": (c_int, [P, P, c_int64, P, P, POINTER(c_double)]),

@@ -108,6 +108,15 @@ class Engine:
         (Chan's merge, RMSF.py:36-41, or a sum)."""
         call("rmsf_fold_balanced", work.data_ptr(), n_coord, mode, acc_n, acc0.data_ptr(), _ptr(acc1), self.stream)
 
+    def fold_balanced_shift(self, work: torch.Tensor, n_coord: int, acc_n: int, acc0: torch.Tensor,
+                            acc1: torch.Tensor, shift: torch.Tensor, off3, out: torch.Tensor) -> None:
+        """fold_balanced (WELFORD) + chan_shift_pack in one launch: ``out`` =
+        the moments about c = shift + off3 that the cross-rank merge sums."""
+        if out.numel() < 2 * n_coord or shift.numel() < n_coord:
+            raise ValueError("fold_balanced_shift: buffer sizes")
+        call("rmsf_fold_balanced_shift", work.data_ptr(), n_coord, acc_n, acc0.data_ptr(), acc1.data_ptr(),
+             shift.data_ptr(), int(shift.dtype == torch.float32), _ptr(off3), out.data_ptr(), self.stream)
+
     def chan_merge(self, mean_parts: torch.Tensor, m2_parts: torch.Tensor, counts, n_coord: int,
                    mean_out: torch.Tensor, m2_out: torch.Tensor) -> None:
         """second_order_moments (RMSF.py:36-41) folded over the partials in order."""

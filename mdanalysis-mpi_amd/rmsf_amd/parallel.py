@@ -85,7 +85,7 @@ def broadcast_async(t: torch.Tensor, src: int):
 
 
 def global_chan_shifted(ops, mean_k: torch.Tensor, m2_k: torch.Tensor, n_k: int, n_total: int, shift: torch.Tensor,
-                        off3: torch.Tensor | None = None, shift_work=None):
+                        off3: torch.Tensor | None = None, shift_work=None, packed: torch.Tensor | None = None):
     """The k-way Chan merge in ONE all-reduce: moments about a shift c that
     every rank already holds (c = shift + off3 per xyz: the sweep's reference
     structure, the sweep-1 average, or frame 0 broadcast during the sweep).
@@ -95,15 +95,19 @@ def global_chan_shifted(ops, mean_k: torch.Tensor, m2_k: torch.Tensor, n_k: int,
     arithmetic; c within the fluctuation of the data keeps it free of
     cancellation).  Returns (mean, M2, rmsf) -- the finalise of RMSF.py:146 is
     fused into the unpacking.  ``shift_work``: the pending broadcast that
-    fills ``shift``, waited for here (it ran beside the sweep)."""
+    fills ``shift``, waited for here (it ran beside the sweep).  ``packed``:
+    T1/T2 already written by the last fold (rmsf_fold_balanced_shift)."""
     _, size = world()
     if n_total <= 0:
         raise ZeroDivisionError("global_chan_shifted: no frames on any rank")
     n = mean_k.numel()
-    t = torch.empty(2 * n, dtype=mean_k.dtype, device=mean_k.device)
-    if shift_work is not None:
-        shift_work.wait()
-    ops.chan_shift_pack(mean_k, m2_k, shift, off3, float(n_k), t)
+    if packed is not None:
+        t = packed
+    else:
+        t = torch.empty(2 * n, dtype=mean_k.dtype, device=mean_k.device)
+        if shift_work is not None:
+            shift_work.wait()
+        ops.chan_shift_pack(mean_k, m2_k, shift, off3, float(n_k), t)
     if size > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     mean, m2 = torch.empty_like(mean_k), torch.empty_like(m2_k)

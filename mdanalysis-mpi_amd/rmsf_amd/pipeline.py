@@ -104,6 +104,7 @@ class Accumulator:
         if mode == RMSF_MODE_WELFORD:
             self.parts1 = eng.empty(1 + self.s_max, self.n_coord)
         self.n = 0
+        self.packed = False
         self._zeroed = False
         if n_splits:
             self._zero()
@@ -115,7 +116,12 @@ class Accumulator:
                 self.parts1[0].zero_()
             self._zeroed = True
 
-    def add(self, b: Batch, xform: torch.Tensor | None = None, refinfo: torch.Tensor | None = None) -> None:
+    def add(self, b: Batch, xform: torch.Tensor | None = None, refinfo: torch.Tensor | None = None,
+            pack=None) -> None:
+        """``pack`` = (shift, off3, t, pending broadcast or None): this is the
+        rank's last batch before the cross-rank merge; on the balanced grid
+        in WELFORD mode the fold also writes the merge's moments about the
+        shift into ``t`` (one launch; ``self.packed`` tells the caller)."""
         eng = self.eng
         p1 = None if self.parts1 is None else self.parts1[0]
         if not self.fixed_splits:
@@ -125,7 +131,14 @@ class Accumulator:
             with _span(self.timer, "accumulate", b.n_frames * self.n_sel):
                 eng.accumulate_balanced(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, xform, refinfo, self.mode,
                                         self.work)
-            eng.fold_balanced(self.work, self.n_coord, self.mode, self.n, self.parts0[0], p1)
+            if pack is not None and self.mode == RMSF_MODE_WELFORD:
+                shift, off3, t, work = pack
+                if work is not None:
+                    work.wait()  # the shift's broadcast ran beside the sweep
+                eng.fold_balanced_shift(self.work, self.n_coord, self.n, self.parts0[0], p1, shift, off3, t)
+                self.packed = True
+            else:
+                eng.fold_balanced(self.work, self.n_coord, self.mode, self.n, self.parts0[0], p1)
             self.n += b.n_frames
             return
         s = max(self.fixed_splits, -(-b.n_frames // RMSF_MAX_SPLIT_FRAMES))
@@ -292,7 +305,7 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     xf_first = eng.empty(n_local, RMSF_XFORM_DOUBLES) if (keep and align == "average") else None
     average = None
 
-    def sweep(acc: Accumulator, ref=None, info=None, xf_out=None):
+    def sweep(acc: Accumulator, ref=None, info=None, xf_out=None, pack=None):
         done = 0
         for b in source.batches(frames, b0, b1, max_batch, eng.stream):
             xf = None
@@ -302,7 +315,7 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                     rmsd[done:done + b.n_frames].copy_(xf[:, 12])
                 if xf_out is not None:
                     xf_out[done:done + b.n_frames].copy_(xf)
-            acc.add(b, xf, info)
+            acc.add(b, xf, info, pack if done + b.n_frames == n_local else None)
             done += b.n_frames
             b.done()
 
@@ -334,11 +347,14 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
             shift, shift_work = _frame_shift(eng, source, frames, n_total, size, rank)
 
     acc = Accumulator(eng, n_sel, RMSF_MODE_WELFORD, max_batch, aligned, n_splits, timer)
+    # N > 1: the last batch's fold also packs the merge's moments (one launch)
+    t = torch.empty(6 * n_sel, dtype=torch.float64, device=eng.device) if size > 1 else None
     if n_local:
-        sweep(acc, ref, info, xf_last)
+        sweep(acc, ref, info, xf_last, (shift, off3, t, shift_work) if size > 1 else None)
     if size > 1:                                             # RMSF.py:141-143 + 146: one all-reduce
         mean, m2, rmsf = parallel.global_chan_shifted(eng, acc.result0, acc.result1, acc.n, n_total,
-                                                      shift, off3, shift_work)
+                                                      shift, off3, None if acc.packed else shift_work,
+                                                      packed=t if acc.packed else None)
     else:
         mean, m2 = acc.result0, acc.result1
         rmsf = eng.empty(n_sel)

@@ -338,6 +338,51 @@ def test_chan_shift_merge_kernels(eng, shift_kind):
     np.testing.assert_array_equal(mean.cpu().numpy(), f0.astype(np.float64))
 
 
+@pytest.mark.parametrize("shift_kind", ["f64", "f64+off3", "f32"])
+@pytest.mark.parametrize("n_sel,nf,groups", [(4096, 1000, 0), (1001, 333, 7), (3, 5, 2), (100_000, 64, 0),
+                                            (300_000, 33, 0)])
+def test_fold_balanced_shift_bitwise(eng, shift_kind, n_sel, nf, groups):
+    """rmsf_fold_balanced_shift (the N > 1 pipeline's last fold) equals
+    rmsf_fold_balanced + rmsf_chan_shift_pack bit for bit: the running result
+    and the merge's T1/T2, over two batches (acc_n > 0 on the second)."""
+    from rmsf_amd.synth import generate
+    from rmsf_amd._lib import RMSF_MODE_WELFORD
+    traj = generate(eng, n_sel, 0, nf, seed=27)
+    nc = 3 * n_sel
+    f0 = traj[0].reshape(-1)
+    if shift_kind == "f32":
+        shift, off3 = f0.clone(), None
+    elif shift_kind == "f64":
+        shift, off3 = f0.double(), None
+    else:
+        com = f0.double().reshape(-1, 3).mean(0)
+        shift, off3 = (f0.double().reshape(-1, 3) - com).reshape(-1), com.contiguous()
+    outs = []
+    for fused in (False, True):
+        mean, m2 = eng.empty(nc), eng.empty(nc)
+        t = torch.full((2 * nc,), float("nan"), dtype=torch.float64, device=eng.device)
+        acc, cut = 0, nf // 3
+        for f0_, f1_ in ((0, cut), (cut, nf)):
+            if f1_ <= f0_:
+                continue
+            n = f1_ - f0_
+            work = eng.empty(eng.balanced_workspace_bytes(n_sel, n, groups) // 8 + 2)
+            ptr = traj.data_ptr() + f0_ * 3 * n_sel * 4
+            eng.accumulate_balanced(ptr, 3 * n_sel, n, n_sel, None, None, None, RMSF_MODE_WELFORD, work, groups)
+            if fused and f1_ == nf:
+                eng.fold_balanced_shift(work, nc, acc, mean, m2, shift, off3, t)
+            else:
+                eng.fold_balanced(work, nc, RMSF_MODE_WELFORD, acc, mean, m2)
+            acc += n
+        if not fused:
+            eng.chan_shift_pack(mean, m2, shift, off3, float(acc), t)
+        _sync()
+        outs.append([x.cpu().numpy() for x in (mean, m2, t)])
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+    assert np.isfinite(outs[1][2]).all()
+
+
 def test_second_order_moments_api(eng):
     from rmsf_amd import second_order_moments
     rng = np.random.default_rng(1)
