@@ -105,6 +105,9 @@ def parse(argv=None):
     ap.add_argument("--host-cache", action="store_true",
                     help="c5: keep the staged frames in HBM within a step (RMSF.py's second sweep reads them there)")
     ap.add_argument("--align", choices=["none", "frame0", "average"], default=None, help="override the workload's")
+    ap.add_argument("--merge-slabs", type=int, default=None,
+                    help="N>1, no alignment: atom slabs of the final sweep whose all-reduces overlap the next slab "
+                         "(default: 4 from 1M atoms, else none; 0 = off)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo only "
                                                      "to rehearse several ranks on one GPU)")
     return ap.parse_args(argv)
@@ -493,7 +496,7 @@ def main():
         if hasattr(src, "drop_cache"):
             src.drop_cache()  # every step streams the file again
         return run_pipeline(eng, src, fl, align=align, block=(b0, b1), ref_owner=0, n_splits=a.splits,
-                            max_batch=a.batch_frames, timer=timer)
+                            max_batch=a.batch_frames, timer=timer, merge_slabs=a.merge_slabs)
 
     def timed(align, steps, warmup):
         timer = KernelTimer()
@@ -518,6 +521,8 @@ def main():
     par = (f"frame-sharded x{world} (RMSF.py:65-69 blocks), one process per GPU, {transport} Chan merge"
            if world > 1 else "1 GPU")
     out = base_line(a, wl, world, dt, par)
+    if world > 1:
+        out["config"]["merge_slabs"] = res.extras.get("merge_slabs", 0)
     launches, acc_ms, acc_af = timer.totals("accumulate")
     traffic = load_traffic(a.workload, n_atoms, n_local) if launches == a.steps else None
     kname = (("k_accum_atoms" if wl["align"] else "k_welford_flat") if a.splits

@@ -203,6 +203,34 @@ int rmsf_fold_balanced_shift(const void *d_work, int64_t n_coord,
                              const void *d_shift, int shift_is_f32,
                              const double *d_off3, double *d_t, void *stream);
 
+/* Atom slabs of the flat WELFORD plan (no selection, no transform, 16-B
+ * aligned float4 columns), so a rank's cross-rank merge can start on the
+ * first slab while the next one streams (large n_sel; RMSF.py:140-143).
+ * rmsf_balanced_slab_chunks: *h_chunks = the plan's chunk count C (256
+ * lanes of 4 coordinates = 1024 coordinates each) when the plan is
+ * chunk-aligned, else 0 (no slabs).  rmsf_accumulate_balanced_slab runs
+ * the whole plan's ranges of chunks [c0, c1) -- the same segments, so the
+ * slab's partials equal the whole launch's -- into the same d_work;
+ * rmsf_fold_balanced_shift_slab folds those chunks into d_acc* (global
+ * coordinates) and writes the slab's [T1 | T2] (2 (j1 - j0) doubles,
+ * j0 = 1024 c0, j1 = min(1024 c1, n_coord)) to d_t.  Bit-identical to the
+ * whole-selection calls for every coordinate.  Slab bounds that are a
+ * multiple of 3 chunks keep whole atoms together (rmsf_chan_shift_finish
+ * per slab).                                                               */
+int rmsf_balanced_slab_chunks(const float *d_xyz, int64_t frame_stride,
+                              int64_t n_frames, int64_t n_sel,
+                              int64_t *h_chunks);
+int rmsf_accumulate_balanced_slab(const float *d_xyz, int64_t frame_stride,
+                                  int64_t n_frames, int64_t n_sel, int64_t c0,
+                                  int64_t c1, void *d_work, size_t work_bytes,
+                                  void *stream);
+int rmsf_fold_balanced_shift_slab(const void *d_work, int64_t n_coord,
+                                  int64_t acc_n, double *d_acc0,
+                                  double *d_acc1, const void *d_shift,
+                                  int shift_is_f32, const double *d_off3,
+                                  double *d_t, int64_t c0, int64_t c1,
+                                  void *stream);
+
 /* ---- finalise: RMSF.py:146  rmsf = sqrt(M2.sum(axis=1) / n) ---------------*/
 int rmsf_finalize(const double *d_m2, int64_t n_sel, int64_t n_frames,
                   double *d_rmsf, void *stream);

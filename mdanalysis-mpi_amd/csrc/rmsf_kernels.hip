@@ -336,13 +336,16 @@ struct SkPlan {
   int G, P, cpl, mode;
   int S;   // > 0: chunk-aligned ranges, S per chunk, dispatched split-major
   int cw;  // lanes per chunk (kBlock; 16 for the tiled float4 stream)
+  // launch subset (chunk-aligned plans): chunks [c0, c0 + Cs) -- an atom slab
+  // whose ranges and segments are exactly the whole plan's (not in the header)
+  int64_t c0, Cs;
 };
 
 // range processed by hardware workgroup `hw`: with chunk-aligned ranges the
 // dispatch is split-major (consecutive workgroups = consecutive chunks of
 // the same frames, as the split grid's), otherwise the identity
 __device__ __forceinline__ int sk_range(const SkPlan &p, int hw) {
-  return p.S > 0 ? (int)((int64_t)(hw % p.C) * p.S + hw / p.C) : hw;
+  return p.S > 0 ? (int)((p.c0 + (int64_t)hw % p.Cs) * p.S + hw / p.Cs) : hw;
 }
 
 __host__ __device__ inline int64_t sk_lo(const SkPlan &p, int64_t b) { return p.T * b / p.G; }
@@ -579,8 +582,11 @@ __global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ 
                                                     const double *__restrict__ parts0, int64_t n_coord,
                                                     double acc_n, double *__restrict__ acc0,
                                                     double *__restrict__ acc1, const void *__restrict__ shift,
-                                                    const double *__restrict__ off3, double *__restrict__ t) {
-  const int64_t l = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+                                                    const double *__restrict__ off3, double *__restrict__ t,
+                                                    int64_t l_off, int64_t l_end, int64_t t_n) {
+  // lanes [l_off, l_end) (an atom slab; 0, INT64_MAX = all).  T1/T2 of the
+  // slab's coordinates go to t[j - j_lo] and t[t_n + j - j_lo].
+  const int64_t l = l_off + (int64_t)blockIdx.x * kBlock + threadIdx.x;
   SkPlan pl;
   pl.lanes = hdr[0];
   pl.C = hdr[1];
@@ -592,7 +598,7 @@ __global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ 
   pl.mode = (int)hdr[7];
   pl.S = (int)hdr[8];
   pl.cw = (int)hdr[9];
-  if (l >= pl.lanes) return;
+  if (l >= pl.lanes || l >= l_end) return;
   const int cpl = pl.cpl;
   const int64_t j0 = l * cpl;  // first coordinate of the lane
   const int nx = (int)(n_coord - j0 < cpl ? n_coord - j0 : cpl);
@@ -701,9 +707,10 @@ __global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ 
   }
   if (PACK) {
     const double nk = acc_n + (double)pl.nf;  // frames folded in: this rank's n_k
+    double *t1 = t + (j0 - l_off * cpl), *t2 = t1 + t_n;
 #pragma unroll
     for (int x = 0; x < 4; ++x)
-      if (x < nx) shift_moments(mu[x], M[x], cs[x], nk, t + j0 + x, t + n_coord + j0 + x);
+      if (x < nx) shift_moments(mu[x], M[x], cs[x], nk, t1 + x, t2 + x);
   }
 }
 
@@ -1634,6 +1641,7 @@ SkPlan sk_plan(int64_t lanes, int cpl, int64_t nf, int n_groups, int mode, int p
   p.T = p.C * nf;
   p.cpl = cpl;
   p.mode = mode;
+  p.c0 = 0;
   int64_t G = n_groups > 0 ? n_groups : (int64_t)per_cu * cu_count();
   int64_t S = 0;  // > 0: chunk-aligned ranges, S per chunk
   if (n_groups <= 0 && p.C > G) {
@@ -1658,6 +1666,7 @@ SkPlan sk_plan(int64_t lanes, int cpl, int64_t nf, int n_groups, int mode, int p
     p.S = (int)S;
     if (nf % S == 0) p.P = (int)((nf / S + kCoefN - 1) / kCoefN);  // exact: one chunk per range
   }
+  p.Cs = p.C;
   return p;
 }
 
@@ -1670,6 +1679,18 @@ bool flat_layout(const float *d_xyz, int64_t fstride, int64_t n_sel, const int32
                  int mode) {
   return !d_xform && !d_sel && mode == RMSF_MODE_WELFORD && (3 * n_sel) % 4 == 0 && fstride % 4 == 0 &&
          reinterpret_cast<uintptr_t>(d_xyz) % 16 == 0;
+}
+
+int fold_shift_launch(const int64_t *hdr, const double *p0, int64_t n_coord, int64_t acc_n, double *acc0, double *acc1,
+                      const void *shift, int shift_is_f32, const double *off3, double *t, int64_t l0, int64_t l1,
+                      int64_t t_n, int64_t threads, hipStream_t s) {
+  if (shift_is_f32)
+    hipLaunchKernelGGL(k_fold_sk<1>, dim3(grid1(threads)), dim3(kBlock), 0, s, hdr, p0, n_coord, (double)acc_n, acc0,
+                       acc1, shift, off3, t, l0, l1, t_n);
+  else
+    hipLaunchKernelGGL(k_fold_sk<2>, dim3(grid1(threads)), dim3(kBlock), 0, s, hdr, p0, n_coord, (double)acc_n, acc0,
+                       acc1, shift, off3, t, l0, l1, t_n);
+  return after_launch("k_fold_sk");
 }
 
 }  // namespace
@@ -1757,7 +1778,7 @@ RMSF_EXPORT int rmsf_fold_balanced(const void *d_work, int64_t n_coord, int mode
   // accumulate kernel wrote
   // one thread per lane of >= 3 coordinates (the plan's cpl is on the device)
   hipLaunchKernelGGL(k_fold_sk<0>, dim3(grid1((n_coord + 2) / 3)), dim3(kBlock), 0, S(stream), hdr, p0, n_coord,
-                     (double)acc_n, d_acc0, d_acc1, nullptr, nullptr, nullptr);
+                     (double)acc_n, d_acc0, d_acc1, nullptr, nullptr, nullptr, (int64_t)0, INT64_MAX, n_coord);
   return after_launch("k_fold_sk");
 }
 
@@ -1768,13 +1789,56 @@ RMSF_EXPORT int rmsf_fold_balanced_shift(const void *d_work, int64_t n_coord, in
     return fail(RMSF_EINVAL, "rmsf_fold_balanced_shift: bad arguments");
   const int64_t *hdr = static_cast<const int64_t *>(d_work);
   const double *p0 = reinterpret_cast<const double *>(hdr + kSkHdr);
-  if (shift_is_f32)
-    hipLaunchKernelGGL(k_fold_sk<1>, dim3(grid1((n_coord + 2) / 3)), dim3(kBlock), 0, S(stream), hdr, p0, n_coord,
-                       (double)acc_n, d_acc0, d_acc1, d_shift, d_off3, d_t);
-  else
-    hipLaunchKernelGGL(k_fold_sk<2>, dim3(grid1((n_coord + 2) / 3)), dim3(kBlock), 0, S(stream), hdr, p0, n_coord,
-                       (double)acc_n, d_acc0, d_acc1, d_shift, d_off3, d_t);
-  return after_launch("k_fold_sk");
+  return fold_shift_launch(hdr, p0, n_coord, acc_n, d_acc0, d_acc1, d_shift, shift_is_f32, d_off3, d_t, 0, INT64_MAX,
+                           n_coord, (n_coord + 2) / 3, S(stream));
+}
+
+// ---- atom slabs of the flat balanced plan (C4's merge overlap) ------------
+RMSF_EXPORT int rmsf_balanced_slab_chunks(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
+                                          int64_t *h_chunks) {
+  if (!h_chunks || n_sel < 1 || n_frames < 1) return fail(RMSF_EINVAL, "rmsf_balanced_slab_chunks: bad arguments");
+  *h_chunks = 0;
+  if (!flat_layout(d_xyz, fstride, n_sel, nullptr, nullptr, RMSF_MODE_WELFORD)) return RMSF_OK;
+  const SkPlan pl = sk_plan(3 * n_sel / 4, 4, n_frames, 0, RMSF_MODE_WELFORD, kSkPerCuFlat);
+  if (pl.S > 0) *h_chunks = pl.C;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_accumulate_balanced_slab(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
+                                              int64_t c0, int64_t c1, void *d_work, size_t work_bytes,
+                                              void *stream) {
+  if (!d_xyz || !d_work || n_sel < 1 || n_frames < 1 || reinterpret_cast<uintptr_t>(d_work) % 16 != 0)
+    return fail(RMSF_EINVAL, "rmsf_accumulate_balanced_slab: bad arguments");
+  if (!flat_layout(d_xyz, fstride, n_sel, nullptr, nullptr, RMSF_MODE_WELFORD))
+    return fail(RMSF_EINVAL, "rmsf_accumulate_balanced_slab: needs the flat float4 layout (no selection, aligned)");
+  SkPlan pl = sk_plan(3 * n_sel / 4, 4, n_frames, 0, RMSF_MODE_WELFORD, kSkPerCuFlat);
+  if (pl.S <= 0) return fail(RMSF_EINVAL, "rmsf_accumulate_balanced_slab: the plan is not chunk-aligned");
+  if (c0 < 0 || c1 <= c0 || c1 > pl.C) return fail(RMSF_EINVAL, "rmsf_accumulate_balanced_slab: bad chunk range");
+  if (work_bytes < sk_bytes(pl, true)) return fail(RMSF_ENOMEM, "rmsf_accumulate_balanced_slab: workspace too small");
+  pl.c0 = c0;
+  pl.Cs = c1 - c0;
+  int64_t *hdr = static_cast<int64_t *>(d_work);
+  double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
+  double *p1 = p0 + (size_t)pl.G * pl.P * kBlock * 4;
+  hipLaunchKernelGGL((k_welford_flat_sk<4>), dim3((unsigned)(pl.Cs * pl.S)), dim3(kBlock), 0, S(stream), d_xyz,
+                     fstride / 4, pl, hdr, p0, p1);
+  return after_launch("k_welford_flat_sk");
+}
+
+RMSF_EXPORT int rmsf_fold_balanced_shift_slab(const void *d_work, int64_t n_coord, int64_t acc_n, double *d_acc0,
+                                              double *d_acc1, const void *d_shift, int shift_is_f32,
+                                              const double *d_off3, double *d_t, int64_t c0, int64_t c1,
+                                              void *stream) {
+  if (!d_work || !d_acc0 || !d_acc1 || !d_shift || !d_t || n_coord < 4 || acc_n < 0 || c0 < 0 || c1 <= c0)
+    return fail(RMSF_EINVAL, "rmsf_fold_balanced_shift_slab: bad arguments");
+  // flat plan: 256-lane chunks of 4 coordinates
+  const int64_t l0 = c0 * kBlock, l1 = c1 * kBlock;
+  const int64_t j0 = 4 * l0, j1 = std::min(4 * l1, n_coord);
+  if (j0 >= n_coord) return fail(RMSF_EINVAL, "rmsf_fold_balanced_shift_slab: bad chunk range");
+  const int64_t *hdr = static_cast<const int64_t *>(d_work);
+  const double *p0 = reinterpret_cast<const double *>(hdr + kSkHdr);
+  return fold_shift_launch(hdr, p0, n_coord, acc_n, d_acc0, d_acc1, d_shift, shift_is_f32, d_off3, d_t, l0, l1,
+                           j1 - j0, l1 - l0, S(stream));
 }
 
 RMSF_EXPORT int rmsf_chan_merge(const double *d_mean_parts, const double *d_m2_parts, const int64_t *h_counts,

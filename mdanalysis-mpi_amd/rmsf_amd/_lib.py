@@ -70,6 +70,9 @@ SIGNATURES = {
     "rmsf_finalize": (c_int, [P, c_int64, c_int64, P, P]),
     "rmsf_chan_shift_pack": (c_int, [P, P, P, c_int, P, c_double, c_int64, P, P]),
     "rmsf_fold_balanced_shift": (c_int, [P, c_int64, c_int64, P, P, P, c_int, P, P, P]),
+    "rmsf_balanced_slab_chunks": (c_int, [P, c_int64, c_int64, c_int64, P]),
+    "rmsf_accumulate_balanced_slab": (c_int, [P, c_int64, c_int64, c_int64, c_int64, c_int64, P, c_size_t, P]),
+    "rmsf_fold_balanced_shift_slab": (c_int, [P, c_int64, c_int64, P, P, P, c_int, P, P, c_int64, c_int64, P]),
     "rmsf_chan_shift_finish": (c_int, [P, P, c_int, P, c_int64, c_int64, P, P, P, P]),
     "rmsf_qcp_batch": (c_int, [P, P, P, c_int64, P, P, P]),
     "rmsf_calc_rmsd_rotational_matrix": (c_int, [P, P, c_int64, P, P, POINTER(c_double)]),

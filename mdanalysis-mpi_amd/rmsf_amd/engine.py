@@ -117,6 +117,30 @@ class Engine:
         call("rmsf_fold_balanced_shift", work.data_ptr(), n_coord, acc_n, acc0.data_ptr(), acc1.data_ptr(),
              shift.data_ptr(), int(shift.dtype == torch.float32), _ptr(off3), out.data_ptr(), self.stream)
 
+    def balanced_slab_chunks(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int) -> int:
+        """Chunks (1024 coordinates each) of the flat balanced plan when it is
+        chunk-aligned (atom slabs possible), else 0."""
+        c = ctypes.c_int64(0)
+        call("rmsf_balanced_slab_chunks", xyz_ptr, fstride, n_frames, n_sel, ctypes.cast(ctypes.pointer(c),
+                                                                                        ctypes.c_void_p))
+        return int(c.value)
+
+    def accumulate_balanced_slab(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, c0: int, c1: int,
+                                 work: torch.Tensor) -> None:
+        """The whole flat plan's ranges of chunks [c0, c1) (WELFORD)."""
+        call("rmsf_accumulate_balanced_slab", xyz_ptr, fstride, n_frames, n_sel, c0, c1, work.data_ptr(),
+             work.numel() * work.element_size(), self.stream)
+
+    def fold_balanced_shift_slab(self, work: torch.Tensor, n_coord: int, acc_n: int, acc0: torch.Tensor,
+                                 acc1: torch.Tensor, shift: torch.Tensor, off3, out: torch.Tensor, c0: int,
+                                 c1: int) -> None:
+        """Fold chunks [c0, c1) and write their [T1 | T2] to ``out``."""
+        j0, j1 = 1024 * c0, min(1024 * c1, n_coord)
+        if out.numel() < 2 * (j1 - j0) or shift.numel() < n_coord:
+            raise ValueError("fold_balanced_shift_slab: buffer sizes")
+        call("rmsf_fold_balanced_shift_slab", work.data_ptr(), n_coord, acc_n, acc0.data_ptr(), acc1.data_ptr(),
+             shift.data_ptr(), int(shift.dtype == torch.float32), _ptr(off3), out.data_ptr(), c0, c1, self.stream)
+
     def chan_merge(self, mean_parts: torch.Tensor, m2_parts: torch.Tensor, counts, n_coord: int,
                    mean_out: torch.Tensor, m2_out: torch.Tensor) -> None:
         """second_order_moments (RMSF.py:36-41) folded over the partials in order."""

@@ -75,6 +75,15 @@ def global_chan(ops, mean_k: torch.Tensor, m2_k: torch.Tensor, n_k: int, n_total
     return mean, m2
 
 
+def allreduce_sum_async(t: torch.Tensor):
+    """Start an in-place SUM across ranks; returns the work (wait() orders
+    the then-current stream after it), or None for a single process."""
+    _, size = world()
+    if size > 1:
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
+    return None
+
+
 def broadcast_async(t: torch.Tensor, src: int):
     """Start an in-place broadcast from ``src``; returns the work (wait() orders
     the then-current stream after it), or None for a single process."""

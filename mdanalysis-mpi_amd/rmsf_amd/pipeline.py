@@ -271,10 +271,51 @@ def _frame_shift(eng: Engine, source, frames: FrameList, n_total: int, size: int
     return buf, work
 
 
+SLAB_MIN_ATOMS = 1_000_000  # auto merge slabs from here: ~16 us per extra slab launch < 1 % of the step
+SLABS_AUTO = 4
+
+
+def _slab_bounds(n_chunks: int, k: int) -> list[tuple[int, int]]:
+    """k atom slabs of the flat plan's chunks, cut at multiples of 3 chunks
+    (3 x 1024 coordinates = whole atoms)."""
+    cuts = sorted({min(n_chunks, max(0, 3 * round(i * n_chunks / k / 3))) for i in range(1, k)} - {0, n_chunks})
+    b = [0] + cuts + [n_chunks]
+    return list(zip(b[:-1], b[1:]))
+
+
+def _slab_sweep(eng: Engine, acc: "Accumulator", b: Batch, slabs: list, shift, off3, shift_work, timer):
+    """The final Welford sweep of one resident batch in atom slabs (N > 1):
+    slab k's accumulate + fold (which packs its [T1 | T2]) and the start of
+    its all-reduce, then slab k+1 streams while that all-reduce runs.
+    Every coordinate's partials, segments and fold are the whole launch's
+    (rmsf_accumulate_balanced_slab), so the result is bit-identical to the
+    unslabbed merge wherever the collective's summation order is (any 2
+    ranks).  Returns [(t_k, j0, j1, work_k)]."""
+    n_coord = acc.n_coord
+    out = []
+    for c0, c1 in slabs:
+        j0, j1 = 1024 * c0, min(1024 * c1, n_coord)
+        with _span(timer, "accumulate", b.n_frames * (j1 - j0) // 3):
+            eng.accumulate_balanced_slab(b.ptr, b.fstride, b.n_frames, acc.n_sel, c0, c1, acc.work)
+        if shift_work is not None:
+            shift_work.wait()  # the shift's broadcast ran beside the first slab
+            shift_work = None
+        t = torch.empty(2 * (j1 - j0), dtype=torch.float64, device=eng.device)
+        eng.fold_balanced_shift_slab(acc.work, n_coord, acc.n, acc.parts0[0], acc.parts1[0], shift, off3, t, c0, c1)
+        out.append((t, j0, j1, parallel.allreduce_sum_async(t)))
+    acc.n += b.n_frames
+    return out
+
+
 def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=None, ref_frame: int = 0,
                  max_batch: int | None = None, n_splits: int | None = None, collect_rmsd: bool = False,
                  ref_owner: int | None = None, block: tuple[int, int] | None = None,
-                 timer: KernelTimer | None = None, collect_transforms: bool = False) -> PipelineResult:
+                 timer: KernelTimer | None = None, collect_transforms: bool = False,
+                 merge_slabs: int | None = None) -> PipelineResult:
+    """``merge_slabs`` (N > 1, no alignment, HBM-resident block in one batch,
+    flat chunk-aligned plan): cut the final sweep into that many atom slabs
+    so each slab's cross-rank all-reduce overlaps the next slab's stream;
+    None = SLABS_AUTO from SLAB_MIN_ATOMS selected atoms, 0/1 = off."""
     if align not in ALIGN_MODES:
         raise ValueError(f"align must be one of {ALIGN_MODES}, got {align!r}")
     rank, size = parallel.world()
@@ -305,8 +346,8 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     xf_first = eng.empty(n_local, RMSF_XFORM_DOUBLES) if (keep and align == "average") else None
     average = None
 
-    def sweep(acc: Accumulator, ref=None, info=None, xf_out=None, pack=None):
-        done = 0
+    def sweep(acc: Accumulator, ref=None, info=None, xf_out=None, pack=None, slabs=None):
+        done, slabbed = 0, None
         for b in source.batches(frames, b0, b1, max_batch, eng.stream):
             xf = None
             if aligned:
@@ -315,9 +356,17 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                     rmsd[done:done + b.n_frames].copy_(xf[:, 12])
                 if xf_out is not None:
                     xf_out[done:done + b.n_frames].copy_(xf)
-            acc.add(b, xf, info, pack if done + b.n_frames == n_local else None)
+            last = done + b.n_frames == n_local
+            if slabs and done == 0 and last and b.sel is None and xf is None:
+                n_chunks = eng.balanced_slab_chunks(b.ptr, b.fstride, b.n_frames, n_sel)
+                if n_chunks >= 2 * 3:
+                    shift_, off3_, _, work_ = pack
+                    slabbed = _slab_sweep(eng, acc, b, _slab_bounds(n_chunks, slabs), shift_, off3_, work_, timer)
+            if slabbed is None:
+                acc.add(b, xf, info, pack if last else None)
             done += b.n_frames
             b.done()
+        return slabbed
 
     if align == "average":
         ref0, info0 = reference_from_frame(eng, source, ref_frame, n_sel, m_dev, ref_owner)
@@ -347,10 +396,24 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
             shift, shift_work = _frame_shift(eng, source, frames, n_total, size, rank)
 
     acc = Accumulator(eng, n_sel, RMSF_MODE_WELFORD, max_batch, aligned, n_splits, timer)
-    # N > 1: the last batch's fold also packs the merge's moments (one launch)
+    # N > 1: the last batch's fold also packs the merge's moments (one launch);
+    # large selections in one resident batch run as overlapped atom slabs
     t = torch.empty(6 * n_sel, dtype=torch.float64, device=eng.device) if size > 1 else None
+    k_slabs = merge_slabs if merge_slabs is not None else (SLABS_AUTO if n_sel >= SLAB_MIN_ATOMS else 0)
+    slabs = k_slabs if (size > 1 and k_slabs > 1 and not aligned and not n_splits) else None
+    slabbed = None
     if n_local:
-        sweep(acc, ref, info, xf_last, (shift, off3, t, shift_work) if size > 1 else None)
+        slabbed = sweep(acc, ref, info, xf_last, (shift, off3, t, shift_work) if size > 1 else None, slabs)
+    if slabbed is not None:                                  # RMSF.py:141-143 + 146, slab by slab
+        mean, m2, rmsf = eng.empty(3 * n_sel), eng.empty(3 * n_sel), eng.empty(n_sel)
+        for t_k, j0, j1, work in slabbed:
+            if work is not None:
+                work.wait()
+            eng.chan_shift_finish(t_k, shift[j0:j1], off3, (j1 - j0) // 3, n_total, mean[j0:j1], m2[j0:j1],
+                                  rmsf[j0 // 3:j1 // 3])
+        return PipelineResult(rmsf=rmsf, mean=mean.view(n_sel, 3), m2=m2.view(n_sel, 3), n_frames=n_total,
+                              n_local=n_local, block=(b0, b1), average=None, rmsd=rmsd,
+                              extras={"merge_slabs": len(slabbed)})
     if size > 1:                                             # RMSF.py:141-143 + 146: one all-reduce
         mean, m2, rmsf = parallel.global_chan_shifted(eng, acc.result0, acc.result1, acc.n, n_total,
                                                       shift, off3, None if acc.packed else shift_work,

@@ -255,3 +255,65 @@ def test_stager_slot_reuse(slots):
     torch.cuda.synchronize()
     ref = RMSF(torch.tensor(traj, device="cuda"), select=sel, align="frame0").run().results.rmsf
     np.testing.assert_allclose(res.rmsf.cpu().numpy(), ref, rtol=0, atol=1e-9)
+
+
+def _slab_worker(rank, size, init, q, n_atoms, n_frames):
+    sys.path[:0] = [ROOT, PKG]
+    import torch
+    import torch.distributed as dist
+
+    from conftest import init_gloo
+    init_gloo(init, rank, size)
+    try:
+        from rmsf_amd import parallel
+        from rmsf_amd.engine import Engine
+        from rmsf_amd.pipeline import run_pipeline
+        from rmsf_amd.sources import DeviceSource, FrameList
+        from rmsf_amd.synth import generate
+        eng = Engine(torch.device("cuda", 0))
+        b0, b1 = parallel.blocks(n_frames, size)[rank]
+        shard = generate(eng, n_atoms, b0, b1 - b0, seed=12)
+        src = DeviceSource(shard, offset=b0, n_traj=n_frames)
+        outs = {}
+        for k in (0, 4, 3):
+            res = run_pipeline(eng, src, FrameList(n_frames), merge_slabs=k)
+            torch.cuda.synchronize()
+            outs[k] = (res.rmsf.cpu().numpy(), res.mean.cpu().numpy(), res.m2.cpu().numpy(),
+                       res.extras.get("merge_slabs", 0))
+        q.put((rank, outs))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("size", [2, 3])
+def test_merge_slabs_bitwise(size):
+    """C4's merge in atom slabs (each slab's all-reduce started while the
+    next slab streams): every slab replays the whole plan's ranges and
+    segments for its chunks, so the per-rank T1/T2 are the unslabbed ones bit
+    for bit.  2 ranks: the summed result too (a + b = b + a); 3 ranks: the
+    collective's summation order may follow the message size -- measured
+    here, and within 1e-15 relative of the unslabbed merge either way.  300k
+    atoms: the flat plan is chunk-aligned (more chunks than workgroups), as
+    at C4's 1M."""
+    from conftest import spawn_ranks
+    from oracle import synth as SY
+    n_atoms, n_frames = 300_000, 64 * size + 1
+    out = spawn_ranks(_slab_worker, size, lambda r, init, q: (r, size, init, q, n_atoms, n_frames), timeout=200)
+    for rank, outs in sorted(out, key=lambda o: o[0]):
+        assert isinstance(outs, dict), outs
+        assert outs[0][3] == 0 and outs[4][3] == 4 and outs[3][3] == 3
+        for k in (4, 3):
+            for a, b in zip(outs[0][:3], outs[k][:3]):
+                if size == 2:
+                    np.testing.assert_array_equal(a, b)
+                else:
+                    np.testing.assert_allclose(a, b, rtol=1e-15, atol=0)
+            same = all(np.array_equal(a, b) for a, b in zip(outs[0][:3], outs[k][:3]))
+            print(f"\nsize {size} rank {rank} slabs {k}: bit-identical to unslabbed: {same}")
+    # sampled atoms against a two-pass variance of the regenerated frames
+    atoms = np.sort(np.random.default_rng(1).choice(n_atoms, 64, replace=False))
+    host = SY.frames(12, n_atoms, 0, n_frames, atoms=atoms).astype(np.float64)
+    exp = np.sqrt(((host - host.mean(0)) ** 2).sum(0).sum(1) / n_frames)
+    np.testing.assert_allclose(out[0][1][4][0][atoms], exp, rtol=0, atol=1e-9)
