@@ -107,7 +107,7 @@ def parse(argv=None):
     ap.add_argument("--align", choices=["none", "frame0", "average"], default=None, help="override the workload's")
     ap.add_argument("--merge-slabs", type=int, default=None,
                     help="N>1, no alignment: atom slabs of the final sweep whose all-reduces overlap the next slab "
-                         "(default: 4 from 1M atoms, else none; 0 = off)")
+                         "(default: 2 from 1M atoms, else none; 0 = off)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo only "
                                                      "to rehearse several ranks on one GPU)")
     return ap.parse_args(argv)

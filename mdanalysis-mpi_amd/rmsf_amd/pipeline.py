@@ -271,8 +271,12 @@ def _frame_shift(eng: Engine, source, frames: FrameList, n_total: int, size: int
     return buf, work
 
 
-SLAB_MIN_ATOMS = 1_000_000  # auto merge slabs from here: ~16 us per extra slab launch < 1 % of the step
-SLABS_AUTO = 4
+# Auto merge slabs from 1M selected atoms, 2 of them: at C4's share (1M x
+# 2,500 frames) the cut costs 45 us of device time (+1.0 %; 4 slabs +85 us,
+# profiles/r03_workloads/merge_slabs_c4_share.txt) and lets half of the 48 MB
+# all-reduce run beside the second slab's stream
+SLAB_MIN_ATOMS = 1_000_000
+SLABS_AUTO = 2
 
 
 def _slab_bounds(n_chunks: int, k: int) -> list[tuple[int, int]]:
