@@ -125,3 +125,28 @@ def test_torchrun_two_ranks_same_result_as_one_gpu(align):
     traj = SY.frames(0, 6000, 0, 301, mt)
     exp = O.rmsf_script(traj, None, None, size=2, align=None if align == "none" else align)["rmsf"]
     assert abs(l2["rmsf_checksum"] - float(exp.sum())) < 1e-6 * len(exp)
+
+
+def test_torchrun_merge_slabs_same_checksum():
+    """The driver's N>1 form with the final sweep in atom slabs (C4's
+    merge overlap, forced at 300k atoms where the flat plan is chunk-aligned):
+    2 gloo ranks on the GPU, slabbed and unslabbed give the same RMSF bit for
+    bit (two ranks: the sum of two partials is order-free), and the line
+    records the slab count."""
+    common = ["--n-atoms", "300000", "--frames", "130", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+              "--no-modes", "--gpus", "2", "--backend", "gloo"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    lines = {}
+    for k in ("2", "0"):
+        for _ in range(3):
+            r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+                                "--merge-slabs", k] + common, cwd=ROOT, capture_output=True, text=True, timeout=300,
+                               env=env)
+            if r.returncode == 0 or "EADDRINUSE" not in r.stderr:
+                break
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines[k] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert lines["2"]["config"]["merge_slabs"] == 2 and lines["0"]["config"]["merge_slabs"] == 0
+    assert lines["2"]["rmsf_checksum"] == lines["0"]["rmsf_checksum"]
+    assert lines["2"]["roofline"]["launches"] == 2 * 2 * 2  # 2 ranks x 2 steps x 2 slabs
