@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""Randomised parity sweep of the N > 1 pipeline (not product code, not a
+test): P = 2..4 gloo ranks sharing the GPU, random atoms / selection /
+frames / alignment / batch size, and merge slabs forced on where the flat
+plan allows them -- each rank's RMSF against the oracle's mpirun -n P
+emulation of RMSF.py.  python tools/fuzz_multirank.py [n_cases]"""
+import os
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "mdanalysis-mpi_amd")
+sys.path[:0] = [ROOT, PKG]
+
+import numpy as np  # noqa: E402
+
+
+def _worker(rank, size, init, q, case):
+    sys.path[:0] = [ROOT, PKG]
+    from datetime import timedelta
+
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=size, timeout=timedelta(seconds=120))
+    try:
+        from rmsf_amd import parallel
+        from rmsf_amd.engine import Engine
+        from rmsf_amd.pipeline import run_pipeline
+        from rmsf_amd.sources import DeviceSource, FrameList
+        from rmsf_amd.synth import generate, motion_table
+        eng = Engine(torch.device("cuda", 0))
+        na, nf, align, sel, batch, slabs = (case[k] for k in ("na", "nf", "align", "sel", "batch", "slabs"))
+        b0, b1 = parallel.blocks(nf, size)[rank]
+        mt = motion_table(case["mseed"], nf) if align else None
+        shard = generate(eng, na, b0, max(b1 - b0, 1), seed=case["seed"], motion=mt)[: b1 - b0]
+        src = DeviceSource(shard, sel, offset=b0, n_traj=nf)
+        res = run_pipeline(eng, src, FrameList(nf), align=align, max_batch=batch, merge_slabs=slabs)
+        torch.cuda.synchronize()
+        q.put((rank, res.rmsf.cpu().numpy(), res.extras.get("merge_slabs", 0)))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), -1))
+    finally:
+        dist.destroy_process_group()
+
+
+def run_case(case):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    d = tempfile.mkdtemp(prefix="fuzzmr_")
+    init = "file://" + os.path.join(d, "store")
+    ps = [ctx.Process(target=_worker, args=(r, case["P"], init, q, case), daemon=True) for r in range(case["P"])]
+    for p in ps:
+        p.start()
+    try:
+        return [q.get(timeout=240) for _ in ps]
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+
+
+def main():
+    from oracle import rmsf_oracle as O
+    from oracle import synth as SY
+    from rmsf_amd.synth import motion_table
+    n_cases = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+    rng = np.random.default_rng(303)
+    worst = 0.0
+    for k in range(n_cases):
+        P = int(rng.integers(2, 5))
+        big = k % 6 == 5  # every sixth case: 300k atoms, the chunk-aligned plan (merge slabs)
+        na = 300_000 if big else int(rng.integers(1, 4000))
+        nf = int(rng.integers(P, 40 if big else 160))
+        align = None if big else [None, "frame0", "average"][int(rng.integers(0, 3))]
+        if not big and rng.random() < 0.5:
+            ns = int(rng.integers(1, na + 1))
+            sel = np.sort(rng.choice(na, ns, replace=False))
+        else:
+            sel = None
+        batch = None if (big or rng.random() < 0.5) else int(rng.integers(1, nf + 1))
+        slabs = int(rng.integers(2, 5)) if big else None
+        case = dict(P=P, na=na, nf=nf, align=align, sel=sel, batch=batch, slabs=slabs,
+                    seed=int(rng.integers(0, 1000)), mseed=int(rng.integers(0, 1000)))
+        out = run_case(case)
+        if any(o[2] == -1 for o in out):
+            print(f"case {k}: FAILED {[o[1] for o in out if o[2] == -1][:1]}", flush=True)
+            sys.exit(1)
+        traj = SY.frames(case["seed"], na, 0, nf, motion_table(case["mseed"], nf) if align else None,
+                         atoms=None if not big else None)
+        cols = np.arange(na) if sel is None else sel
+        exp = (O.rmsf_script(traj, cols, None, size=P, align=align)["rmsf"] if not big
+               else O.rmsf_two_pass(traj[:, cols]))
+        d = max(float(np.abs(o[1] - exp).max()) for o in out)
+        worst = max(worst, d)
+        print(f"case {k:2d}: P={P} {na:7d} atoms {len(cols):7d} sel {nf:4d} frames align={align} "
+              f"batch={batch} slabs={out[0][2]} max|d|={d:.2e}", flush=True)
+        if d > 1e-6:
+            print("EXCEEDS 1e-6", flush=True)
+            sys.exit(1)
+    print(f"all {n_cases} cases within 1e-6 A (worst {worst:.2e})")
+
+
+if __name__ == "__main__":
+    main()
