@@ -769,8 +769,8 @@ struct StatsPlan {
 
 __host__ __device__ inline int64_t st_lo(const StatsPlan &p, int64_t b) { return p.T * b / p.G; }
 
-template <bool GATHER, bool MASSES, bool VEC4>
-__global__ __launch_bounds__(kBlock) void k_frame_stats(
+template <bool GATHER, bool MASSES, bool VEC4, int WPE = 1>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_frame_stats(
     const float *__restrict__ xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
     const int32_t *__restrict__ sel, const double *__restrict__ masses, const double *__restrict__ ref,
     StatsPlan pl, double *__restrict__ part) {
