@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""A/B of the balanced grid's plan walks between two builds of the library in
+one process (tools/_ab/librmsf_old.so vs the current one): the fold
+(rmsf_fold_balanced / _shift, k_fold_sk), the accumulate and the
+superposition (k_frame_stats + k_qcp_frames) at the strong-scaling shares,
+each launch timed alone with HIP events, A/B/A; outputs compared byte for
+byte.  python tools/ab_fold.py"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "mdanalysis-mpi_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from rmsf_amd._lib import LIB_PATH, RMSF_MODE_WELFORD, SIGNATURES  # noqa: E402
+from rmsf_amd.engine import Engine  # noqa: E402
+from rmsf_amd.synth import generate, motion_table  # noqa: E402
+
+
+def lib(path):
+    L = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        if hasattr(L, name):
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+    return L
+
+
+def med_time(fn, reps):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    return [a.elapsed_time(b) * 1e3 for a, b in ev]
+
+
+def main():
+    libs = {"old": lib(os.path.join(ROOT, "tools", "_ab", "librmsf_old.so")), "new": lib(LIB_PATH)}
+    eng = Engine()
+    s = lambda: eng.stream  # noqa: E731
+    for n, nf, aligned in ((100_000, 2_500, False), (100_000, 20_000, False), (1_000_000, 2_500, False),
+                           (100_000, 2_500, True), (100_000, 20_000, True)):
+        traj = generate(eng, n, 0, nf, seed=0, motion=motion_table(1, nf) if aligned else None)
+        nc = 3 * n
+        ref, info = eng.reference_setup(n, frame_ptr=traj.data_ptr())
+        xf = {k: eng.empty(nf, 16) for k in libs}
+        sw = eng.empty(eng.workspace_bytes(n, nf) // 8 + 2)
+        work = eng.empty(eng.balanced_workspace_bytes(n, nf) // 8 + 2)
+        shift = traj[0].reshape(-1).clone()
+        out = {k: [eng.empty(nc), eng.empty(nc), eng.empty(2 * nc)] for k in libs}
+        t = {k: {"superpose": [], "accumulate": [], "fold": []} for k in libs}
+        for order in ("old", "new", "old", "new"):
+            L = libs[order]
+
+            def sup():
+                assert L.rmsf_superpose(traj.data_ptr(), nc, nf, n, None, None, ref.data_ptr(), info.data_ptr(),
+                                        xf[order].data_ptr(), sw.data_ptr(), sw.numel() * 8, s()) == 0
+
+            x = xf[order].data_ptr() if aligned else None
+            ip = info.data_ptr() if aligned else None
+
+            def acc():
+                assert L.rmsf_accumulate_balanced(traj.data_ptr(), nc, nf, n, None, x, ip, RMSF_MODE_WELFORD, 0,
+                                                  work.data_ptr(), work.numel() * 8, s()) == 0
+
+            a0, a1, tt = out[order]
+
+            def fold():
+                assert L.rmsf_fold_balanced_shift(work.data_ptr(), nc, 0, a0.data_ptr(), a1.data_ptr(),
+                                                  shift.data_ptr(), 1, None, tt.data_ptr(), s()) == 0
+
+            reps = 30 if nf <= 2500 else 10
+            if aligned:
+                t[order]["superpose"] += med_time(sup, reps)
+            sup()
+            acc()
+            torch.cuda.synchronize()
+            t[order]["accumulate"] += med_time(acc, reps)
+            t[order]["fold"] += med_time(fold, reps)  # acc_n = 0: the fold is idempotent
+            acc()
+            fold()
+            torch.cuda.synchronize()
+        same = all(np.array_equal(a.cpu().numpy().view(np.uint64), b.cpu().numpy().view(np.uint64))
+                   for a, b in zip(out["old"] + [xf["old"]], out["new"] + [xf["new"]]))
+        line = f"{n:8d} x {nf:6d} aligned {aligned!s:5s}:"
+        for kname in ("superpose", "accumulate", "fold"):
+            if not t["old"][kname]:
+                continue
+            o, w = float(np.median(t["old"][kname])), float(np.median(t["new"][kname]))
+            line += f"  {kname} old {o:8.1f} new {w:8.1f} us ({(w / o - 1) * 100:+.1f} %)"
+        print(line + f"  bitwise equal {same}", flush=True)
+        del traj, work, sw
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
