@@ -102,6 +102,9 @@ def parse(argv=None):
     ap.add_argument("--xtc-cache", action="store_true",
                     help="c5xtc (GPU decode): keep decoded frames in HBM within a step (RMSF.py's second sweep "
                          "reads them from HBM); dropped before every step, so each step decodes once")
+    ap.add_argument("--host-layout", choices=["fac", "soa"], default="fac",
+                    help="c5: the host array as [F, n_atoms, 3] (fac) or as x/y/z coordinate planes [F, 3, n_atoms] "
+                         "(soa: the stager interleaves them on the host)")
     ap.add_argument("--host-cache", action="store_true",
                     help="c5: keep the staged frames in HBM within a step (RMSF.py's second sweep reads them there)")
     ap.add_argument("--align", choices=["none", "frame0", "average"], default=None, help="override the workload's")
@@ -486,8 +489,12 @@ def main():
                             n_threads=a.stager_threads if a.xtc_decode == "host" else max(a.stager_threads, 16),
                             n_slots=3, cache=a.xtc_cache)
         else:
+            if a.host_layout == "soa":  # untimed: the same frames as coordinate planes
+                import numpy as np
+
+                host = np.ascontiguousarray(host.transpose(0, 2, 1))
             src = HostSource(host, None, batch_frames=a.stager_batch, n_threads=a.stager_threads, offset=b0,
-                             n_traj=n_total, cache=a.host_cache)
+                             n_traj=n_total, cache=a.host_cache, layout=a.host_layout)
     else:
         src = DeviceSource(traj, offset=b0, n_traj=n_total)
     fl = FrameList(n_total)
@@ -560,6 +567,7 @@ def main():
                          "h2d_gbs": h2d_bytes * a.steps / dt / 1e9,
                          "decoded_frame_gbs": decoded * a.steps / dt / 1e9,
                          "host_cache": bool(getattr(src, "cache", None) is not None),
+                         "host_layout": getattr(src, "layout", "fac"),
                          "threads": a.stager_threads, "batch_frames": src.batch_frames,
                          "host_link_spec_gbs": 63.0}
         if wl.get("xtc"):

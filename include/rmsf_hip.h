@@ -295,6 +295,15 @@ int rmsf_stager_stage(rmsf_stager *st, const float *h_frames,
 int rmsf_stager_stage_ptrs(rmsf_stager *st, const float *const *h_frame_ptrs,
                            int64_t n_frames, void *consumer_stream, int *slot,
                            float **d_batch);
+/* Stage frames stored as coordinate planes (SoA): frame f's x[n_atoms_frame],
+ * y and z at h_frame_ptrs[f], + h_plane_stride and + 2*h_plane_stride floats
+ * (h_plane_stride >= n_atoms_frame) -- a synthetic [F][3][n] array, or a DCD
+ * frame's X/Y/Z records in place (RMSF.py:92,124's reader interleaves them
+ * per frame).  The selection is gathered and interleaved on the host into
+ * the same compact [n_frames][n_sel][3] device batch as rmsf_stager_stage().*/
+int rmsf_stager_stage_planes(rmsf_stager *st, const float *const *h_frame_ptrs,
+                             int64_t h_plane_stride, int64_t n_frames,
+                             void *consumer_stream, int *slot, float **d_batch);
 /* Decode XTC frames f0, f0+step, ... (n_frames of them) frame-parallel
  * straight into the next pinned slot (selection applied), then DMA it. */
 typedef struct rmsf_xtc rmsf_xtc;
@@ -480,6 +489,11 @@ int rmsf_push_xtc_frames(rmsf_ctx *ctx, const rmsf_xtc *x, const int64_t *h_fram
  * stager gathers the selection from every frame into its pinned slots.      */
 int rmsf_push_frame_ptrs(rmsf_ctx *ctx, const float *const *h_ptrs,
                          int64_t n_frames, int mode);
+/* The same for host frames stored as coordinate planes (SoA; see
+ * rmsf_stager_stage_planes): x, y, z of frame f at h_ptrs[f] + {0, 1, 2} *
+ * plane_stride floats.                                                      */
+int rmsf_push_frame_planes(rmsf_ctx *ctx, const float *const *h_ptrs,
+                           int64_t plane_stride, int64_t n_frames, int mode);
 
 /* Running Welford partial (RMSF.py:120-121,137-138): *n frames, mean and M2
  * f64 [n_sel][3] (any output may be NULL).  Synchronises.                    */

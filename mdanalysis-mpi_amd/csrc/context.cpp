@@ -911,6 +911,29 @@ RMSF_EXPORT int rmsf_push_frame_ptrs(rmsf_ctx *c, const float *const *h_ptrs, in
   return RMSF_OK;
 }
 
+RMSF_EXPORT int rmsf_push_frame_planes(rmsf_ctx *c, const float *const *h_ptrs, int64_t plane_stride,
+                                       int64_t n_frames, int mode) {
+  CX_OK(check_ctx(c, "rmsf_push_frame_planes"));
+  CX_OK(check_mode(mode, "rmsf_push_frame_planes"));
+  if (n_frames < 0 || (n_frames > 0 && !h_ptrs) || plane_stride < c->n_atoms)
+    return fail(RMSF_EINVAL, "rmsf_push_frame_planes: bad arguments");
+  if (n_frames == 0) return RMSF_OK;
+  DeviceScope ds(c->dev);
+  if (ds.err != hipSuccess) return fail(RMSF_EHIP, "rmsf_push_frame_planes: hipSetDevice failed");
+  CX_OK(ensure_stager(c));
+  for (int64_t f = 0; f < n_frames; f += c->stage_batch) {
+    const int64_t nf = std::min(c->stage_batch, n_frames - f);
+    int slot = -1;
+    float *d = nullptr;
+    CX_OK(rmsf_stager_stage_planes(c->stager, h_ptrs + f, plane_stride, nf, c->stream, &slot, &d));
+    int rc = process(c, d, 3 * c->n_sel, nf, nullptr, mode);
+    int rc2 = rmsf_stager_release(c->stager, slot, c->stream);
+    CX_OK(rc);
+    CX_OK(rc2);
+  }
+  return RMSF_OK;
+}
+
 RMSF_EXPORT int rmsf_get_partial(rmsf_ctx *c, int64_t *n, double *h_mean, double *h_m2) {
   CX_OK(check_ctx(c, "rmsf_get_partial"));
   DeviceScope ds(c->dev);

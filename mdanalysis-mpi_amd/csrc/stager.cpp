@@ -220,6 +220,47 @@ int gather(rmsf_stager *st, int64_t n_frames, const std::function<const float *(
   return bad ? fail(RMSF_EINVAL, "rmsf_stager_stage: null frame pointer") : RMSF_OK;
 }
 
+// Gather the selection of host frames stored as coordinate planes (SoA: x[n],
+// y[n], z[n] at plane(f), plane(f) + plane_stride, plane(f) + 2 plane_stride
+// floats -- a DCD frame's X/Y/Z records, or a synthetic [F][3][n] array) and
+// interleave them into dst's (frame, atom, xyz) rows on the way into the
+// pinned slot: the device sees the same frame blocks as for [F][n][3] input,
+// and the bytes over PCIe stay 12 per selected atom.
+int gather_planes(rmsf_stager *st, int64_t n_frames, const std::function<const float *(int64_t)> &frame,
+                  int64_t plane_stride, float *dst) {
+  const int64_t row = 3 * st->n_sel;
+  const int32_t *sel = st->sel.empty() ? nullptr : st->sel.data();
+  const int64_t n_sel = st->n_sel;
+  const int64_t piece = 1 << 16;
+  const int64_t per_frame = (n_sel + piece - 1) / piece;
+  std::atomic<bool> bad{false};
+  st->pool->run(n_frames * per_frame, [&](int64_t w) {
+    const int64_t f = w / per_frame, a0 = (w % per_frame) * piece, a1 = std::min(n_sel, a0 + piece);
+    const float *x = frame(f);
+    if (!x) {
+      bad = true;
+      return;
+    }
+    const float *y = x + plane_stride, *z = y + plane_stride;
+    float *o = dst + f * row;
+    if (!sel) {
+      for (int64_t a = a0; a < a1; ++a) {
+        o[3 * a] = x[a];
+        o[3 * a + 1] = y[a];
+        o[3 * a + 2] = z[a];
+      }
+    } else {
+      for (int64_t a = a0; a < a1; ++a) {
+        const int64_t i = sel[a];
+        o[3 * a] = x[i];
+        o[3 * a + 1] = y[i];
+        o[3 * a + 2] = z[i];
+      }
+    }
+  });
+  return bad ? fail(RMSF_EINVAL, "rmsf_stager_stage_planes: null frame pointer") : RMSF_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -289,6 +330,18 @@ RMSF_EXPORT int rmsf_stager_stage_ptrs(rmsf_stager *st, const float *const *h_fr
   if (!st || !h_frame_ptrs || !slot || !d_batch) return fail(RMSF_EINVAL, "rmsf_stager_stage_ptrs: bad arguments");
   return fill_and_copy(
       st, n_frames, [&](float *dst) { return gather(st, n_frames, [&](int64_t f) { return h_frame_ptrs[f]; }, dst); },
+      consumer_stream, slot, d_batch);
+}
+
+RMSF_EXPORT int rmsf_stager_stage_planes(rmsf_stager *st, const float *const *h_frame_ptrs, int64_t h_plane_stride,
+                                         int64_t n_frames, void *consumer_stream, int *slot, float **d_batch) {
+  if (!st || !h_frame_ptrs || !slot || !d_batch || h_plane_stride < st->n_atoms_frame)
+    return fail(RMSF_EINVAL, "rmsf_stager_stage_planes: bad arguments");
+  return fill_and_copy(
+      st, n_frames,
+      [&](float *dst) {
+        return gather_planes(st, n_frames, [&](int64_t f) { return h_frame_ptrs[f]; }, h_plane_stride, dst);
+      },
       consumer_stream, slot, d_batch);
 }
 

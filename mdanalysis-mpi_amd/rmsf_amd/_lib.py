@@ -82,6 +82,7 @@ SIGNATURES = {
     "rmsf_stager_destroy": (c_int, [P]),
     "rmsf_stager_stage": (c_int, [P, P, c_int64, c_int64, P, POINTER(c_int), POINTER(c_void_p)]),
     "rmsf_stager_stage_ptrs": (c_int, [P, P, c_int64, P, POINTER(c_int), POINTER(c_void_p)]),
+    "rmsf_stager_stage_planes": (c_int, [P, P, c_int64, c_int64, P, POINTER(c_int), POINTER(c_void_p)]),
     "rmsf_stager_stage_xtc": (c_int, [P, P, c_int64, c_int64, c_int64, P, POINTER(c_int), POINTER(c_void_p)]),
     "rmsf_stager_release": (c_int, [P, c_int, P]),
     "rmsf_stager_synchronize": (c_int, [P]),
@@ -118,6 +119,7 @@ SIGNATURES = {
     "rmsf_push_xtc": (c_int, [P, P, c_int64, c_int64, c_int64, c_int]),
     "rmsf_push_xtc_frames": (c_int, [P, P, P, c_int64, c_int]),
     "rmsf_push_frame_ptrs": (c_int, [P, P, c_int64, c_int]),
+    "rmsf_push_frame_planes": (c_int, [P, P, c_int64, c_int64, c_int]),
     "rmsf_get_partial": (c_int, [P, POINTER(c_int64), P, P]),
     "rmsf_get_sum": (c_int, [P, POINTER(c_int64), P]),
     "rmsf_get_average": (c_int, [P, P]),

@@ -233,6 +233,19 @@ class Context:
         ptrs = (a.ctypes.data + r * (a.strides[0])).astype(np.uint64)
         call("rmsf_push_frame_ptrs", self._h, ptrs.ctypes.data, r.size, mode)
 
+    def push_planes(self, frames: np.ndarray, rows, mode: int = PUSH_WELFORD) -> None:
+        """Push rows ``rows`` of a host float32 trajectory stored as
+        coordinate planes, [F, 3, n_atoms] (SoA: x, y, z planes per frame),
+        through the stager, which interleaves the selection on the host."""
+        a = frames
+        if a.dtype != np.float32 or a.ndim != 3 or a.shape[1] != 3 or a.shape[2] != self.n_atoms or a.strides[2] != 4:
+            raise ValueError("push_planes: a float32 [F, 3, n_atoms] host array with contiguous planes is required")
+        r = np.asarray(rows, dtype=np.int64)
+        if r.size and (r.min() < 0 or r.max() >= a.shape[0]):
+            raise IndexError("push_planes: row out of range")
+        ptrs = (a.ctypes.data + r * a.strides[0]).astype(np.uint64)
+        call("rmsf_push_frame_planes", self._h, ptrs.ctypes.data, a.strides[1] // 4, r.size, mode)
+
     # -- results --------------------------------------------------------------
     def partial(self):
         n = ctypes.c_int64()

@@ -149,6 +149,29 @@ class DCDFile:
             out[k] = fr if idx is None else fr[idx]
         return out
 
+    def plane_ptrs(self, frames) -> tuple[np.ndarray, int] | None:
+        """Host addresses of the X records of ``frames`` and the distance
+        between a frame's X, Y and Z records in floats (4 n_atoms + 8 bytes),
+        for staging the coordinate planes straight from the memory map
+        (rmsf_stager_stage_planes interleaves them): native-endian files
+        with every atom in every frame and no 4D record; otherwise None.
+        Checks every frame's X/Y/Z record markers, as read() does."""
+        import sys
+
+        if self._e != ("<" if sys.byteorder == "little" else ">") or self.free is not None or self.has_4d:
+            return None
+        f = np.asarray(frames, dtype=np.int64)
+        if f.size and (f.min() < 0 or f.max() >= self.n_frames):
+            raise IndexError(f"frame out of range ({self.n_frames} frames)")
+        n = self.n_atoms
+        x0 = self._data0 + f * self._full + (56 if self.has_cell else 0)  # marker before the X record
+        words = np.frombuffer(self._raw, dtype=np.int32, count=self._raw.size // 4)
+        for k in range(3):
+            m = x0 + k * (8 + 4 * n)
+            if np.any(words[m // 4] != 4 * n) or np.any(words[(m + 4 + 4 * n) // 4] != 4 * n):
+                raise ValueError(f"{self.path}: bad coordinate record markers")
+        return (self._raw.ctypes.data + x0 + 4).astype(np.uint64), n + 2
+
     def close(self) -> None:
         self._raw = None
 

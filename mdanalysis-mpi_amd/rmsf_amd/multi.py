@@ -47,22 +47,35 @@ def device_list(gpus) -> list[int]:
 
 
 class _HostFrames:
-    """A float32 [F, n_atoms, 3] host trajectory; the contexts gather the selection."""
+    """A float32 [F, n_atoms, 3] host trajectory (or [F, 3, n_atoms]
+    coordinate planes, ``layout="soa"``); the contexts gather the selection
+    (and interleave planes) into their stagers."""
 
-    def __init__(self, arr: np.ndarray, sel):
-        if arr.dtype != np.float32 or arr.ndim != 3 or arr.shape[2] != 3:
-            raise ValueError("host trajectory must be float32 [n_frames, n_atoms, 3]")
-        self.arr = np.ascontiguousarray(arr)
-        self.n_traj, self.n_atoms = self.arr.shape[0], self.arr.shape[1]
+    def __init__(self, arr: np.ndarray, sel, layout: str = "fac"):
+        self.layout = layout
+        if layout == "soa":
+            if arr.dtype != np.float32 or arr.ndim != 3 or arr.shape[1] != 3:
+                raise ValueError("SoA host trajectory must be float32 [n_frames, 3, n_atoms]")
+            self.arr = np.ascontiguousarray(arr)
+            self.n_traj, self.n_atoms = self.arr.shape[0], self.arr.shape[2]
+        else:
+            if arr.dtype != np.float32 or arr.ndim != 3 or arr.shape[2] != 3:
+                raise ValueError("host trajectory must be float32 [n_frames, n_atoms, 3]")
+            self.arr = np.ascontiguousarray(arr)
+            self.n_traj, self.n_atoms = self.arr.shape[0], self.arr.shape[1]
         self.sel = None if sel is None else np.ascontiguousarray(sel, dtype=np.int64)
         if self.sel is not None and self.sel.size and (self.sel.min() < 0 or self.sel.max() >= self.n_atoms):
             raise IndexError("selection index out of range")
 
     def reference(self, frame: int) -> np.ndarray:
-        return self.arr[frame]
+        return np.ascontiguousarray(self.arr[frame].T) if self.layout == "soa" else self.arr[frame]
 
     def push(self, ctx: Context, rows: range, mode: int) -> None:
-        if len(rows):
+        if not len(rows):
+            return
+        if self.layout == "soa":
+            ctx.push_planes(self.arr, np.arange(rows.start, rows.stop, rows.step), mode)
+        else:
             # rows is an arithmetic range: a strided view, pushed with its step
             ctx.push(self.arr[rows.start:rows[-1] + 1], mode, step=rows.step)
 
@@ -72,7 +85,11 @@ class _HostFrames:
         if len(runs) == 1:
             self.push(ctx, runs[0], mode)
         elif runs:
-            ctx.push_rows(self.arr, np.concatenate([np.arange(r.start, r.stop, r.step) for r in runs]), mode)
+            rows = np.concatenate([np.arange(r.start, r.stop, r.step) for r in runs])
+            if self.layout == "soa":
+                ctx.push_planes(self.arr, rows, mode)
+            else:
+                ctx.push_rows(self.arr, rows, mode)
 
     def n_sel(self) -> int:
         return self.n_atoms if self.sel is None else len(self.sel)
@@ -102,7 +119,10 @@ class _HostFrames:
                 addr = (self.arr.ctypes.data + frames * self.arr.strides[0]).astype(np.uint64)
                 for row in range(0, total, batch):
                     n = min(batch, total - row)
-                    slot, ptr = st.stage_ptrs(addr[row:row + n], stream)
+                    if self.layout == "soa":
+                        slot, ptr = st.stage_planes(addr[row:row + n], self.arr.strides[1] // 4, stream)
+                    else:
+                        slot, ptr = st.stage_ptrs(addr[row:row + n], stream)
                     cache.fill(row, 1, n, ptr, stream)
                     st.release(slot, stream)
                 torch.cuda.current_stream(dev).synchronize()
@@ -290,11 +310,11 @@ def _blocks_fit(devs, blocks, n_sel: int) -> bool:
     return all(n <= torch.cuda.mem_get_info(d)[0] // 2 for d, n in need.items())
 
 
-def _frames_of(inp, sel, batch_frames):
+def _frames_of(inp, sel, batch_frames, layout: str = "fac"):
     import os
 
     if isinstance(inp, np.ndarray):
-        return _HostFrames(inp, sel)
+        return _HostFrames(inp, sel, layout)
     if isinstance(inp, (list, tuple)) or (hasattr(inp, "is_cuda") and inp.is_cuda):
         return _DeviceShards([inp] if hasattr(inp, "is_cuda") else inp, sel)
     if isinstance(inp, (str, bytes)) or hasattr(inp, "__fspath__"):
@@ -311,7 +331,8 @@ def _frames_of(inp, sel, batch_frames):
 
 
 def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int = 0, start=None, stop=None,
-              step=None, batch_frames: int | None = None, frames=None, collect_rmsd: bool = False) -> dict:
+              step=None, batch_frames: int | None = None, frames=None, collect_rmsd: bool = False,
+              layout: str = "fac") -> dict:
     """RMSF.py's computation over the devices ``gpus`` from one process.
     Returns the ``results`` fields (rmsf, mean, sumsquares, n_frames, ...;
     ``rmsd`` with ``collect_rmsd``: per-frame QCP rmsd of the last sweep in
@@ -323,7 +344,7 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
                          "(one process per GPU) leave it unset")
     if collect_rmsd and align is None:
         raise ValueError("collect_rmsd needs an aligned run (align='frame0' or 'average')")
-    src = _frames_of(inp, select, batch_frames)
+    src = _frames_of(inp, select, batch_frames, layout)
     fl = FrameList(src.n_traj, start, stop, step, frames=frames)
     if len(fl) == 0:
         raise RmsfEmptyError(-4, "RMSF.run", "no frames selected")

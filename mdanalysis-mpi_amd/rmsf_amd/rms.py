@@ -14,7 +14,8 @@ superposes every frame on ``ref_frame`` first (config C3).  Under
 contiguous blocks of RMSF.py:65-69 and merged with RCCL.
 
 Inputs: an MDAnalysis AtomGroup, a host ``numpy`` float32 array
-[n_frames, n_atoms, 3], an HBM-resident torch tensor of that shape, or the
+[n_frames, n_atoms, 3] (or [n_frames, 3, n_atoms] coordinate planes with
+``layout="soa"``), an HBM-resident torch tensor [n_frames, n_atoms, 3], or the
 path of a GROMACS ``.xtc`` or CHARMM/NAMD ``.dcd`` file (read natively,
 selection by ``select``).
 
@@ -69,6 +70,11 @@ class RMSF:
         masses are used.
     ref_frame : int
         Trajectory frame of the first reference (RMSF.py:63).
+    layout : "fac" | "soa"
+        Host array inputs only: "fac" = [F, n_atoms, 3] (MDAnalysis'
+        positions per frame), "soa" = [F, 3, n_atoms] (x, y and z coordinate
+        planes per frame; the stager interleaves the selection on the host,
+        the device path is unchanged).
     gpus : int | list of int, optional
         Drive this many devices (or these device ids) from one process: each
         takes the RMSF.py:65-69 block of its index and the blocks merge over
@@ -82,7 +88,13 @@ class RMSF:
     def __init__(self, atomgroup, *, select=None, align=None, masses=None, ref_frame: int = 0,
                  device=None, batch_frames: int | None = None, n_splits: int | None = None,
                  collect_rmsd: bool = False, verbose: bool = False, gpus=None,
-                 collect_transforms: bool = False, **kwargs):
+                 collect_transforms: bool = False, layout: str = "fac", **kwargs):
+        if layout not in ("fac", "soa"):
+            raise ValueError(f"layout must be 'fac' or 'soa', got {layout!r}")
+        if layout == "soa" and not isinstance(atomgroup, np.ndarray):
+            raise ValueError("layout='soa' describes a host numpy array [F, 3, n_atoms]; HBM tensors, files and "
+                             "AtomGroups have their own layout")
+        self.layout = layout
         self._input = atomgroup
         self.select = select
         self.align = align
@@ -146,7 +158,8 @@ class RMSF:
 
         out = run_multi(self._input, self.gpus, select=self.select, align=self.align, masses=self.masses,
                         ref_frame=self.ref_frame, start=start, stop=stop, step=step,
-                        batch_frames=self.batch_frames, frames=frames, collect_rmsd=self.collect_rmsd)
+                        batch_frames=self.batch_frames, frames=frames, collect_rmsd=self.collect_rmsd,
+                        layout=self.layout)
         r = self.results
         r.update(out)
         r.m2 = r.sumsquares
@@ -170,7 +183,8 @@ class RMSF:
         # (RMSF.py:92,124): host sources then keep the staged frames in HBM
         two = self.align == "average"
         if isinstance(x, np.ndarray):
-            return HostSource(x, self.select, batch_frames=self.batch_frames, cache=two), self.masses
+            return HostSource(x, self.select, batch_frames=self.batch_frames, cache=two,
+                              layout=self.layout), self.masses
         if isinstance(x, (str, bytes)) or hasattr(x, "__fspath__"):
             import os
             path = os.fspath(x)

@@ -75,6 +75,16 @@ class Stager:
         call("rmsf_stager_stage_ptrs", self._h, p.ctypes.data, p.size, stream, ctypes.byref(slot), ctypes.byref(dptr))
         return slot.value, dptr.value
 
+    def stage_planes(self, ptrs: np.ndarray, plane_stride: int, stream: int) -> tuple[int, int]:
+        """Stage the frames whose x planes start at host addresses ``ptrs``
+        (uint64, one per frame; y and z ``plane_stride`` floats apart): the
+        selection is interleaved into (frame, atom, xyz) rows on the host."""
+        p = np.ascontiguousarray(ptrs, dtype=np.uint64)
+        slot, dptr = ctypes.c_int(), ctypes.c_void_p()
+        call("rmsf_stager_stage_planes", self._h, p.ctypes.data, int(plane_stride), p.size, stream,
+             ctypes.byref(slot), ctypes.byref(dptr))
+        return slot.value, dptr.value
+
     def stage_compact(self, buf: np.ndarray, n: int, stream: int) -> tuple[int, int]:
         slot, dptr = ctypes.c_int(), ctypes.c_void_p()
         call("rmsf_stager_stage", self._h, buf.ctypes.data, buf.shape[1] * 3, n, stream, ctypes.byref(slot),
@@ -360,15 +370,33 @@ class HostSource:
     keeps the staged frames resident in HBM for later sweeps (FrameCache;
     ignored when they would take more than half of the free device memory).
     A cached row is not re-read: call ``drop_cache()`` after changing the
-    host array in place (``RMSF.run`` builds a fresh source per run)."""
+    host array in place (``RMSF.run`` builds a fresh source per run).
+
+    ``layout="soa"``: the array is [F, 3, n_atoms] -- each frame's x, y and
+    z coordinate planes (structure of arrays; frames and planes may be
+    strided, atoms contiguous).  The stager interleaves the selection into
+    the (frame, atom, xyz) device batches on the host
+    (rmsf_stager_stage_planes): same device frames, same results."""
 
     def __init__(self, traj: np.ndarray, sel=None, batch_frames: int | None = None, n_slots: int = 3,
-                 n_threads: int = 4, offset: int = 0, n_traj: int | None = None, cache: bool = False):
-        traj = np.ascontiguousarray(traj, dtype=np.float32)
-        if traj.ndim != 3 or traj.shape[2] != 3:
-            raise ValueError("trajectory must be [n_frames, n_atoms, 3]")
+                 n_threads: int = 4, offset: int = 0, n_traj: int | None = None, cache: bool = False,
+                 layout: str = "fac"):
+        if layout not in ("fac", "soa"):
+            raise ValueError(f"layout must be 'fac' ([F, n_atoms, 3]) or 'soa' ([F, 3, n_atoms]), got {layout!r}")
+        self.layout = layout
+        if layout == "soa":
+            traj = np.asarray(traj)
+            if traj.ndim != 3 or traj.shape[1] != 3:
+                raise ValueError("an SoA trajectory must be [n_frames, 3, n_atoms]")
+            if traj.dtype != np.float32 or traj.strides[2] != 4 or traj.strides[0] % 4 or traj.strides[1] % 4 \
+                    or traj.strides[0] < 0 or traj.strides[1] < 0:
+                traj = np.ascontiguousarray(traj, dtype=np.float32)
+        else:
+            traj = np.ascontiguousarray(traj, dtype=np.float32)
+            if traj.ndim != 3 or traj.shape[2] != 3:
+                raise ValueError("trajectory must be [n_frames, n_atoms, 3]")
         self.traj = traj
-        self.n_atoms = traj.shape[1]
+        self.n_atoms = traj.shape[2] if layout == "soa" else traj.shape[1]
         self.offset = offset
         self.n_traj = traj.shape[0] + offset if n_traj is None else n_traj
         sel_arr = None if sel is None else np.ascontiguousarray(sel, dtype=np.int64)
@@ -395,8 +423,19 @@ class HostSource:
             raise IndexError(f"frame {frame} is not in this host shard")
         return frame - self.offset
 
+    def _stage_rows(self, rows: np.ndarray, stream: int) -> Batch:
+        """Host rows ``rows`` (any list) staged as one batch, one pointer per frame."""
+        addr = (self.traj.ctypes.data + np.asarray(rows, dtype=np.int64) * self.traj.strides[0]).astype(np.uint64)
+        if self.layout == "soa":
+            slot, ptr = self.stager.stage_planes(addr, self.traj.strides[1] // 4, stream)
+        else:
+            slot, ptr = self.stager.stage_ptrs(addr, stream)
+        return Batch(ptr, 3 * self.n_sel, len(addr), None, lambda: self.stager.release(slot, stream))
+
     def _stage(self, row: int, step: int, n: int, stream: int) -> Batch:
         def stage():
+            if self.layout == "soa":
+                return self._stage_rows(row + step * np.arange(n, dtype=np.int64), stream)
             slot, ptr = self.stager.stage(self.traj, row, step, n, stream)
             return Batch(ptr, 3 * self.n_sel, n, None, lambda: self.stager.release(slot, stream))
 
@@ -410,11 +449,9 @@ class HostSource:
         if _scattered(frames, b0, b1, nb):
             g = _Gather(self.n_sel, nb, self.cache.buf.device) if self.cache is not None else None
             idx = frames.idx[b0:b1]
-            fb = self.traj.strides[0]
 
             def stage(rows):
-                slot, ptr = self.stager.stage_ptrs(self.traj.ctypes.data + rows * fb, stream)
-                return Batch(ptr, 3 * self.n_sel, len(rows), None, lambda: self.stager.release(slot, stream))
+                return self._stage_rows(rows, stream)
 
             for i in range(0, len(idx), nb):
                 part = idx[i:i + nb]
@@ -632,7 +669,11 @@ class DcdSource:
     streamed: each batch's selected rows are read from the memory-mapped file
     (the x/y/z planes interleaved on the host -- what RMSF.py:92,124's reader
     does per frame) and staged, so reading batch k+1 overlaps the copy and
-    kernels of batch k and host memory stays bounded by the batch.
+    kernels of batch k and host memory stays bounded by the batch.  Native-
+    endian files with every atom in every frame are staged straight from the
+    map: the stager's threads gather the selection from the X/Y/Z records and
+    interleave it into the pinned slot (rmsf_stager_stage_planes), with no
+    intermediate array; other files are read by DCDFile.read first.
     ``cache=True``: FrameCache (RMSF.py's second loop reads HBM)."""
 
     def __init__(self, path, sel=None, batch_frames: int | None = None, n_slots: int = 3, cache: bool = False):
@@ -647,7 +688,11 @@ class DcdSource:
         if batch_frames is None:  # ~64 MB per slot
             batch_frames = max(1, min(4096, (64 << 20) // max(1, 12 * self.n_sel)))
         self.batch_frames = batch_frames
-        self.stager = Stager(self.n_sel, self.n_sel, None, batch_frames, n_slots, 1)
+        self.planes = self.n_traj > 0 and self.f.plane_ptrs([0]) is not None
+        if self.planes:  # the stager gathers the selection from the mapped planes
+            self.stager = Stager(self.n_atoms, self.n_sel, self.sel, batch_frames, n_slots, 4)
+        else:
+            self.stager = Stager(self.n_sel, self.n_sel, None, batch_frames, n_slots, 1)
         ok = cache and FrameCache.fits(self.n_traj, self.n_sel)
         self.cache = FrameCache(self.n_traj, self.n_sel) if ok else None
 
@@ -658,8 +703,20 @@ class DcdSource:
         if self.cache is not None:
             self.cache.drop()
 
+    def _stage_frames(self, frames: np.ndarray, stream: int) -> Batch:
+        """Frames ``frames`` (any list) as one staged batch."""
+        if self.planes:
+            ptrs, plane_stride = self.f.plane_ptrs(frames)
+            slot, ptr = self.stager.stage_planes(ptrs, plane_stride, stream)
+        else:
+            buf = np.concatenate([self.f.read(first, n, step, self.sel) for first, step, n in _list_runs(frames)])
+            slot, ptr = self.stager.stage_compact(buf, len(frames), stream)  # copied into the pinned slot on return
+        return Batch(ptr, 3 * self.n_sel, len(frames), None, lambda: self.stager.release(slot, stream))
+
     def _stage(self, first: int, step: int, n: int, stream: int) -> Batch:
         def stage():
+            if self.planes:
+                return self._stage_frames(first + step * np.arange(n, dtype=np.int64), stream)
             buf = np.ascontiguousarray(self.f.read(first, n, step, self.sel))
             slot, ptr = self.stager.stage_compact(buf, n, stream)  # copied into the pinned slot on return
             return Batch(ptr, 3 * self.n_sel, n, None, lambda: self.stager.release(slot, stream))
@@ -677,9 +734,7 @@ class DcdSource:
             g = _Gather(self.n_sel, nb, self.cache.buf.device) if self.cache is not None else None
 
             def stage(rows):
-                buf = np.concatenate([self.f.read(first, n, step, self.sel) for first, step, n in _list_runs(rows)])
-                slot, ptr = self.stager.stage_compact(buf, len(rows), stream)
-                return Batch(ptr, 3 * self.n_sel, len(rows), None, lambda: self.stager.release(slot, stream))
+                return self._stage_frames(rows, stream)
 
             idx = frames.idx[b0:b1]
             for i in range(0, len(idx), nb):

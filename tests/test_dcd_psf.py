@@ -97,6 +97,50 @@ def test_dcd_rejects_garbage(tmp_path):
         DCDFile(p).read()
 
 
+@pytest.mark.parametrize("box", [None, (60.0, 90.0, 60.0, 90.0, 90.0, 60.0)])
+def test_dcd_plane_ptrs(tmp_path, box):
+    """The addresses DcdSource hands to rmsf_stager_stage_planes: frame f's X
+    record, Y and Z records plane_stride floats further on -- read back
+    through them, they give read()'s frames; markers are checked; files the
+    plane path cannot read in place (other byte order, fixed atoms) return
+    None and keep the read() path."""
+    import ctypes
+
+    rng = np.random.default_rng(5)
+    x = rng.uniform(-50, 50, (6, 101, 3)).astype(np.float32)
+    p = str(tmp_path / "p.dcd")
+    write_dcd(p, x, box=box)
+    with DCDFile(p) as f:
+        frames = np.array([0, 2, 5, 3])
+        ptrs, ps = f.plane_ptrs(frames)
+        assert ps == 101 + 2 and ptrs.dtype == np.uint64
+        for k, fr in enumerate(frames):
+            buf = (ctypes.c_float * (2 * ps + 101)).from_address(int(ptrs[k]))
+            planes = np.frombuffer(buf, dtype=np.float32)
+            got = np.stack([planes[c * ps:c * ps + 101] for c in range(3)], axis=1)
+            np.testing.assert_array_equal(got, x[fr])
+        with pytest.raises(IndexError):
+            f.plane_ptrs([6])
+    b = bytearray(open(p, "rb").read())
+    with DCDFile(p) as f:
+        pos = f._data0 + 2 * f._full + (56 if box else 0) + (8 + 4 * 101)  # frame 2's Y record marker
+    b[pos:pos + 4] = struct.pack("<i", 8)
+    q = str(tmp_path / "bad.dcd")
+    open(q, "wb").write(bytes(b))
+    with DCDFile(q) as f:
+        f.plane_ptrs([0, 1])
+        with pytest.raises(ValueError, match="markers"):
+            f.plane_ptrs([1, 2])
+    write_dcd(p, x, byteorder=">")
+    with DCDFile(p) as f:
+        assert f.plane_ptrs([0]) is None
+    fixed = np.array([1, 4])
+    x[1:, fixed] = x[0, fixed]
+    write_dcd(p, x, fixed=fixed)
+    with DCDFile(p) as f:
+        assert f.plane_ptrs([0]) is None
+
+
 def test_psf_topology_selection(tmp_path):
     resids = [1, 1, 1, 2, 2, 2, 3, 4, 4]
     resnames = ["MET", "MET", "MET", "HSD", "HSD", "HSD", "TIP3", "POPC", "POPC"]

@@ -1,0 +1,138 @@
+"""GPU tier: host frames stored as coordinate planes (SoA, [F, 3, n_atoms] --
+the north star's "synthetic in-memory SoA coordinate array", and a DCD
+frame's X/Y/Z records in place) staged through rmsf_stager_stage_planes,
+which interleaves the selection into the same (frame, atom, xyz) device
+batches as [F, n_atoms, 3] input.  The results must be BITWISE those of the
+[F, n_atoms, 3] path (itself checked against the oracle and the reference
+vectors) in every mode, for selections, strides, scattered frame lists,
+padded planes, the one-process multi-device path and the context ABI; and
+within 1e-6 A of the C1 golden vectors (RMSF.py)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import synth as SY
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def c1():
+    d = np.load(os.path.join(GOLDEN, "c1_synth.npz"))
+    traj = SY.frames(int(d["seed"]), int(d["n_atoms"]), 0, int(d["n_frames"]), d["motion"])
+    return d, traj
+
+
+def _soa(traj, pad=0):
+    """[F, 3, n] planes (optionally padded: plane stride n + pad floats)."""
+    F, n, _ = traj.shape
+    out = np.full((F, 3, n + pad), np.nan, np.float32)
+    out[:, :, :n] = traj.transpose(0, 2, 1)
+    return out[:, :, :n] if pad else np.ascontiguousarray(out)
+
+
+def _same(a, b):
+    for k in ("rmsf", "mean", "sumsquares"):
+        np.testing.assert_array_equal(a.results[k], b.results[k])
+    assert a.results.n_frames == b.results.n_frames
+
+
+@pytest.mark.parametrize("align,tag", [(None, "none"), ("frame0", "frame0"), ("average", "average")])
+@pytest.mark.parametrize("pad", [0, 5])
+def test_soa_bitwise_and_golden(c1, align, tag, pad):
+    from rmsf_amd import RMSF
+    d, traj = c1
+    soa = _soa(traj, pad)
+    r_fac = RMSF(traj, select=d["sel"], align=align).run()
+    r_soa = RMSF(soa, select=d["sel"], align=align, layout="soa").run()
+    _same(r_fac, r_soa)
+    np.testing.assert_allclose(r_soa.results.rmsf, d[f"rmsf_{tag}_P1"], rtol=0, atol=TOL)
+
+
+@pytest.mark.parametrize("align", [None, "average"])
+def test_soa_slices_frames_batches(c1, align):
+    from rmsf_amd import RMSF
+    d, traj = c1
+    soa = _soa(traj)
+    for kw, run in (({"batch_frames": 7}, {"start": 3, "stop": 90, "step": 2}),
+                    ({}, {"frames": np.sort(np.random.default_rng(2).choice(98, 41, replace=False))}),
+                    ({"batch_frames": 5}, {"frames": np.arange(0, 98, 9)})):
+        a = RMSF(traj, select=d["sel"], align=align, **kw).run(**run)
+        b = RMSF(soa, select=d["sel"], align=align, layout="soa", **kw).run(**run)
+        _same(a, b)
+
+
+def test_soa_all_atoms_large():
+    """Every atom of a 60k-atom frame set (the contiguous gather, several
+    65,536-atom pieces per frame in the stager's pool at 150k)."""
+    from rmsf_amd import RMSF
+    for n in (60_000, 150_000):
+        traj = SY.frames(9, n, 0, 12, None)
+        _same(RMSF(traj).run(), RMSF(_soa(traj), layout="soa").run())
+
+
+@pytest.mark.parametrize("align", [None, "frame0", "average"])
+def test_soa_multi_device_path(c1, align):
+    """gpus=1: the context ABI's rmsf_push_frame_planes."""
+    from rmsf_amd import RMSF
+    d, traj = c1
+    a = RMSF(traj, select=d["sel"], align=align, gpus=1).run()
+    b = RMSF(_soa(traj), select=d["sel"], align=align, layout="soa", gpus=1).run()
+    _same(a, b)
+    a = RMSF(traj, select=d["sel"], align=align, gpus=1).run(frames=[1, 5, 6, 40, 41, 42, 97])
+    b = RMSF(_soa(traj), select=d["sel"], align=align, layout="soa", gpus=1).run(frames=[1, 5, 6, 40, 41, 42, 97])
+    _same(a, b)
+
+
+def test_soa_context_push(c1):
+    from rmsf_amd.context import PUSH_WELFORD, Context
+    d, traj = c1
+    soa = _soa(traj)
+    out = []
+    for planes in (False, True):
+        c = Context(traj.shape[1], d["sel"])
+        rows = np.array([0, 3, 4, 5, 50, 97])
+        if planes:
+            c.push_planes(soa, rows, PUSH_WELFORD)
+        else:
+            c.push_rows(traj, rows, PUSH_WELFORD)
+        out.append(c.partial())
+        c.close()
+    assert out[0][0] == out[1][0] == 6
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+    np.testing.assert_array_equal(out[0][2], out[1][2])
+
+
+@pytest.mark.parametrize("box", [None, (60.0, 90.0, 60.0, 90.0, 90.0, 60.0)])
+@pytest.mark.parametrize("align", [None, "average"])
+def test_dcd_planes_path_bitwise(tmp_path, c1, box, align, monkeypatch):
+    """A native DCD staged from its mapped X/Y/Z records equals the read()
+    path (the same file with the plane path switched off) and the array."""
+    from rmsf_amd import RMSF
+    from rmsf_amd.dcd import DCDFile, write_dcd
+    d, traj = c1
+    p = str(tmp_path / "c1.dcd")
+    write_dcd(p, traj, box=box)
+    fl = np.sort(np.random.default_rng(4).choice(98, 30, replace=False))
+    got = [RMSF(p, select=d["sel"], align=align).run(), RMSF(p, select=d["sel"], align=align).run(frames=fl)]
+    monkeypatch.setattr(DCDFile, "plane_ptrs", lambda self, frames: None)
+    want = [RMSF(p, select=d["sel"], align=align).run(), RMSF(p, select=d["sel"], align=align).run(frames=fl)]
+    for a, b in zip(got, want):
+        _same(a, b)
+    _same(got[0], RMSF(traj, select=d["sel"], align=align).run())
+
+
+def test_soa_bad_inputs(c1):
+    import torch
+
+    from rmsf_amd import RMSF
+    d, traj = c1
+    with pytest.raises(ValueError, match="SoA trajectory"):
+        RMSF(traj, layout="soa").run()  # [F, n, 3] is not planes
+    with pytest.raises(ValueError, match="layout"):
+        RMSF(torch.zeros(2, 5, 3, device="cuda"), layout="soa")
+    with pytest.raises(ValueError, match="layout"):
+        RMSF(traj, layout="aos")
