@@ -1,6 +1,7 @@
 """Randomised parity sweep (not product code, not a test): random shapes,
 selections, align modes, frame selections and inputs (HBM tensor / host
-array / DCD or XTC file) through RMSF(...).run() vs the oracle's RMSF.py
+array in rows or coordinate planes / DCD or XTC file / one-process gpus=1)
+through RMSF(...).run() vs the oracle's RMSF.py
 restatement on the selected frames.  python tools/fuzz_parity.py [n_cases]"""
 import os
 import sys
@@ -34,11 +35,17 @@ def main():
         frames = np.flatnonzero(rng.random(nf) < rng.uniform(0.2, 1.0))
         if frames.size == 0 or frames[0] != 0:
             frames = np.concatenate([[0], frames[frames != 0]])  # keep the frame-0 reference in the list
-        where = ["device", "host", "dcd", "xtc"][int(rng.integers(0, 4))]
+        where = ["device", "host", "soa", "dcd", "xtc", "gpus1"][int(rng.integers(0, 6))]
+        kw = {}
         if where == "device":
             x = torch.tensor(traj, device="cuda")
-        elif where == "host":
+        elif where in ("host", "gpus1"):
             x = traj
+            if where == "gpus1":  # one process, the context ABI (rmsf_amd.multi)
+                kw["gpus"] = 1
+        elif where == "soa":  # [F, 3, n] coordinate planes, interleaved by the stager
+            x = np.ascontiguousarray(traj.transpose(0, 2, 1))
+            kw["layout"] = "soa"
         elif where == "dcd":
             x = os.path.join(tmp, f"c{k}.dcd")
             write_dcd(x, traj)
@@ -48,7 +55,7 @@ def main():
             with XTCFile(x) as f:
                 traj = f.read()
         bf = int(rng.integers(1, 64))
-        got = RMSF(x, select=sel, align=align, batch_frames=bf).run(frames=frames).results.rmsf
+        got = RMSF(x, select=sel, align=align, batch_frames=bf, **kw).run(frames=frames).results.rmsf
         exp = O.rmsf_script(traj[frames], sel, None, size=1, align=align)["rmsf"]
         err = float(np.abs(got - exp).max())
         worst = max(worst, err)
