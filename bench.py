@@ -111,6 +111,9 @@ def parse(argv=None):
     ap.add_argument("--merge-slabs", type=int, default=None,
                     help="N>1, no alignment: atom slabs of the final sweep whose all-reduces overlap the next slab "
                          "(default: 2 from 1M atoms, else none; 0 = off)")
+    ap.add_argument("--merge-root", action="store_true",
+                    help="N>1: merge with a reduce to rank 0 (RMSF.py:143's comm.reduce(root=0)) instead of an "
+                         "all-reduce that leaves the result on every rank")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo only "
                                                      "to rehearse several ranks on one GPU)")
     return ap.parse_args(argv)
@@ -503,7 +506,8 @@ def main():
         if hasattr(src, "drop_cache"):
             src.drop_cache()  # every step streams the file again
         return run_pipeline(eng, src, fl, align=align, block=(b0, b1), ref_owner=0, n_splits=a.splits,
-                            max_batch=a.batch_frames, timer=timer, merge_slabs=a.merge_slabs)
+                            max_batch=a.batch_frames, timer=timer, merge_slabs=a.merge_slabs,
+                            merge_root=0 if a.merge_root else None)
 
     def timed(align, steps, warmup):
         timer = KernelTimer()
@@ -530,6 +534,7 @@ def main():
     out = base_line(a, wl, world, dt, par)
     if world > 1:
         out["config"]["merge_slabs"] = res.extras.get("merge_slabs", 0)
+        out["config"]["merge"] = "reduce to rank 0 (RMSF.py:143)" if a.merge_root else "all-reduce"
     launches, acc_ms, acc_af = timer.totals("accumulate")
     traffic = load_traffic(a.workload, n_atoms, n_local) if launches == a.steps else None
     kname = (("k_accum_atoms" if wl["align"] else "k_welford_flat") if a.splits
@@ -539,7 +544,8 @@ def main():
     rows = gather_rank_rows([launches, acc_ms, acc_af], coll_dev)
     out["roofline"] = rank_roofline(kname, rows, traffic, f"profiles/pmc_{a.workload}.json" if traffic else None)
     out["cpu_baseline"] = cpu
-    out["rmsf_checksum"] = float(res.rmsf.sum())  # the merged result, identical on every rank
+    # the merged result, identical on every rank (on rank 0 only with --merge-root)
+    out["rmsf_checksum"] = float(res.rmsf.sum()) if res.rmsf is not None else None
     # whole-step rate in algorithmic bytes (incl. merges, finalise, launch gaps)
     out["pipeline_hbm_gbs"] = B_PER_ATOM_FRAME * n_atoms * n_local * a.steps / dt / 1e9
     if wl["align"]:

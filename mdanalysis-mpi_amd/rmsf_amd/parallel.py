@@ -5,7 +5,8 @@ Replaces the mpi4py layer of RMSF.py:
   * RMSF.py:107-111 Barrier + Allreduce(SUM) of positions -> ``allreduce_sum_``
   * RMSF.py:141-143 Barrier + pickle comm.reduce(second_order_moments)
         -> ``global_chan_shifted``: the k-way Chan merge as ONE all-reduce(SUM)
-           of moments about a shift every rank holds (the pipeline's form), or
+           of moments about a shift every rank holds (the pipeline's form;
+           ``root=r``: a reduce to rank r, RMSF.py:143's own shape), or
            ``global_chan``: the same merge as two all-reduce(SUM) passes
            (mean, then deviations) -- over RCCL (torch.distributed "nccl"
            backend = RCCL on ROCm).
@@ -84,6 +85,16 @@ def allreduce_sum_async(t: torch.Tensor):
     return None
 
 
+def reduce_sum_async(t: torch.Tensor, root: int):
+    """Start a SUM of ``t`` into rank ``root`` (RMSF.py:143's
+    ``comm.reduce(..., root=0)``); returns the work, or None for a single
+    process.  Only ``root``'s ``t`` holds the sum afterwards."""
+    _, size = world()
+    if size > 1:
+        return dist.reduce(t, dst=root, op=dist.ReduceOp.SUM, async_op=True)
+    return None
+
+
 def broadcast_async(t: torch.Tensor, src: int):
     """Start an in-place broadcast from ``src``; returns the work (wait() orders
     the then-current stream after it), or None for a single process."""
@@ -94,7 +105,8 @@ def broadcast_async(t: torch.Tensor, src: int):
 
 
 def global_chan_shifted(ops, mean_k: torch.Tensor, m2_k: torch.Tensor, n_k: int, n_total: int, shift: torch.Tensor,
-                        off3: torch.Tensor | None = None, shift_work=None, packed: torch.Tensor | None = None):
+                        off3: torch.Tensor | None = None, shift_work=None, packed: torch.Tensor | None = None,
+                        root: int | None = None):
     """The k-way Chan merge in ONE all-reduce: moments about a shift c that
     every rank already holds (c = shift + off3 per xyz: the sweep's reference
     structure, the sweep-1 average, or frame 0 broadcast during the sweep).
@@ -105,8 +117,11 @@ def global_chan_shifted(ops, mean_k: torch.Tensor, m2_k: torch.Tensor, n_k: int,
     cancellation).  Returns (mean, M2, rmsf) -- the finalise of RMSF.py:146 is
     fused into the unpacking.  ``shift_work``: the pending broadcast that
     fills ``shift``, waited for here (it ran beside the sweep).  ``packed``:
-    T1/T2 already written by the last fold (rmsf_fold_balanced_shift)."""
-    _, size = world()
+    T1/T2 already written by the last fold (rmsf_fold_balanced_shift).
+    ``root``: reduce to that rank only, as RMSF.py:143 does (half the
+    collective's bytes of an all-reduce); the other ranks get
+    (None, None, None)."""
+    rank, size = world()
     if n_total <= 0:
         raise ZeroDivisionError("global_chan_shifted: no frames on any rank")
     n = mean_k.numel()
@@ -118,7 +133,12 @@ def global_chan_shifted(ops, mean_k: torch.Tensor, m2_k: torch.Tensor, n_k: int,
             shift_work.wait()
         ops.chan_shift_pack(mean_k, m2_k, shift, off3, float(n_k), t)
     if size > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        if root is None:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        else:
+            dist.reduce(t, dst=root, op=dist.ReduceOp.SUM)
+            if rank != root:
+                return None, None, None
     mean, m2 = torch.empty_like(mean_k), torch.empty_like(m2_k)
     rmsf = torch.empty(n // 3, dtype=mean_k.dtype, device=mean_k.device)
     ops.chan_shift_finish(t, shift, off3, n // 3, n_total, mean, m2, rmsf)

@@ -188,9 +188,10 @@ class Superposer:
 
 @dataclass
 class PipelineResult:
-    rmsf: torch.Tensor            # f64 [n_sel]
-    mean: torch.Tensor            # f64 [n_sel, 3]
-    m2: torch.Tensor              # f64 [n_sel, 3]  (sum of squares, RMSF.py:120)
+    # None on the non-root ranks of a reduce-to-root merge (merge_root)
+    rmsf: torch.Tensor | None     # f64 [n_sel]
+    mean: torch.Tensor | None     # f64 [n_sel, 3]
+    m2: torch.Tensor | None       # f64 [n_sel, 3]  (sum of squares, RMSF.py:120)
     n_frames: int                 # frames over all ranks
     n_local: int                  # frames of this rank's block
     block: tuple[int, int]
@@ -287,7 +288,8 @@ def _slab_bounds(n_chunks: int, k: int) -> list[tuple[int, int]]:
     return list(zip(b[:-1], b[1:]))
 
 
-def _slab_sweep(eng: Engine, acc: "Accumulator", b: Batch, slabs: list, shift, off3, shift_work, timer):
+def _slab_sweep(eng: Engine, acc: "Accumulator", b: Batch, slabs: list, shift, off3, shift_work, timer,
+                root: int | None = None):
     """The final Welford sweep of one resident batch in atom slabs (N > 1):
     slab k's accumulate + fold (which packs its [T1 | T2]) and the start of
     its all-reduce, then slab k+1 streams while that all-reduce runs.
@@ -306,7 +308,8 @@ def _slab_sweep(eng: Engine, acc: "Accumulator", b: Batch, slabs: list, shift, o
             shift_work = None
         t = torch.empty(2 * (j1 - j0), dtype=torch.float64, device=eng.device)
         eng.fold_balanced_shift_slab(acc.work, n_coord, acc.n, acc.parts0[0], acc.parts1[0], shift, off3, t, c0, c1)
-        out.append((t, j0, j1, parallel.allreduce_sum_async(t)))
+        work = parallel.allreduce_sum_async(t) if root is None else parallel.reduce_sum_async(t, root)
+        out.append((t, j0, j1, work))
     acc.n += b.n_frames
     return out
 
@@ -315,17 +318,23 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                  max_batch: int | None = None, n_splits: int | None = None, collect_rmsd: bool = False,
                  ref_owner: int | None = None, block: tuple[int, int] | None = None,
                  timer: KernelTimer | None = None, collect_transforms: bool = False,
-                 merge_slabs: int | None = None) -> PipelineResult:
+                 merge_slabs: int | None = None, merge_root: int | None = None) -> PipelineResult:
     """``merge_slabs`` (N > 1, no alignment, HBM-resident block in one batch,
     flat chunk-aligned plan): cut the final sweep into that many atom slabs
     so each slab's cross-rank all-reduce overlaps the next slab's stream;
-    None = SLABS_AUTO from SLAB_MIN_ATOMS selected atoms, 0/1 = off."""
+    None = SLABS_AUTO from SLAB_MIN_ATOMS selected atoms, 0/1 = off.
+    ``merge_root`` (N > 1): the final merge is a reduce to that rank, as
+    RMSF.py:143's ``comm.reduce(root=0)``; the other ranks' results are None
+    (rmsf, mean, m2), like RMSF.py's non-root ranks."""
     if align not in ALIGN_MODES:
         raise ValueError(f"align must be one of {ALIGN_MODES}, got {align!r}")
     rank, size = parallel.world()
     n_total = len(frames)
     if n_total == 0:
         raise RmsfEmptyError(-4, "RMSF.run", "no frames selected")
+    if merge_root is not None and not 0 <= merge_root < size:
+        raise ValueError(f"merge_root {merge_root} is not a rank of this {size}-rank group")
+    root = merge_root if size > 1 else None
     std = parallel.blocks(n_total, size)[rank]
     if block is not None and size > 1 and tuple(block) != std:
         # the merge's shift frame (and RMSF.py's decomposition) is defined by
@@ -365,7 +374,8 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                 n_chunks = eng.balanced_slab_chunks(b.ptr, b.fstride, b.n_frames, n_sel)
                 if n_chunks >= 2 * 3:
                     shift_, off3_, _, work_ = pack
-                    slabbed = _slab_sweep(eng, acc, b, _slab_bounds(n_chunks, slabs), shift_, off3_, work_, timer)
+                    slabbed = _slab_sweep(eng, acc, b, _slab_bounds(n_chunks, slabs), shift_, off3_, work_, timer,
+                                          root)
             if slabbed is None:
                 acc.add(b, xf, info, pack if last else None)
             done += b.n_frames
@@ -409,6 +419,12 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     if n_local:
         slabbed = sweep(acc, ref, info, xf_last, (shift, off3, t, shift_work) if size > 1 else None, slabs)
     if slabbed is not None:                                  # RMSF.py:141-143 + 146, slab by slab
+        if root is not None and rank != root:
+            for *_, work in slabbed:
+                if work is not None:
+                    work.wait()
+            return PipelineResult(rmsf=None, mean=None, m2=None, n_frames=n_total, n_local=n_local, block=(b0, b1),
+                                  average=None, rmsd=rmsd, extras={"merge_slabs": len(slabbed), "merge_root": root})
         mean, m2, rmsf = eng.empty(3 * n_sel), eng.empty(3 * n_sel), eng.empty(n_sel)
         for t_k, j0, j1, work in slabbed:
             if work is not None:
@@ -417,11 +433,16 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                                   rmsf[j0 // 3:j1 // 3])
         return PipelineResult(rmsf=rmsf, mean=mean.view(n_sel, 3), m2=m2.view(n_sel, 3), n_frames=n_total,
                               n_local=n_local, block=(b0, b1), average=None, rmsd=rmsd,
-                              extras={"merge_slabs": len(slabbed)})
+                              extras={"merge_slabs": len(slabbed), "merge_root": root})
     if size > 1:                                             # RMSF.py:141-143 + 146: one all-reduce
         mean, m2, rmsf = parallel.global_chan_shifted(eng, acc.result0, acc.result1, acc.n, n_total,
                                                       shift, off3, None if acc.packed else shift_work,
-                                                      packed=t if acc.packed else None)
+                                                      packed=t if acc.packed else None, root=root)
+        if rmsf is None:                                     # a non-root rank of the reduce
+            return PipelineResult(rmsf=None, mean=None, m2=None, n_frames=n_total, n_local=n_local,
+                                  block=(b0, b1), average=None if average is None else average.view(n_sel, 3),
+                                  rmsd=rmsd, transforms=xf_last, transforms_sweep1=xf_first,
+                                  extras={"merge_root": root})
     else:
         mean, m2 = acc.result0, acc.result1
         rmsf = eng.empty(n_sel)

@@ -75,6 +75,11 @@ class RMSF:
         positions per frame), "soa" = [F, 3, n_atoms] (x, y and z coordinate
         planes per frame; the stager interleaves the selection on the host,
         the device path is unchanged).
+    merge_root : int, optional
+        Under ``torch.distributed``: merge the ranks' statistics with a
+        reduce to this rank only, as RMSF.py:143 (``comm.reduce(root=0)``)
+        does; the other ranks' ``results.rmsf`` / ``mean`` / ``sumsquares``
+        are None.  Default: every rank receives the merged result.
     gpus : int | list of int, optional
         Drive this many devices (or these device ids) from one process: each
         takes the RMSF.py:65-69 block of its index and the blocks merge over
@@ -88,13 +93,14 @@ class RMSF:
     def __init__(self, atomgroup, *, select=None, align=None, masses=None, ref_frame: int = 0,
                  device=None, batch_frames: int | None = None, n_splits: int | None = None,
                  collect_rmsd: bool = False, verbose: bool = False, gpus=None,
-                 collect_transforms: bool = False, layout: str = "fac", **kwargs):
+                 collect_transforms: bool = False, layout: str = "fac", merge_root: int | None = None, **kwargs):
         if layout not in ("fac", "soa"):
             raise ValueError(f"layout must be 'fac' or 'soa', got {layout!r}")
         if layout == "soa" and not isinstance(atomgroup, np.ndarray):
             raise ValueError("layout='soa' describes a host numpy array [F, 3, n_atoms]; HBM tensors, files and "
                              "AtomGroups have their own layout")
         self.layout = layout
+        self.merge_root = merge_root
         self._input = atomgroup
         self.select = select
         self.align = align
@@ -129,12 +135,13 @@ class RMSF:
                 print("Process:%3d --> Frames: %10d -- %10d" % (rank, b0, b1))  # RMSF.py:74
             res = run_pipeline(eng, src, fl, align=self.align, masses=masses, ref_frame=self.ref_frame,
                                max_batch=self.batch_frames, n_splits=self.n_splits, collect_rmsd=self.collect_rmsd,
-                               collect_transforms=self.collect_transforms)
+                               collect_transforms=self.collect_transforms, merge_root=self.merge_root)
             torch.cuda.current_stream(eng.device).synchronize()
             r = self.results
-            r.rmsf = res.rmsf.cpu().numpy()
-            r.mean = res.mean.cpu().numpy()
-            r.sumsquares = res.m2.cpu().numpy()
+            host = lambda t: None if t is None else t.cpu().numpy()  # noqa: E731  (None: a non-root rank)
+            r.rmsf = host(res.rmsf)
+            r.mean = host(res.mean)
+            r.sumsquares = host(res.m2)
             r.m2 = r.sumsquares
             r.n_frames = res.n_frames
             r.n_local = res.n_local

@@ -83,7 +83,7 @@ def _worker(rank, size, port, n_frames, q, merge="two"):
             # reference (f64 centred + COM: align="frame0"'s form), by the
             # sweep-1 average (f64: align="average"), or by frame 0 (f32,
             # broadcast by the owner of block 0: no alignment)
-            if merge == "ref":
+            if merge in ("ref", "root"):
                 shift, off3, work = torch.from_numpy(ref_c2.reshape(-1).copy()), torch.from_numpy(ref_com2), None
             elif merge == "average":
                 shift, off3, work = torch.from_numpy(avg.reshape(-1).copy()), None, None
@@ -94,19 +94,20 @@ def _worker(rank, size, port, n_frames, q, merge="two"):
                     shift.copy_(torch.from_numpy(traj[0][sel].reshape(-1)))
                 off3, work = None, parallel.broadcast_async(shift, owner)
             mean, m2, rmsf_t = parallel.global_chan_shifted(OracleOps, mean_k, m2_k, n_k, n_frames, shift, off3,
-                                                            work)
-            rmsf = rmsf_t.numpy()
+                                                            work, root=0 if merge == "root" else None)
+            rmsf = None if rmsf_t is None else rmsf_t.numpy()
         q.put((rank, rmsf, avg))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("merge", ["two", "ref", "average", "frame0"])
+@pytest.mark.parametrize("merge", ["two", "ref", "average", "frame0", "root"])
 @pytest.mark.parametrize("size,n_frames", [(2, 40), (3, 40), (2, 1), (3, 2)])
 def test_gloo_two_sweep_merge(size, n_frames, merge):
     """world_size 2/3, including ranks with empty blocks (n_frames < size);
     the two-all-reduce Chan merge and the one-all-reduce shifted form with
-    each of the pipeline's shifts."""
+    each of the pipeline's shifts; "root": the reduce to rank 0 of
+    RMSF.py:143 (the other ranks get no result)."""
     from oracle import rmsf_oracle as O
     from oracle import synth as SY
     from rmsf_amd.synth import motion_table
@@ -116,5 +117,8 @@ def test_gloo_two_sweep_merge(size, n_frames, merge):
     traj = SY.frames(8, 60, 0, n_frames, motion_table(9, n_frames))
     ref = O.rmsf_script(traj, np.arange(0, 60, 3), None, size=1, align="average")
     for rank, rmsf, avg in out:
-        np.testing.assert_allclose(rmsf, ref["rmsf"], atol=1e-9)
+        if merge == "root" and rank != 0:
+            assert rmsf is None
+        else:
+            np.testing.assert_allclose(rmsf, ref["rmsf"], atol=1e-9)
         np.testing.assert_allclose(avg, ref["average"], atol=1e-9)

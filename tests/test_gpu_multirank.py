@@ -318,3 +318,58 @@ def test_merge_slabs_bitwise(size):
     host = SY.frames(12, n_atoms, 0, n_frames, atoms=atoms).astype(np.float64)
     exp = np.sqrt(((host - host.mean(0)) ** 2).sum(0).sum(1) / n_frames)
     np.testing.assert_allclose(out[0][1][4][0][atoms], exp, rtol=0, atol=1e-9)
+
+
+def _root_worker(rank, size, init, q, n_atoms, n_frames, align, slabs):
+    sys.path[:0] = [ROOT, PKG]
+    import torch
+    import torch.distributed as dist
+
+    from conftest import init_gloo
+    init_gloo(init, rank, size)
+    try:
+        from rmsf_amd import parallel
+        from rmsf_amd.engine import Engine
+        from rmsf_amd.pipeline import run_pipeline
+        from rmsf_amd.sources import DeviceSource, FrameList
+        from rmsf_amd.synth import generate, motion_table
+        eng = Engine(torch.device("cuda", 0))
+        b0, b1 = parallel.blocks(n_frames, size)[rank]
+        mt = motion_table(5, n_frames) if align else None
+        shard = generate(eng, n_atoms, b0, b1 - b0, seed=14, motion=mt)
+        src = DeviceSource(shard, offset=b0, n_traj=n_frames)
+        fl = FrameList(n_frames)
+        every = run_pipeline(eng, src, fl, align=align, merge_slabs=slabs, ref_owner=0)
+        root = run_pipeline(eng, src, fl, align=align, merge_slabs=slabs, ref_owner=0, merge_root=0)
+        torch.cuda.synchronize()
+        got = None if root.rmsf is None else [t.cpu().numpy() for t in (root.rmsf, root.mean, root.m2)]
+        q.put((rank, [t.cpu().numpy() for t in (every.rmsf, every.mean, every.m2)], got,
+               root.extras.get("merge_slabs", 0)))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), None, -1))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("size,n_atoms,align,slabs", [(2, 3000, None, 0), (3, 3000, "frame0", 0),
+                                                      (3, 3000, "average", 0), (2, 300_000, None, 2)])
+def test_merge_to_root(size, n_atoms, align, slabs):
+    """RMSF.py:143's shape: the final merge as a reduce to rank 0.  Rank 0's
+    result equals the all-reduce merge's (same T1/T2 summed; 2 ranks bit for
+    bit, 3 ranks within the collective's summation order); the other ranks
+    get None.  Also through C4's atom slabs (300k atoms)."""
+    from conftest import spawn_ranks
+    n_frames = 40 * size + 1
+    out = spawn_ranks(_root_worker, size, lambda r, init, q: (r, size, init, q, n_atoms, n_frames, align, slabs),
+                      timeout=200)
+    for rank, every, got, k in sorted(out, key=lambda o: o[0]):
+        assert isinstance(every, list), every
+        assert k == slabs
+        if rank != 0:
+            assert got is None
+            continue
+        for a, b in zip(every, got):
+            if size == 2:
+                np.testing.assert_array_equal(a, b)
+            else:
+                np.testing.assert_allclose(a, b, rtol=1e-13, atol=1e-13)
