@@ -3,7 +3,8 @@
 test): P = 2..4 gloo ranks sharing the GPU, random atoms / selection /
 frames / alignment / batch size, and merge slabs forced on where the flat
 plan allows them -- each rank's RMSF against the oracle's mpirun -n P
-emulation of RMSF.py.  python tools/fuzz_multirank.py [n_cases]"""
+emulation of RMSF.py.  ``--root``: half the cases merge with a reduce to a
+random rank (merge_root).  python tools/fuzz_multirank.py [n_cases [--root]]"""
 import os
 import sys
 import tempfile
@@ -34,9 +35,10 @@ def _worker(rank, size, init, q, case):
         mt = motion_table(case["mseed"], nf) if align else None
         shard = generate(eng, na, b0, max(b1 - b0, 1), seed=case["seed"], motion=mt)[: b1 - b0]
         src = DeviceSource(shard, sel, offset=b0, n_traj=nf)
-        res = run_pipeline(eng, src, FrameList(nf), align=align, max_batch=batch, merge_slabs=slabs)
+        res = run_pipeline(eng, src, FrameList(nf), align=align, max_batch=batch, merge_slabs=slabs,
+                           merge_root=case.get("root"))
         torch.cuda.synchronize()
-        q.put((rank, res.rmsf.cpu().numpy(), res.extras.get("merge_slabs", 0)))
+        q.put((rank, None if res.rmsf is None else res.rmsf.cpu().numpy(), res.extras.get("merge_slabs", 0)))
     except Exception as e:  # noqa: BLE001
         q.put((rank, repr(e), -1))
     finally:
@@ -83,6 +85,8 @@ def main():
         slabs = int(rng.integers(2, 5)) if big else None
         case = dict(P=P, na=na, nf=nf, align=align, sel=sel, batch=batch, slabs=slabs,
                     seed=int(rng.integers(0, 1000)), mseed=int(rng.integers(0, 1000)))
+        if len(sys.argv) > 2 and sys.argv[2] == "--root" and rng.random() < 0.5:
+            case["root"] = int(rng.integers(0, P))  # the merge as a reduce to this rank (RMSF.py:143)
         out = run_case(case)
         if any(o[2] == -1 for o in out):
             print(f"case {k}: FAILED {[o[1] for o in out if o[2] == -1][:1]}", flush=True)
@@ -92,10 +96,13 @@ def main():
         cols = np.arange(na) if sel is None else sel
         exp = (O.rmsf_script(traj, cols, None, size=P, align=align)["rmsf"] if not big
                else O.rmsf_two_pass(traj[:, cols]))
-        d = max(float(np.abs(o[1] - exp).max()) for o in out)
+        root = case.get("root")
+        if root is not None:  # only the root has a result
+            assert all((o[1] is None) == (o[0] != root) for o in out), "reduce-to-root results on the wrong ranks"
+        d = max(float(np.abs(o[1] - exp).max()) for o in out if o[1] is not None)
         worst = max(worst, d)
         print(f"case {k:2d}: P={P} {na:7d} atoms {len(cols):7d} sel {nf:4d} frames align={align} "
-              f"batch={batch} slabs={out[0][2]} max|d|={d:.2e}", flush=True)
+              f"batch={batch} slabs={out[0][2]} root={root} max|d|={d:.2e}", flush=True)
         if d > 1e-6:
             print("EXCEEDS 1e-6", flush=True)
             sys.exit(1)
