@@ -260,6 +260,18 @@ int rmsf_gather_frames(const float *d_src, int64_t frame_stride,
                        const int64_t *d_frames, int64_t n_frames, int64_t n_sel,
                        const int32_t *d_sel, float *d_dst, void *stream);
 
+/* The same compact batch from HBM-resident frames stored as coordinate
+ * planes (SoA): frame k's x[n_atoms], y and z at d_src + d_frames[k] *
+ * frame_stride + {0, 1, 2} * plane_stride floats (frame_stride >=
+ * 3 * plane_stride).  The selection is gathered from each plane and
+ * interleaved into d_dst's [n_frames][n_sel][3] rows for the kernels above
+ * (an extra read and write of the selected bytes: a convenience path for
+ * data that already lives in HBM as planes).                               */
+int rmsf_gather_planes(const float *d_src, int64_t frame_stride,
+                       int64_t plane_stride, const int64_t *d_frames,
+                       int64_t n_frames, int64_t n_sel, const int32_t *d_sel,
+                       float *d_dst, void *stream);
+
 /* ---- synthetic trajectories -------------------------------
  * out[f*frame_stride + 3*a + c] for frames [f0, f0+nf) of n_atoms atoms:
  *   base(a,c) ~ U[0,100), sigma(a) ~ U[0.2,2.0), g ~ triangular, unit var,

@@ -1316,6 +1316,26 @@ __global__ __launch_bounds__(kBlock) void k_gather_frames(const float *__restric
   dst[k * 3 * n_sel + i] = __builtin_nontemporal_load(fr + (GATHER ? 3 * (int64_t)sel[a] + c : i));
 }
 
+// k_gather_planes: the same compact batch from frames stored as coordinate
+// planes (SoA: x[n], y[n], z[n] at plane_stride floats apart, HBM-resident):
+// one selected atom per thread, its three plane values (consecutive lanes
+// read consecutive -- or gathered -- atoms of each plane) interleaved into
+// dst's (frame, atom, xyz) rows.  grid = (atom blocks, frames).
+template <bool GATHER>
+__global__ __launch_bounds__(kBlock) void k_gather_planes(const float *__restrict__ src, int64_t fstride,
+                                                          int64_t pstride, const int64_t *__restrict__ frames,
+                                                          int64_t n_sel, const int32_t *__restrict__ sel,
+                                                          float *__restrict__ dst) {
+  const int64_t a = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (a >= n_sel) return;
+  const int64_t k = blockIdx.y;
+  const float *fr = src + frames[k] * fstride + (GATHER ? (int64_t)sel[a] : a);
+  float *o = dst + k * 3 * n_sel + 3 * a;
+  o[0] = __builtin_nontemporal_load(fr);
+  o[1] = __builtin_nontemporal_load(fr + pstride);
+  o[2] = __builtin_nontemporal_load(fr + 2 * pstride);
+}
+
 __global__ __launch_bounds__(kBlock) void k_synth(float *__restrict__ out, int64_t fstride, int64_t n_atoms,
                                                   int64_t f0, int64_t nf, uint64_t seed,
                                                   const double *__restrict__ motion) {
@@ -1985,6 +2005,24 @@ RMSF_EXPORT int rmsf_gather_frames(const float *d_src, int64_t fstride, const in
     hipLaunchKernelGGL(k_gather_frames<false>, grid, dim3(kBlock), 0, S(stream), d_src, fstride, d_frames, n_sel,
                        d_sel, d_dst);
   return after_launch("k_gather_frames");
+}
+
+RMSF_EXPORT int rmsf_gather_planes(const float *d_src, int64_t fstride, int64_t pstride, const int64_t *d_frames,
+                                   int64_t n_frames, int64_t n_sel, const int32_t *d_sel, float *d_dst,
+                                   void *stream) {
+  if (!d_src || !d_frames || !d_dst || n_frames < 0 || n_sel < 1 || pstride < (d_sel ? 1 : n_sel) ||
+      fstride < 3 * pstride)
+    return fail(RMSF_EINVAL, "rmsf_gather_planes: bad arguments");
+  if (n_frames == 0) return RMSF_OK;
+  if (n_frames > 65535) return fail(RMSF_EINVAL, "rmsf_gather_planes: at most 65535 frames per call");
+  const dim3 grid((unsigned)grid1(n_sel), (unsigned)n_frames);
+  if (d_sel)
+    hipLaunchKernelGGL(k_gather_planes<true>, grid, dim3(kBlock), 0, S(stream), d_src, fstride, pstride, d_frames,
+                       n_sel, d_sel, d_dst);
+  else
+    hipLaunchKernelGGL(k_gather_planes<false>, grid, dim3(kBlock), 0, S(stream), d_src, fstride, pstride, d_frames,
+                       n_sel, d_sel, d_dst);
+  return after_launch("k_gather_planes");
 }
 
 RMSF_EXPORT int rmsf_synth_frames(float *d_out, int64_t fstride, int64_t n_atoms, int64_t f0, int64_t nf,

@@ -344,6 +344,8 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
                          "(one process per GPU) leave it unset")
     if collect_rmsd and align is None:
         raise ValueError("collect_rmsd needs an aligned run (align='frame0' or 'average')")
+    if layout == "soa" and not isinstance(inp, np.ndarray):
+        raise NotImplementedError("gpus=: SoA input is supported for host numpy arrays [F, 3, n_atoms]")
     src = _frames_of(inp, select, batch_frames, layout)
     fl = FrameList(src.n_traj, start, stop, step, frames=frames)
     if len(fl) == 0:

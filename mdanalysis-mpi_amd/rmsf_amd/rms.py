@@ -71,10 +71,11 @@ class RMSF:
     ref_frame : int
         Trajectory frame of the first reference (RMSF.py:63).
     layout : "fac" | "soa"
-        Host array inputs only: "fac" = [F, n_atoms, 3] (MDAnalysis'
-        positions per frame), "soa" = [F, 3, n_atoms] (x, y and z coordinate
-        planes per frame; the stager interleaves the selection on the host,
-        the device path is unchanged).
+        Array inputs: "fac" = [F, n_atoms, 3] (MDAnalysis' positions per
+        frame), "soa" = [F, 3, n_atoms] (x, y and z coordinate planes per
+        frame).  Host planes are interleaved by the stager on the host (the
+        device path is unchanged); HBM-resident planes are gathered into
+        (frame, atom, xyz) batches on the device (rmsf_gather_planes).
     merge_root : int, optional
         Under ``torch.distributed``: merge the ranks' statistics with a
         reduce to this rank only, as RMSF.py:143 (``comm.reduce(root=0)``)
@@ -96,8 +97,8 @@ class RMSF:
                  collect_transforms: bool = False, layout: str = "fac", merge_root: int | None = None, **kwargs):
         if layout not in ("fac", "soa"):
             raise ValueError(f"layout must be 'fac' or 'soa', got {layout!r}")
-        if layout == "soa" and not isinstance(atomgroup, np.ndarray):
-            raise ValueError("layout='soa' describes a host numpy array [F, 3, n_atoms]; HBM tensors, files and "
+        if layout == "soa" and not (isinstance(atomgroup, np.ndarray) or isinstance(atomgroup, torch.Tensor)):
+            raise ValueError("layout='soa' describes a numpy array or HIP tensor [F, 3, n_atoms]; files and "
                              "AtomGroups have their own layout")
         self.layout = layout
         self.merge_root = merge_root
@@ -185,7 +186,7 @@ class RMSF:
             if x.device.type != "cuda":
                 x = x.detach().cpu().numpy()
             else:
-                return DeviceSource(x, self.select), self.masses
+                return DeviceSource(x, self.select, layout=self.layout), self.masses
         # RMSF.py's two sweeps (align="average") read every frame twice
         # (RMSF.py:92,124): host sources then keep the staged frames in HBM
         two = self.align == "average"

@@ -215,6 +215,21 @@ class _Gather:
         return Batch(self.buf.data_ptr(), 3 * self.n_sel, len(rows), None)
 
 
+class _GatherPlanes(_Gather):
+    """The same scratch batch filled by rmsf_gather_planes from HBM-resident
+    coordinate planes (SoA frames)."""
+
+    def __init__(self, n_sel: int, nb: int, device, plane_stride: int):
+        super().__init__(n_sel, nb, device)
+        self.plane_stride = plane_stride
+
+    def __call__(self, base_ptr: int, fstride: int, rows: np.ndarray, sel: torch.Tensor | None, stream: int) -> Batch:
+        idx = torch.as_tensor(np.ascontiguousarray(rows, dtype=np.int64)).to(self.buf.device)
+        call("rmsf_gather_planes", base_ptr, fstride, self.plane_stride, idx.data_ptr(), len(rows), self.n_sel,
+             None if sel is None else sel.data_ptr(), self.buf.data_ptr(), stream)
+        return Batch(self.buf.data_ptr(), 3 * self.n_sel, len(rows), None)
+
+
 def _gather_batch_frames(n_sel: int, nb: int) -> int:
     """Frames per gathered batch: the pipeline's batch, at most ~256 MB of scratch."""
     return max(1, min(nb, 65535, (256 << 20) // max(1, 12 * n_sel)))
@@ -222,18 +237,35 @@ def _gather_batch_frames(n_sel: int, nb: int) -> int:
 
 class DeviceSource:
     """HBM-resident float32 trajectory [F_local, n_atoms, 3] holding global frames
-    [offset, offset + F_local) of a trajectory with ``n_traj`` frames."""
+    [offset, offset + F_local) of a trajectory with ``n_traj`` frames.
 
-    def __init__(self, traj: torch.Tensor, sel=None, offset: int = 0, n_traj: int | None = None):
+    ``layout="soa"``: the tensor is [F_local, 3, n_atoms] coordinate planes
+    (atoms contiguous; frames and planes may be strided).  Each batch is
+    gathered into a compact (frame, atom, xyz) scratch batch by
+    rmsf_gather_planes first -- one extra read and write of the selected
+    bytes, a convenience for frames that already live in HBM as planes."""
+
+    def __init__(self, traj: torch.Tensor, sel=None, offset: int = 0, n_traj: int | None = None,
+                 layout: str = "fac"):
         if traj.dtype != torch.float32 or traj.device.type != "cuda":
             raise TypeError("DeviceSource needs a float32 tensor on a HIP device")
-        if traj.dim() != 3 or traj.shape[2] != 3:
-            raise ValueError("trajectory must be [n_frames, n_atoms, 3]")
-        if traj.stride(2) != 1 or traj.stride(1) != 3:
-            raise ValueError("trajectory frames must be contiguous [n_atoms, 3] rows")
+        if layout not in ("fac", "soa"):
+            raise ValueError(f"layout must be 'fac' ([F, n_atoms, 3]) or 'soa' ([F, 3, n_atoms]), got {layout!r}")
+        self.layout = layout
+        if layout == "soa":
+            if traj.dim() != 3 or traj.shape[1] != 3:
+                raise ValueError("an SoA trajectory must be [n_frames, 3, n_atoms]")
+            if traj.stride(2) != 1 or traj.stride(1) < traj.shape[2] or traj.stride(0) < 3 * traj.stride(1):
+                raise ValueError("SoA frames must hold three contiguous, non-overlapping coordinate planes")
+        else:
+            if traj.dim() != 3 or traj.shape[2] != 3:
+                raise ValueError("trajectory must be [n_frames, n_atoms, 3]")
+            if traj.stride(2) != 1 or traj.stride(1) != 3:
+                raise ValueError("trajectory frames must be contiguous [n_atoms, 3] rows")
         self.traj = traj
-        self.n_atoms = traj.shape[1]
+        self.n_atoms = traj.shape[2] if layout == "soa" else traj.shape[1]
         self.fstride = traj.stride(0)
+        self._planes = self._ref_planes = None
         self.offset = offset
         self.n_traj = traj.shape[0] + offset if n_traj is None else n_traj
         self.sel_host = None if sel is None else np.ascontiguousarray(sel, dtype=np.int64)
@@ -254,13 +286,36 @@ class DeviceSource:
         return self.traj.data_ptr() + (frame - self.offset) * self.fstride * 4
 
     def reference(self, frame: int, stream: int) -> Batch:
+        if self.layout == "soa":  # its own one-frame scratch: may run on a side stream beside a sweep's batches
+            self._ptr(frame)
+            if self._ref_planes is None:
+                self._ref_planes = _GatherPlanes(self.n_sel, 1, self.traj.device, self.traj.stride(1))
+            return self._ref_planes(self.traj.data_ptr(), self.fstride, np.array([frame - self.offset]),
+                                    self.sel_dev, stream)
         return Batch(self._ptr(frame), self.fstride, 1, self.sel_dev)
 
     @property
     def n_rows(self) -> int:
         return self.traj.shape[0]
 
+    def _plane_batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
+        """SoA: every batch (runs or a scattered list) gathered from the planes."""
+        nb = max(1, min(max_frames, 65535, (512 << 20) // max(1, 12 * self.n_sel)))
+        if self._planes is None or self._planes.buf.shape[0] < nb:
+            self._planes = _GatherPlanes(self.n_sel, nb, self.traj.device, self.traj.stride(1))
+        rows = frames.idx[b0:b1] if frames.idx is not None else np.arange(b0, b1, dtype=np.int64)
+        if frames.idx is None and b1 > b0:
+            rows = frames.r.start + frames.r.step * rows  # positions -> frame numbers
+        for i in range(0, len(rows), nb):
+            part = rows[i:i + nb]
+            _check_run(self, int(part[0]), 1, 1, "HBM shard")
+            _check_run(self, int(part[-1]), 1, 1, "HBM shard")
+            yield self._planes(self.traj.data_ptr(), self.fstride, part - self.offset, self.sel_dev, stream)
+
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
+        if self.layout == "soa":
+            yield from self._plane_batches(frames, b0, b1, max_frames, stream)
+            return
         if _scattered(frames, b0, b1, max_frames):
             nb = _gather_batch_frames(self.n_sel, max_frames)
             g = _Gather(self.n_sel, nb, self.traj.device)

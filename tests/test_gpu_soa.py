@@ -132,7 +132,44 @@ def test_soa_bad_inputs(c1):
     d, traj = c1
     with pytest.raises(ValueError, match="SoA trajectory"):
         RMSF(traj, layout="soa").run()  # [F, n, 3] is not planes
-    with pytest.raises(ValueError, match="layout"):
-        RMSF(torch.zeros(2, 5, 3, device="cuda"), layout="soa")
+    with pytest.raises(ValueError, match="SoA trajectory"):
+        RMSF(torch.zeros(2, 5, 3, device="cuda"), layout="soa").run()
+    with pytest.raises(ValueError, match="non-overlapping"):
+        RMSF(torch.zeros(30, device="cuda").as_strided((2, 3, 5), (15, 2, 1)), layout="soa").run()
     with pytest.raises(ValueError, match="layout"):
         RMSF(traj, layout="aos")
+
+
+@pytest.mark.parametrize("align", [None, "frame0", "average"])
+@pytest.mark.parametrize("pad", [0, 7])
+def test_device_soa_bitwise(c1, align, pad):
+    """HBM-resident planes [F, 3, n] (rmsf_gather_planes into compact
+    batches) against the host row array streamed in batches of the same
+    frames (the stager's compact batches): the same device batches, so the
+    same bits -- for ranges, steps and a scattered frame list."""
+    import torch
+
+    from rmsf_amd import RMSF
+    d, traj = c1
+    dev = torch.tensor(_soa(traj, pad) if not pad else np.ascontiguousarray(
+        np.pad(traj.transpose(0, 2, 1), ((0, 0), (0, 0), (0, pad)))), device="cuda")
+    if pad:
+        dev = dev[:, :, :traj.shape[1]]
+    for bf, run in ((11, {}), (7, {"start": 3, "stop": 90, "step": 2}),
+                    (13, {"frames": np.sort(np.random.default_rng(5).choice(98, 40, replace=False))})):
+        a = RMSF(traj, select=d["sel"], align=align, batch_frames=bf).run(**run)
+        b = RMSF(dev, select=d["sel"], align=align, layout="soa", batch_frames=bf).run(**run)
+        _same(a, b)
+    r = RMSF(dev, select=d["sel"], align=align, layout="soa").run()
+    tag = {None: "none", "frame0": "frame0", "average": "average"}[align]
+    np.testing.assert_allclose(r.results.rmsf, d[f"rmsf_{tag}_P1"], rtol=0, atol=TOL)
+
+
+def test_device_soa_all_atoms():
+    """Every atom (no selection), 50k atoms: the planes gather's identity path."""
+    import torch
+
+    from rmsf_amd import RMSF
+    traj = SY.frames(21, 50_000, 0, 30, None)
+    dev = torch.tensor(_soa(traj), device="cuda")
+    _same(RMSF(traj, batch_frames=9).run(), RMSF(dev, layout="soa", batch_frames=9).run())
