@@ -272,6 +272,14 @@ int rmsf_gather_planes(const float *d_src, int64_t frame_stride,
                        int64_t n_frames, int64_t n_sel, const int32_t *d_sel,
                        float *d_dst, void *stream);
 
+/* Per-coordinate f64 statistics in plane order (x[n], y[n], z[n]) to
+ * (atom, xyz) order, d_dst[3a + c] = d_src[c*n + a] (d_dst != d_src): the
+ * unaligned accumulate reads contiguous coordinate planes in place, as it
+ * reads rows (its statistics are per coordinate), and its mean / M2 come
+ * out in plane order.                                                      */
+int rmsf_planes_to_rows(const double *d_src, int64_t n, double *d_dst,
+                        void *stream);
+
 /* ---- synthetic trajectories -------------------------------
  * out[f*frame_stride + 3*a + c] for frames [f0, f0+nf) of n_atoms atoms:
  *   base(a,c) ~ U[0,100), sigma(a) ~ U[0.2,2.0), g ~ triangular, unit var,

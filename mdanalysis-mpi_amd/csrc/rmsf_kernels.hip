@@ -1336,6 +1336,17 @@ __global__ __launch_bounds__(kBlock) void k_gather_planes(const float *__restric
   o[2] = __builtin_nontemporal_load(fr + 2 * pstride);
 }
 
+// k_planes_to_rows: per-coordinate f64 statistics kept in plane order
+// (x[n], y[n], z[n] -- what the unaligned kernels produce when they read
+// coordinate planes in place) to (atom, xyz) order: dst[3a + c] = src[c n + a].
+__global__ __launch_bounds__(kBlock) void k_planes_to_rows(const double *__restrict__ src, int64_t n,
+                                                           double *__restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // destination index: coalesced stores
+  if (i >= 3 * n) return;
+  const int64_t a = i / 3, c = i - 3 * a;
+  dst[i] = src[c * n + a];
+}
+
 __global__ __launch_bounds__(kBlock) void k_synth(float *__restrict__ out, int64_t fstride, int64_t n_atoms,
                                                   int64_t f0, int64_t nf, uint64_t seed,
                                                   const double *__restrict__ motion) {
@@ -2023,6 +2034,12 @@ RMSF_EXPORT int rmsf_gather_planes(const float *d_src, int64_t fstride, int64_t 
     hipLaunchKernelGGL(k_gather_planes<false>, grid, dim3(kBlock), 0, S(stream), d_src, fstride, pstride, d_frames,
                        n_sel, d_sel, d_dst);
   return after_launch("k_gather_planes");
+}
+
+RMSF_EXPORT int rmsf_planes_to_rows(const double *d_src, int64_t n, double *d_dst, void *stream) {
+  if (!d_src || !d_dst || n < 1 || d_src == d_dst) return fail(RMSF_EINVAL, "rmsf_planes_to_rows: bad arguments");
+  hipLaunchKernelGGL(k_planes_to_rows, dim3(grid1(3 * n)), dim3(kBlock), 0, S(stream), d_src, n, d_dst);
+  return after_launch("k_planes_to_rows");
 }
 
 RMSF_EXPORT int rmsf_synth_frames(float *d_out, int64_t fstride, int64_t n_atoms, int64_t f0, int64_t nf,

@@ -79,6 +79,7 @@ SIGNATURES = {
     "rmsf_synth_frames": (c_int, [P, c_int64, c_int64, c_int64, c_int64, c_uint64, P, P]),
     "rmsf_gather_frames": (c_int, [P, c_int64, P, c_int64, c_int64, P, P, P]),
     "rmsf_gather_planes": (c_int, [P, c_int64, c_int64, P, c_int64, c_int64, P, P, P]),
+    "rmsf_planes_to_rows": (c_int, [P, c_int64, P, P]),
     "rmsf_stager_create": (c_int, [c_int64, c_int64, P, c_int64, c_int, c_int, POINTER(c_void_p)]),
     "rmsf_stager_destroy": (c_int, [P]),
     "rmsf_stager_stage": (c_int, [P, P, c_int64, c_int64, P, POINTER(c_int), POINTER(c_void_p)]),

@@ -190,6 +190,12 @@ class Engine:
         call("rmsf_gather_frames", base_ptr, fstride, rows.data_ptr(), n, n_sel, _ptr(sel), out.data_ptr(),
              self.stream)
 
+    def planes_to_rows(self, x: torch.Tensor, n: int) -> torch.Tensor:
+        """f64 [3n] in plane order (x[n], y[n], z[n]) -> a new [3n] in (atom, xyz) order."""
+        out = self.empty(3 * n)
+        call("rmsf_planes_to_rows", x.data_ptr(), n, out.data_ptr(), self.stream)
+        return out
+
     def finalize(self, m2: torch.Tensor, n_sel: int, n_frames: int, out: torch.Tensor) -> None:
         """RMSF.py:146: sqrt(M2.sum(axis=1)/n)."""
         call("rmsf_finalize", m2.data_ptr(), n_sel, n_frames, out.data_ptr(), self.stream)

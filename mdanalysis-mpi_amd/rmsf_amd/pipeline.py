@@ -242,18 +242,21 @@ def reference_from_frame(eng: Engine, source, frame: int, n_sel: int, masses, ow
     return r, i
 
 
-def _frame_shift(eng: Engine, source, frames: FrameList, n_total: int, size: int, rank: int):
+def _frame_shift(eng: Engine, source, frames: FrameList, n_total: int, size: int, rank: int, raw: bool = False):
     """Frame 0 of the list, selected, as f32 on every rank: gathered by the
     rank whose RMSF.py:65-69 block starts with it and broadcast asynchronously
-    (the broadcast runs beside the sweep; the merge waits for it)."""
+    (the broadcast runs beside the sweep; the merge waits for it).  ``raw``:
+    as stored (coordinate planes read in place stay in plane order)."""
     from .sources import DeviceSource
+
+    ref_of = source.raw_reference if raw else source.reference
 
     owner = next(r for r, (a, b) in enumerate(parallel.blocks(n_total, size)) if b > a)
     buf = torch.empty(3 * source.n_sel, dtype=torch.float32, device=eng.device)
     idx = eng.zero_index()
     if not isinstance(source, DeviceSource):  # staged / decoded on the launching stream
         if rank == owner:
-            b = source.reference(frames[0], eng.stream)
+            b = ref_of(frames[0], eng.stream)
             eng.gather_frames(b.ptr, b.fstride, idx, 1, source.n_sel, b.sel, buf)
             b.done()
         return buf, parallel.broadcast_async(buf, owner)
@@ -264,7 +267,7 @@ def _frame_shift(eng: Engine, source, frames: FrameList, n_total: int, size: int
     side.wait_stream(main)
     with torch.cuda.stream(side):
         if rank == owner:
-            b = source.reference(frames[0], eng.stream)
+            b = ref_of(frames[0], eng.stream)
             eng.gather_frames(b.ptr, b.fstride, idx, 1, source.n_sel, b.sel, buf)
             b.done()
         work = parallel.broadcast_async(buf, owner)
@@ -314,6 +317,15 @@ def _slab_sweep(eng: Engine, acc: "Accumulator", b: Batch, slabs: list, shift, o
     return out
 
 
+def _rows_from_planes(eng: Engine, mean, m2, n_sel: int, n_total: int):
+    """Plane-order statistics (coordinate planes read in place) to (atom, xyz)
+    order, and the RMSF of RMSF.py:146 from them."""
+    mean, m2 = eng.planes_to_rows(mean, n_sel), eng.planes_to_rows(m2, n_sel)
+    rmsf = eng.empty(n_sel)
+    eng.finalize(m2, n_sel, n_total, rmsf)
+    return mean, m2, rmsf
+
+
 def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=None, ref_frame: int = 0,
                  max_batch: int | None = None, n_splits: int | None = None, collect_rmsd: bool = False,
                  ref_owner: int | None = None, block: tuple[int, int] | None = None,
@@ -352,6 +364,10 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
         if m_dev.numel() != n_sel:
             raise ValueError("masses must have one entry per selected atom")
     aligned = align is not None
+    # coordinate planes read in place by the unaligned accumulate: statistics
+    # in plane order, permuted to (atom, xyz) at the end
+    planes = not aligned and not n_splits and bool(getattr(source, "native_planes", False))
+    batches_of = source.raw_batches if planes else source.batches
     sup = Superposer(eng, n_sel, max_batch, m_dev, timer) if aligned else None
     rmsd = eng.empty(n_local) if (aligned and collect_rmsd) else None
     keep = aligned and collect_transforms
@@ -361,7 +377,7 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
 
     def sweep(acc: Accumulator, ref=None, info=None, xf_out=None, pack=None, slabs=None):
         done, slabbed = 0, None
-        for b in source.batches(frames, b0, b1, max_batch, eng.stream):
+        for b in batches_of(frames, b0, b1, max_batch, eng.stream):
             xf = None
             if aligned:
                 xf = sup.run(b, ref, info)
@@ -407,7 +423,7 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
         elif align == "frame0":
             shift, off3 = ref, info[:3]
         else:
-            shift, shift_work = _frame_shift(eng, source, frames, n_total, size, rank)
+            shift, shift_work = _frame_shift(eng, source, frames, n_total, size, rank, raw=planes)
 
     acc = Accumulator(eng, n_sel, RMSF_MODE_WELFORD, max_batch, aligned, n_splits, timer)
     # N > 1: the last batch's fold also packs the merge's moments (one launch);
@@ -431,6 +447,8 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                 work.wait()
             eng.chan_shift_finish(t_k, shift[j0:j1], off3, (j1 - j0) // 3, n_total, mean[j0:j1], m2[j0:j1],
                                   rmsf[j0 // 3:j1 // 3])
+        if planes:
+            mean, m2, rmsf = _rows_from_planes(eng, mean, m2, n_sel, n_total)
         return PipelineResult(rmsf=rmsf, mean=mean.view(n_sel, 3), m2=m2.view(n_sel, 3), n_frames=n_total,
                               n_local=n_local, block=(b0, b1), average=None, rmsd=rmsd,
                               extras={"merge_slabs": len(slabbed), "merge_root": root})
@@ -438,11 +456,15 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
         mean, m2, rmsf = parallel.global_chan_shifted(eng, acc.result0, acc.result1, acc.n, n_total,
                                                       shift, off3, None if acc.packed else shift_work,
                                                       packed=t if acc.packed else None, root=root)
+        if planes and rmsf is not None:
+            mean, m2, rmsf = _rows_from_planes(eng, mean, m2, n_sel, n_total)
         if rmsf is None:                                     # a non-root rank of the reduce
             return PipelineResult(rmsf=None, mean=None, m2=None, n_frames=n_total, n_local=n_local,
                                   block=(b0, b1), average=None if average is None else average.view(n_sel, 3),
                                   rmsd=rmsd, transforms=xf_last, transforms_sweep1=xf_first,
                                   extras={"merge_root": root})
+    elif planes:
+        mean, m2, rmsf = _rows_from_planes(eng, acc.result0, acc.result1, n_sel, n_total)
     else:
         mean, m2 = acc.result0, acc.result1
         rmsf = eng.empty(n_sel)

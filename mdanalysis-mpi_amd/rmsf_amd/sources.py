@@ -312,10 +312,27 @@ class DeviceSource:
             _check_run(self, int(part[-1]), 1, 1, "HBM shard")
             yield self._planes(self.traj.data_ptr(), self.fstride, part - self.offset, self.sel_dev, stream)
 
+    @property
+    def native_planes(self) -> bool:
+        """SoA frames the unaligned accumulate reads in place, as if they were
+        rows (its statistics are per coordinate; they come out in plane
+        order): three contiguous planes, no selection, float4-aligned."""
+        return (self.layout == "soa" and self.sel_dev is None and self.traj.stride(1) == self.n_atoms
+                and (3 * self.n_atoms) % 4 == 0 and self.fstride % 4 == 0 and self.traj.data_ptr() % 16 == 0)
+
+    def raw_reference(self, frame: int, stream: int) -> Batch:
+        """Frame ``frame`` as stored (planes stay planes)."""
+        return Batch(self._ptr(frame), self.fstride, 1, self.sel_dev)
+
     def batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
         if self.layout == "soa":
             yield from self._plane_batches(frames, b0, b1, max_frames, stream)
             return
+        yield from self.raw_batches(frames, b0, b1, max_frames, stream)
+
+    def raw_batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
+        """Batches of the frames as stored: rows read in place (or gathered
+        for a scattered list); for native_planes SoA frames, 3 n floats each."""
         if _scattered(frames, b0, b1, max_frames):
             nb = _gather_batch_frames(self.n_sel, max_frames)
             g = _Gather(self.n_sel, nb, self.traj.device)

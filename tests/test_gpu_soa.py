@@ -166,10 +166,87 @@ def test_device_soa_bitwise(c1, align, pad):
 
 
 def test_device_soa_all_atoms():
-    """Every atom (no selection), 50k atoms: the planes gather's identity path."""
+    """Every atom (no selection), 50,001 atoms (3 n not a multiple of 4, so
+    not read in place): the planes gather's identity path, bitwise."""
     import torch
 
     from rmsf_amd import RMSF
-    traj = SY.frames(21, 50_000, 0, 30, None)
+    traj = SY.frames(21, 50_001, 0, 30, None)
     dev = torch.tensor(_soa(traj), device="cuda")
     _same(RMSF(traj, batch_frames=9).run(), RMSF(dev, layout="soa", batch_frames=9).run())
+
+
+@pytest.mark.parametrize("n_atoms", [4000, 3001])
+def test_device_planes_in_place(n_atoms):
+    """Unaligned runs over contiguous planes with no selection read the planes
+    in place (per-coordinate statistics in plane order, permuted to (atom,
+    xyz) at the end): the rows path's results within f64 rounding (the
+    coordinates sit in different chunks, so the folds round differently),
+    for the whole list, a step and a scattered list.  n_atoms = 3001 makes
+    3 n odd of 4: the gather path, bitwise."""
+    import torch
+
+    from rmsf_amd import RMSF
+    from rmsf_amd.sources import DeviceSource
+    traj = SY.frames(17, n_atoms, 0, 70, None)
+    dev = torch.tensor(_soa(traj), device="cuda")
+    assert DeviceSource(dev, layout="soa").native_planes == (n_atoms % 4 == 0)
+    for run in ({}, {"start": 1, "stop": 69, "step": 3},
+                {"frames": np.sort(np.random.default_rng(8).choice(70, 25, replace=False))}):
+        a = RMSF(traj).run(**run)
+        b = RMSF(dev, layout="soa").run(**run)
+        for k in ("rmsf", "mean", "sumsquares"):
+            np.testing.assert_allclose(a.results[k], b.results[k], rtol=1e-13, atol=1e-13)
+
+
+def _planes_rank_worker(rank, size, init, q, n_atoms, n_frames, root):
+    import sys
+
+    from conftest import PKG, ROOT
+    sys.path[:0] = [ROOT, PKG]
+    import torch
+    import torch.distributed as dist
+
+    from conftest import init_gloo
+    init_gloo(init, rank, size)
+    try:
+        from rmsf_amd import parallel
+        from rmsf_amd.engine import Engine
+        from rmsf_amd.pipeline import run_pipeline
+        from rmsf_amd.sources import DeviceSource, FrameList
+        from rmsf_amd.synth import generate
+        eng = Engine(torch.device("cuda", 0))
+        b0, b1 = parallel.blocks(n_frames, size)[rank]
+        planes = generate(eng, n_atoms, b0, b1 - b0, seed=19).transpose(1, 2).contiguous()
+        src = DeviceSource(planes, offset=b0, n_traj=n_frames, layout="soa")
+        assert src.native_planes
+        res = run_pipeline(eng, src, FrameList(n_frames), merge_root=root)
+        torch.cuda.synchronize()
+        q.put((rank, None if res.rmsf is None else res.rmsf.cpu().numpy(), res.extras.get("merge_slabs", 0)))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), -1))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("size,n_atoms,root", [(2, 4000, None), (3, 4000, 0), (2, 1_000_000, None)])
+def test_device_planes_in_place_ranks(size, n_atoms, root):
+    """The same over gloo ranks sharing the GPU: the merge's shift (frame 0 of
+    the list, broadcast) stays in plane order with the statistics; 1M atoms:
+    the merge in atom slabs.  Against a two-pass variance of the regenerated
+    frames on sampled atoms."""
+    from conftest import spawn_ranks
+    n_frames = 20 * size + 3
+    out = spawn_ranks(_planes_rank_worker, size, lambda r, init, q: (r, size, init, q, n_atoms, n_frames, root),
+                      timeout=200)
+    atoms = np.sort(np.random.default_rng(2).choice(n_atoms, 64, replace=False))
+    host = SY.frames(19, n_atoms, 0, n_frames, atoms=atoms).astype(np.float64)
+    exp = np.sqrt(((host - host.mean(0)) ** 2).sum(0).sum(1) / n_frames)
+    for rank, rmsf, k in out:
+        assert k != -1, rmsf
+        if root is not None and rank != root:
+            assert rmsf is None
+            continue
+        np.testing.assert_allclose(rmsf[atoms], exp, rtol=0, atol=1e-9)
+        if n_atoms >= 1_000_000:
+            assert k == 2
