@@ -103,6 +103,17 @@ int rmsf_superpose(const float *d_xyz, int64_t frame_stride, int64_t n_frames,
                    const double *d_refinfo, double *d_xform, void *d_work,
                    size_t work_bytes, void *stream);
 
+/* The same for frames stored as coordinate planes (SoA): atom a's x, y and
+ * z of frame f at d_xyz + f*frame_stride + a (or d_sel[a]) + {0, 1, 2} *
+ * plane_stride floats (frame_stride >= 3*plane_stride).  Same workspace,
+ * same records, same arithmetic: the planes are read in place.           */
+int rmsf_superpose_planes(const float *d_xyz, int64_t frame_stride,
+                          int64_t plane_stride, int64_t n_frames,
+                          int64_t n_sel, const int32_t *d_sel,
+                          const double *d_masses, const double *d_ref,
+                          const double *d_refinfo, double *d_xform,
+                          void *d_work, size_t work_bytes, void *stream);
+
 /* ---- streaming accumulator: RMSF.py:99-103 (SUM) and RMSF.py:133-138 (WELFORD)
  * For each frame: if d_xform != NULL apply the f32-faithful transform of
  * RMSF.py:99-101 / 133-135
@@ -149,6 +160,18 @@ int rmsf_accumulate_balanced(const float *d_xyz, int64_t frame_stride,
 int rmsf_fold_balanced(const void *d_work, int64_t n_coord, int mode,
                        int64_t acc_n, double *d_acc0, double *d_acc1,
                        void *stream);
+/* The aligned accumulate (d_xform required: RMSF.py:99-103 / 133-138) over
+ * frames stored as coordinate planes (see rmsf_superpose_planes), read in
+ * place; partials, header and fold as rmsf_accumulate_balanced's.  (The
+ * unaligned sweep reads contiguous planes as rows of 3n floats and permutes
+ * its statistics with rmsf_planes_to_rows.)                                 */
+int rmsf_accumulate_balanced_planes(const float *d_xyz, int64_t frame_stride,
+                                    int64_t plane_stride, int64_t n_frames,
+                                    int64_t n_sel, const int32_t *d_sel,
+                                    const double *d_xform,
+                                    const double *d_refinfo, int mode,
+                                    int n_groups, void *d_work,
+                                    size_t work_bytes, void *stream);
 
 /* ---- Chan merge: second_order_moments, RMSF.py:36-41 ------------------------
  * Folds n_parts partial (count, mean, M2) sets of n_coord coordinates, in

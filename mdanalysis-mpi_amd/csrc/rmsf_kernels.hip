@@ -441,10 +441,11 @@ __global__ __launch_bounds__(kBlock) void k_accum_atoms_sk(const float *__restri
 // accum_span: frames [0, nf) from p (one selected atom per lane), adding to
 // m/q: WELFORD shifted sums (S1 += d, S2 += d^2, d = x - sh), SUM plain sums.
 // xf = frame 0's transform record.
-template <int MODE, bool ALIGN, int U>
+template <int MODE, bool ALIGN, int U, bool PLANES = false>
 __device__ __forceinline__ void accum_span(const float *__restrict__ p, int64_t fstride, int nf,
                                            const double *__restrict__ xf, double rc0, double rc1, double rc2,
-                                           const double (&sh)[3], double (&m)[3], double (&q)[3]) {
+                                           const double (&sh)[3], double (&m)[3], double (&q)[3], int64_t ps = 0) {
+  const int64_t cs = PLANES ? ps : 1;  // x -> y -> z of the lane's atom
   auto consume = [&](float x, float y, float z, int k) {
     if (ALIGN) apply_xform(x, y, z, xf + (int64_t)k * kXform, rc0, rc1, rc2);
     if (MODE == RMSF_MODE_WELFORD) {
@@ -462,15 +463,15 @@ __device__ __forceinline__ void accum_span(const float *__restrict__ p, int64_t 
     for (int u = 0; u < U; ++u) {
       const float *r = p + (int64_t)(k + u) * fstride;
       vx[u] = __builtin_nontemporal_load(r);
-      vy[u] = __builtin_nontemporal_load(r + 1);
-      vz[u] = __builtin_nontemporal_load(r + 2);
+      vy[u] = __builtin_nontemporal_load(r + cs);
+      vz[u] = __builtin_nontemporal_load(r + 2 * cs);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) consume(vx[u], vy[u], vz[u], k + u);
   }
   for (; k < nf; ++k) {
     const float *r = p + (int64_t)k * fstride;
-    consume(r[0], r[1], r[2], k);
+    consume(r[0], r[cs], r[2 * cs], k);
   }
 }
 
@@ -483,14 +484,14 @@ __device__ __forceinline__ void accum_span(const float *__restrict__ p, int64_t 
 // partial per segment.  Q x fewer partials at the same wave count: at 8,192
 // ranges x 2 segments the partials are 196 MB per launch, which the fold
 // reads back -- 6 % of a 2,500-frame share (tools/ubench_accum3.hip).
-template <int MODE, bool ALIGN, bool GATHER, int U, int Q>
+template <int MODE, bool ALIGN, bool GATHER, int U, int Q, bool PLANES = false>
 __global__ __launch_bounds__(kBlock *Q) void k_accum_split_sk(const float *__restrict__ xyz, int64_t fstride,
                                                               const int32_t *__restrict__ sel,
                                                               const double *__restrict__ xform,
                                                               const double *__restrict__ refinfo, SkPlan pl,
                                                               int64_t *__restrict__ hdr,
                                                               double *__restrict__ parts0,
-                                                              double *__restrict__ parts1) {
+                                                              double *__restrict__ parts1, int64_t ps = 0) {
   static_assert(Q > 1 && RMSF_SHIFTED_SUMS, "k_accum_split_sk combines shifted sums of Q > 1 sub-blocks");
   constexpr int NV = MODE == RMSF_MODE_WELFORD ? 6 : 3;  // doubles per lane handed over
   __shared__ double red[(Q - 1) * NV * kBlock];
@@ -512,14 +513,15 @@ __global__ __launch_bounds__(kBlock *Q) void k_accum_split_sk(const float *__res
     const int s0 = (int)((int64_t)len * qd / Q), s1 = (int)((int64_t)len * (qd + 1) / Q);
     double m[3] = {0.0, 0.0, 0.0}, q[3] = {0.0, 0.0, 0.0}, sh[3] = {0.0, 0.0, 0.0};
     if (live) {
-      const float *p = xyz + f0 * fstride + (GATHER ? 3 * (int64_t)sel[a] : 3 * a);
+      const float *p = xyz + f0 * fstride + (PLANES ? 1 : 3) * (GATHER ? (int64_t)sel[a] : a);
       if (MODE == RMSF_MODE_WELFORD) {
-        float x = p[0], y = p[1], z = p[2];
+        const int64_t cs = PLANES ? ps : 1;
+        float x = p[0], y = p[cs], z = p[2 * cs];
         if (ALIGN) apply_xform(x, y, z, xform + f0 * kXform, rc0, rc1, rc2);
         sh[0] = (double)x, sh[1] = (double)y, sh[2] = (double)z;
       }
-      accum_span<MODE, ALIGN, U>(p + (int64_t)s0 * fstride, fstride, s1 - s0,
-                                 ALIGN ? xform + (f0 + s0) * kXform : nullptr, rc0, rc1, rc2, sh, m, q);
+      accum_span<MODE, ALIGN, U, PLANES>(p + (int64_t)s0 * fstride, fstride, s1 - s0,
+                                         ALIGN ? xform + (f0 + s0) * kXform : nullptr, rc0, rc1, rc2, sh, m, q, ps);
     }
     if (qd > 0) {
 #pragma unroll
@@ -769,16 +771,22 @@ struct StatsPlan {
 
 __host__ __device__ inline int64_t st_lo(const StatsPlan &p, int64_t b) { return p.T * b / p.G; }
 
-template <bool GATHER, bool MASSES, bool VEC4, int WPE = 1>
+// PLANES: frames stored as coordinate planes (x[n], y[n], z[n], ps floats
+// apart; SoA).  The element path gathers each atom's three plane values into
+// the same (atom, xyz) tile rows; the VEC4 path stages each tile row as
+// [x(32) | y(32) | z(32)] (three 128-B plane segments per frame, the same
+// 24 float4 per row) and its 4-atom groups read one float4 of each plane.
+template <bool GATHER, bool MASSES, bool VEC4, int WPE = 1, bool PLANES = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_frame_stats(
     const float *__restrict__ xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
     const int32_t *__restrict__ sel, const double *__restrict__ masses, const double *__restrict__ ref,
-    StatsPlan pl, double *__restrict__ part) {
+    StatsPlan pl, double *__restrict__ part, int64_t ps = 0) {
   __shared__ __attribute__((aligned(16))) float tile[kStatsLds];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t last = n_frames - 1;
-  const int64_t o0 = GATHER ? 3 * (int64_t)sel[0] : 0;
+  const int64_t o0 = GATHER ? (PLANES ? 1 : 3) * (int64_t)sel[0] : 0;
+  const int64_t cs = PLANES ? ps : 1;  // x -> y -> z of one atom
   const int64_t lim = 3 * n_sel;  // floats of the selection inside a frame row (VEC4)
   int64_t lo = uni64(st_lo(pl, blockIdx.x));
   const int64_t hi = uni64(st_lo(pl, blockIdx.x + 1));
@@ -790,7 +798,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     const int64_t f0 = g * kTF;
     const int64_t a_beg = t_lo * kTA, a_end = min(n_sel, t_hi * kTA);
     const float *myfr = xyz + min(f0 + lane, last) * fstride;
-    const double px = myfr[o0], py = myfr[o0 + 1], pz = myfr[o0 + 2];
+    const double px = myfr[o0], py = myfr[o0 + cs], pz = myfr[o0 + 2 * cs];
     double acc[kStats];
 #pragma unroll
     for (int j = 0; j < kStats; ++j) acc[j] = 0.0;
@@ -804,6 +812,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
           const int idx = threadIdx.x + k * kBlock;
           const int row = idx / kRow4, col = idx % kRow4;
           const float *src = xyz + min(f0 + row, last) * fstride;
+          if (PLANES) {  // col 0-7: x plane, 8-15: y, 16-23: z; 4 atoms each
+            const int64_t a = t0 + 4 * (col % 8);
+            const float *q = src + (col / 8) * ps + a;
+            if (a + 3 < n_sel) {
+              pre[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(q));
+            } else {  // selection tail
+              pre[k] = f32x4{a < n_sel ? q[0] : 0.f, a + 1 < n_sel ? q[1] : 0.f, a + 2 < n_sel ? q[2] : 0.f, 0.f};
+            }
+            continue;
+          }
           const int64_t e = 3 * t0 + 4 * col;
           if (e + 3 < lim) {
             pre[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(src + e));
@@ -819,10 +837,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
           const int64_t a = t0 + j;
           const float *src = xyz + min(f0 + row, last) * fstride;
           if (a < a_end) {
-            const int64_t off = GATHER ? 3 * (int64_t)sel[a] : 3 * a;
+            const int64_t off = (PLANES ? 1 : 3) * (GATHER ? (int64_t)sel[a] : a);
             pel[3 * k] = __builtin_nontemporal_load(src + off);
-            pel[3 * k + 1] = __builtin_nontemporal_load(src + off + 1);
-            pel[3 * k + 2] = __builtin_nontemporal_load(src + off + 2);
+            pel[3 * k + 1] = __builtin_nontemporal_load(src + off + cs);
+            pel[3 * k + 2] = __builtin_nontemporal_load(src + off + 2 * cs);
           } else {
             pel[3 * k] = pel[3 * k + 1] = pel[3 * k + 2] = 0.f;
           }
@@ -851,8 +869,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     };
     // one 4-atom group of this wave's slab (atoms a4..a4+3, a wave-uniform index)
     auto group = [&](const f32x4 *my, int gi, int64_t a4, int n_at) {
-      const f32x4 q0 = my[3 * gi], q1 = my[3 * gi + 1], q2 = my[3 * gi + 2];
-      const float c[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+      float c[12];
+      if (PLANES && VEC4) {  // my = the row; this wave's group gi = float4 (2w + gi) of each plane segment
+        const f32x4 qx = my[2 * w + gi], qy = my[8 + 2 * w + gi], qz = my[16 + 2 * w + gi];
+        const float cp[12] = {qx.x, qy.x, qz.x, qx.y, qy.y, qz.y, qx.z, qy.z, qz.z, qx.w, qy.w, qz.w};
+#pragma unroll
+        for (int j = 0; j < 12; ++j) c[j] = cp[j];
+      } else {
+        const f32x4 q0 = my[3 * gi], q1 = my[3 * gi + 1], q2 = my[3 * gi + 2];
+        const float cr[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+#pragma unroll
+        for (int j = 0; j < 12; ++j) c[j] = cr[j];
+      }
       const double *rr = ref + 3 * a4;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -887,7 +915,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       lstore();
       __syncthreads();
       if (t0 + kTA < a_end) gload(t0 + kTA);
-      const f32x4 *my = reinterpret_cast<const f32x4 *>(tile + lane * kPitch + w * 3 * kAPW);
+      const f32x4 *my = reinterpret_cast<const f32x4 *>(tile + lane * kPitch + (PLANES && VEC4 ? 0 : w * 3 * kAPW));
       const int64_t ab = t0 + w * kAPW;  // first atom of this wave's slab (uniform)
       if (t0 + kTA <= a_end) {           // a whole tile: no per-atom checks
 #pragma unroll 1
@@ -924,11 +952,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
 
 // k_qcp_frames: one wave per frame.  Folds the chunk partials in a fixed
 // order (deterministic), forms COM / A / E0 and solves QCP on lane 0.
-template <bool GATHER, bool MASSES>
+template <bool GATHER, bool MASSES, bool PLANES = false>
 __global__ __launch_bounds__(kBlock) void k_qcp_frames(
     const double *__restrict__ part, StatsPlan pl, int64_t n_frames, const float *__restrict__ xyz,
     int64_t fstride, const int32_t *__restrict__ sel, const double *__restrict__ refinfo,
-    double *__restrict__ xform) {
+    double *__restrict__ xform, int64_t ps = 0) {
   const int64_t f = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (f >= n_frames) return;
@@ -957,9 +985,10 @@ __global__ __launch_bounds__(kBlock) void k_qcp_frames(
 
   const double nsel = refinfo[7 + 1];  // n_sel
   const double mtot = refinfo[7];      // total mass (n_sel without masses)
-  const int64_t o0 = GATHER ? 3 * (int64_t)sel[0] : 0;
+  const int64_t o0 = GATHER ? (PLANES ? 1 : 3) * (int64_t)sel[0] : 0;
+  const int64_t cs = PLANES ? ps : 1;
   const float *fr = xyz + f * fstride;
-  const double px = fr[o0], py = fr[o0 + 1], pz = fr[o0 + 2];
+  const double px = fr[o0], py = fr[o0 + cs], pz = fr[o0 + 2 * cs];
   // COM relative to the pivot
   const double cx = (MASSES ? s[3] : s[0]) / mtot;
   const double cy = (MASSES ? s[4] : s[1]) / mtot;
@@ -1521,42 +1550,79 @@ RMSF_EXPORT size_t rmsf_superpose_workspace_bytes(int64_t n_sel, int64_t n_frame
   return (size_t)p.G * (size_t)p.P * kStats * kTF * sizeof(double);
 }
 
+}  // extern "C"
+
+namespace {
+
+// rmsf_superpose(_planes): ps = 0 for (frame, atom, xyz) rows, else the
+// coordinate-plane stride of SoA frames (PLANES kernels)
+int superpose_impl(const char *who, const float *d_xyz, int64_t fstride, int64_t ps, int64_t n_frames, int64_t n_sel,
+                   const int32_t *d_sel, const double *d_masses, const double *d_ref, const double *d_refinfo,
+                   double *d_xform, void *d_work, size_t work_bytes, hipStream_t s) {
+  if (n_frames == 0) return RMSF_OK;
+  const bool planes = ps > 0;
+  if (!d_xyz || !d_ref || !d_refinfo || !d_xform || !d_work || n_sel < 1 || n_frames < 0 ||
+      (planes ? (ps < (d_sel ? 1 : n_sel) || fstride < 3 * ps) : fstride < (d_sel ? 3 : 3 * n_sel)))
+    return fail(RMSF_EINVAL, std::string(who) + ": bad arguments");
+  const StatsPlan plan = stats_plan(n_sel, n_frames);
+  if (work_bytes < rmsf_superpose_workspace_bytes(n_sel, n_frames))
+    return fail(RMSF_ENOMEM, std::string(who) + ": workspace too small");
+  double *part = static_cast<double *>(d_work);
+  const bool g = d_sel != nullptr, m = d_masses != nullptr;
+  const bool vec4 = !g && fstride % 4 == 0 && (!planes || ps % 4 == 0) &&
+                    reinterpret_cast<uintptr_t>(d_xyz) % 16 == 0;
+  dim3 grid((unsigned)plan.G);
+  auto stats = [&](auto P) {
+    constexpr bool PL = decltype(P)::value;
+#define ST_LAUNCH(G, M, V) \
+  hipLaunchKernelGGL((k_frame_stats<G, M, V, 1, PL>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, plan, part, ps)
+    if (g && m) ST_LAUNCH(true, true, false);
+    else if (g) ST_LAUNCH(true, false, false);
+    else if (m && vec4) ST_LAUNCH(false, true, true);
+    else if (m) ST_LAUNCH(false, true, false);
+    else if (vec4) ST_LAUNCH(false, false, true);
+    else ST_LAUNCH(false, false, false);
+#undef ST_LAUNCH
+  };
+  if (planes) stats(std::true_type{});
+  else stats(std::false_type{});
+  int rc = after_launch("k_frame_stats");
+  if (rc) return rc;
+  const unsigned gq = (unsigned)((n_frames + 3) / 4);
+  auto qcp = [&](auto P) {
+    constexpr bool PL = decltype(P)::value;
+#define QCP_LAUNCH(G, M) \
+  hipLaunchKernelGGL((k_qcp_frames<G, M, PL>), dim3(gq), dim3(kBlock), 0, s, part, plan, n_frames, d_xyz, fstride, d_sel, d_refinfo, d_xform, ps)
+    if (g && m) QCP_LAUNCH(true, true);
+    else if (g) QCP_LAUNCH(true, false);
+    else if (m) QCP_LAUNCH(false, true);
+    else QCP_LAUNCH(false, false);
+#undef QCP_LAUNCH
+  };
+  if (planes) qcp(std::true_type{});
+  else qcp(std::false_type{});
+  return after_launch("k_qcp_frames");
+}
+
+}  // namespace
+
+extern "C" {
+
 RMSF_EXPORT int rmsf_superpose(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
                                const int32_t *d_sel, const double *d_masses, const double *d_ref,
                                const double *d_refinfo, double *d_xform, void *d_work, size_t work_bytes,
                                void *stream) {
-  if (n_frames == 0) return RMSF_OK;
-  if (!d_xyz || !d_ref || !d_refinfo || !d_xform || !d_work || n_sel < 1 || n_frames < 0 ||
-      fstride < (d_sel ? 3 : 3 * n_sel))
-    return fail(RMSF_EINVAL, "rmsf_superpose: bad arguments");
-  const StatsPlan plan = stats_plan(n_sel, n_frames);
-  if (work_bytes < rmsf_superpose_workspace_bytes(n_sel, n_frames))
-    return fail(RMSF_ENOMEM, "rmsf_superpose: workspace too small");
-  hipStream_t s = S(stream);
-  double *part = static_cast<double *>(d_work);
-  const bool g = d_sel != nullptr, m = d_masses != nullptr;
-  const bool vec4 = !g && fstride % 4 == 0 && reinterpret_cast<uintptr_t>(d_xyz) % 16 == 0;
-  dim3 grid((unsigned)plan.G);
-#define ST_LAUNCH(G, M, V) \
-  hipLaunchKernelGGL((k_frame_stats<G, M, V>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, plan, part)
-  if (g && m) ST_LAUNCH(true, true, false);
-  else if (g) ST_LAUNCH(true, false, false);
-  else if (m && vec4) ST_LAUNCH(false, true, true);
-  else if (m) ST_LAUNCH(false, true, false);
-  else if (vec4) ST_LAUNCH(false, false, true);
-  else ST_LAUNCH(false, false, false);
-#undef ST_LAUNCH
-  int rc = after_launch("k_frame_stats");
-  if (rc) return rc;
-  const unsigned gq = (unsigned)((n_frames + 3) / 4);
-#define QCP_LAUNCH(G, M) \
-  hipLaunchKernelGGL((k_qcp_frames<G, M>), dim3(gq), dim3(kBlock), 0, s, part, plan, n_frames, d_xyz, fstride, d_sel, d_refinfo, d_xform)
-  if (g && m) QCP_LAUNCH(true, true);
-  else if (g) QCP_LAUNCH(true, false);
-  else if (m) QCP_LAUNCH(false, true);
-  else QCP_LAUNCH(false, false);
-#undef QCP_LAUNCH
-  return after_launch("k_qcp_frames");
+  return superpose_impl("rmsf_superpose", d_xyz, fstride, 0, n_frames, n_sel, d_sel, d_masses, d_ref, d_refinfo,
+                        d_xform, d_work, work_bytes, S(stream));
+}
+
+RMSF_EXPORT int rmsf_superpose_planes(const float *d_xyz, int64_t fstride, int64_t pstride, int64_t n_frames,
+                                      int64_t n_sel, const int32_t *d_sel, const double *d_masses,
+                                      const double *d_ref, const double *d_refinfo, double *d_xform, void *d_work,
+                                      size_t work_bytes, void *stream) {
+  if (pstride < 1) return fail(RMSF_EINVAL, "rmsf_superpose_planes: plane stride < 1");
+  return superpose_impl("rmsf_superpose_planes", d_xyz, fstride, pstride, n_frames, n_sel, d_sel, d_masses, d_ref,
+                        d_refinfo, d_xform, d_work, work_bytes, S(stream));
 }
 
 RMSF_EXPORT int64_t rmsf_split_count(int64_t n_frames, int n_splits, int s) {
@@ -1796,6 +1862,39 @@ RMSF_EXPORT int rmsf_accumulate_balanced(const float *d_xyz, int64_t fstride, in
   }
 #undef SK_LAUNCH
   return after_launch("k_accum_atoms_sk");
+}
+
+RMSF_EXPORT int rmsf_accumulate_balanced_planes(const float *d_xyz, int64_t fstride, int64_t pstride,
+                                                int64_t n_frames, int64_t n_sel, const int32_t *d_sel,
+                                                const double *d_xform, const double *d_refinfo, int mode,
+                                                int n_groups, void *d_work, size_t work_bytes, void *stream) {
+#if RMSF_SHIFTED_SUMS
+  if (mode != RMSF_MODE_WELFORD && mode != RMSF_MODE_SUM)
+    return fail(RMSF_EINVAL, "rmsf_accumulate_balanced_planes: bad mode");
+  if (!d_xyz || !d_work || !d_xform || !d_refinfo || n_sel < 1 || n_frames < 1 || pstride < (d_sel ? 1 : n_sel) ||
+      fstride < 3 * pstride || reinterpret_cast<uintptr_t>(d_work) % 16 != 0)
+    return fail(RMSF_EINVAL, "rmsf_accumulate_balanced_planes: bad arguments (the aligned sweeps only)");
+  hipStream_t s = S(stream);
+  const bool two = mode == RMSF_MODE_WELFORD, g = d_sel != nullptr;
+  const SkPlan pl = sk_plan(n_sel, 3, n_frames, n_groups, mode, two ? kSkPerCuSplitWel : kSkPerCuSplitSum);
+  if (work_bytes < sk_bytes(pl, two)) return fail(RMSF_ENOMEM, "rmsf_accumulate_balanced_planes: workspace too small");
+  int64_t *hdr = static_cast<int64_t *>(d_work);
+  double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
+  double *p1 = two ? p0 + (size_t)pl.G * pl.P * kBlock * 3 : nullptr;
+#define SPLIT_LAUNCH(M_, G_, Q_) \
+  hipLaunchKernelGGL((k_accum_split_sk<M_, true, G_, 4, Q_, true>), dim3(pl.G), dim3(kBlock * Q_), 0, s, d_xyz, fstride, d_sel, d_xform, d_refinfo, pl, hdr, p0, p1, pstride)
+  if (two) {
+    if (g) SPLIT_LAUNCH(0, true, kQWel);
+    else SPLIT_LAUNCH(0, false, kQWel);
+  } else {
+    if (g) SPLIT_LAUNCH(1, true, kQSum);
+    else SPLIT_LAUNCH(1, false, kQSum);
+  }
+#undef SPLIT_LAUNCH
+  return after_launch("k_accum_split_sk");
+#else
+  return fail(RMSF_EINVAL, "rmsf_accumulate_balanced_planes: needs the shifted-sums build");
+#endif
 }
 
 RMSF_EXPORT int rmsf_fold_balanced(const void *d_work, int64_t n_coord, int mode, int64_t acc_n, double *d_acc0,

@@ -56,12 +56,15 @@ SIGNATURES = {
     "rmsf_reference_setup": (c_int, [P, P, c_int64, P, P, P, P, P]),
     "rmsf_superpose_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "rmsf_superpose": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, P, P, P, c_size_t, P]),
+    "rmsf_superpose_planes": (c_int, [P, c_int64, c_int64, c_int64, c_int64, P, P, P, P, P, P, c_size_t, P]),
     "rmsf_accumulate_splits": (c_int, [c_int64, c_int64, c_int]),
     "rmsf_accumulate": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, c_int, c_int, P, P, P]),
     "rmsf_split_count": (c_int64, [c_int64, c_int, c_int]),
     "rmsf_accumulate_balanced_workspace_bytes": (c_size_t, [c_int64, c_int64, c_int]),
     "rmsf_accumulate_balanced": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, c_int, c_int, P, c_size_t, P]),
     "rmsf_fold_balanced": (c_int, [P, c_int64, c_int, c_int64, P, P, P]),
+    "rmsf_accumulate_balanced_planes": (c_int, [P, c_int64, c_int64, c_int64, c_int64, P, P, P, c_int, c_int, P,
+                                                c_size_t, P]),
     "rmsf_chan_merge": (c_int, [P, P, P, c_int, c_int64, P, P, P]),
     "rmsf_sum_splits": (c_int, [P, c_int, c_int64, P, P]),
     "rmsf_divide": (c_int, [P, c_double, c_int64, P, P]),

@@ -75,8 +75,14 @@ class Engine:
         return int(self.lib.rmsf_superpose_workspace_bytes(n_sel, n_frames))
 
     def superpose(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, sel, masses, ref, refinfo,
-                  xform: torch.Tensor, work: torch.Tensor) -> None:
-        """RMSF.py:94-97,127-131 + get_rotation_matrix (RMSF.py:43-51): per-frame COM + QCP."""
+                  xform: torch.Tensor, work: torch.Tensor, pstride: int = 0) -> None:
+        """RMSF.py:94-97,127-131 + get_rotation_matrix (RMSF.py:43-51): per-frame COM + QCP.
+        ``pstride`` > 0: frames stored as coordinate planes (rmsf_superpose_planes)."""
+        if pstride:
+            call("rmsf_superpose_planes", xyz_ptr, fstride, pstride, n_frames, n_sel, _ptr(sel), _ptr(masses),
+                 ref.data_ptr(), refinfo.data_ptr(), xform.data_ptr(), work.data_ptr(),
+                 work.numel() * work.element_size(), self.stream)
+            return
         call("rmsf_superpose", xyz_ptr, fstride, n_frames, n_sel, _ptr(sel), _ptr(masses), ref.data_ptr(),
              refinfo.data_ptr(), xform.data_ptr(), work.data_ptr(), work.numel() * work.element_size(), self.stream)
 
@@ -96,9 +102,15 @@ class Engine:
         return int(self.lib.rmsf_accumulate_balanced_workspace_bytes(n_sel, n_frames, n_groups))
 
     def accumulate_balanced(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, sel, xform, refinfo,
-                            mode: int, work: torch.Tensor, n_groups: int = 0) -> None:
+                            mode: int, work: torch.Tensor, n_groups: int = 0, pstride: int = 0) -> None:
         """RMSF.py:99-103 (SUM) / 133-138 (WELFORD) on the balanced grid (one equal
-        (lane chunk, frame) range per workgroup); partials go to ``work``."""
+        (lane chunk, frame) range per workgroup); partials go to ``work``.
+        ``pstride`` > 0: aligned sweep over coordinate planes read in place."""
+        if pstride:
+            call("rmsf_accumulate_balanced_planes", xyz_ptr, fstride, pstride, n_frames, n_sel, _ptr(sel),
+                 _ptr(xform), _ptr(refinfo), mode, n_groups, work.data_ptr(), work.numel() * work.element_size(),
+                 self.stream)
+            return
         call("rmsf_accumulate_balanced", xyz_ptr, fstride, n_frames, n_sel, _ptr(sel), _ptr(xform), _ptr(refinfo),
              mode, n_groups, work.data_ptr(), work.numel() * work.element_size(), self.stream)
 

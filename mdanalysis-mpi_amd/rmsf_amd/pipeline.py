@@ -25,7 +25,7 @@ from . import parallel
 from ._lib import (RMSF_MAX_SPLIT_FRAMES, RMSF_MODE_SUM, RMSF_MODE_WELFORD, RMSF_REFINFO_DOUBLES, RMSF_XFORM_DOUBLES,
                    RmsfEmptyError)
 from .engine import Engine
-from .sources import Batch, FrameList
+from .sources import Batch, DeviceSource, FrameList
 
 ALIGN_MODES = (None, "frame0", "average")
 
@@ -130,7 +130,7 @@ class Accumulator:
                 self.work = eng.empty((need + 7) // 8)
             with _span(self.timer, "accumulate", b.n_frames * self.n_sel):
                 eng.accumulate_balanced(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, xform, refinfo, self.mode,
-                                        self.work)
+                                        self.work, pstride=b.pstride)
             if pack is not None and self.mode == RMSF_MODE_WELFORD:
                 shift, off3, t, work = pack
                 if work is not None:
@@ -141,6 +141,8 @@ class Accumulator:
                 eng.fold_balanced(self.work, self.n_coord, self.mode, self.n, self.parts0[0], p1)
             self.n += b.n_frames
             return
+        if b.pstride:
+            raise ValueError("coordinate planes are read in place on the balanced grid only (n_splits=None)")
         s = max(self.fixed_splits, -(-b.n_frames // RMSF_MAX_SPLIT_FRAMES))
         with _span(self.timer, "accumulate", b.n_frames * self.n_sel):
             eng.accumulate(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, xform, refinfo, self.mode, s,
@@ -182,7 +184,7 @@ class Superposer:
             self.work = self.eng.empty((need + 7) // 8)
         with _span(self.timer, "superpose", b.n_frames * self.n_sel):
             self.eng.superpose(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, self.masses, ref, refinfo, xf,
-                               self.work)
+                               self.work, pstride=b.pstride)
         return xf
 
 
@@ -368,6 +370,8 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     # in plane order, permuted to (atom, xyz) at the end
     planes = not aligned and not n_splits and bool(getattr(source, "native_planes", False))
     batches_of = source.raw_batches if planes else source.batches
+    if aligned and not n_splits and isinstance(source, DeviceSource) and source.layout == "soa":
+        batches_of = source.plane_batches_in_place  # the aligned kernels' plane variants read HBM planes in place
     sup = Superposer(eng, n_sel, max_batch, m_dev, timer) if aligned else None
     rmsd = eng.empty(n_local) if (aligned and collect_rmsd) else None
     keep = aligned and collect_transforms

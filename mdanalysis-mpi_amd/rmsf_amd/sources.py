@@ -39,6 +39,7 @@ class Batch:
     n_frames: int
     sel: torch.Tensor | None      # int32 device selection (None = atoms 0..n_sel-1)
     release: Callable[[], None] | None = None
+    pstride: int = 0              # > 0: frames stored as coordinate planes this many floats apart
 
     def done(self) -> None:
         if self.release is not None:
@@ -245,6 +246,9 @@ class DeviceSource:
     rmsf_gather_planes first -- one extra read and write of the selected
     bytes, a convenience for frames that already live in HBM as planes."""
 
+    layout = "fac"
+    _planes = _ref_planes = None
+
     def __init__(self, traj: torch.Tensor, sel=None, offset: int = 0, n_traj: int | None = None,
                  layout: str = "fac"):
         if traj.dtype != torch.float32 or traj.device.type != "cuda":
@@ -265,7 +269,6 @@ class DeviceSource:
         self.traj = traj
         self.n_atoms = traj.shape[2] if layout == "soa" else traj.shape[1]
         self.fstride = traj.stride(0)
-        self._planes = self._ref_planes = None
         self.offset = offset
         self.n_traj = traj.shape[0] + offset if n_traj is None else n_traj
         self.sel_host = None if sel is None else np.ascontiguousarray(sel, dtype=np.int64)
@@ -329,6 +332,18 @@ class DeviceSource:
             yield from self._plane_batches(frames, b0, b1, max_frames, stream)
             return
         yield from self.raw_batches(frames, b0, b1, max_frames, stream)
+
+    def plane_batches_in_place(self, frames: FrameList, b0: int, b1: int, max_frames: int,
+                               stream: int) -> Iterator[Batch]:
+        """SoA frames for the aligned kernels' plane variants
+        (rmsf_superpose_planes, rmsf_accumulate_balanced_planes): runs read
+        in place (``pstride`` set); a scattered list gathered into rows."""
+        if _scattered(frames, b0, b1, max_frames):
+            yield from self._plane_batches(frames, b0, b1, max_frames, stream)
+            return
+        for first, step, n in frames.runs(b0, b1, max_frames):
+            _check_run(self, first, step, n, "HBM shard")
+            yield Batch(self._ptr(first), self.fstride * step, n, self.sel_dev, pstride=self.traj.stride(1))
 
     def raw_batches(self, frames: FrameList, b0: int, b1: int, max_frames: int, stream: int) -> Iterator[Batch]:
         """Batches of the frames as stored: rows read in place (or gathered

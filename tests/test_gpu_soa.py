@@ -250,3 +250,25 @@ def test_device_planes_in_place_ranks(size, n_atoms, root):
         np.testing.assert_allclose(rmsf[atoms], exp, rtol=0, atol=1e-9)
         if n_atoms >= 1_000_000:
             assert k == 2
+
+
+@pytest.mark.parametrize("align", ["frame0", "average"])
+@pytest.mark.parametrize("n_atoms,masses", [(4000, False), (4000, True), (3001, False)])
+def test_device_planes_aligned_in_place(align, n_atoms, masses):
+    """Aligned sweeps read HBM planes in place (rmsf_superpose_planes: the
+    float4 plane staging for 4-aligned planes, the element path otherwise;
+    rmsf_accumulate_balanced_planes): the same tiles, sums and transforms as
+    the row layout, so the same bits as the host rows streamed in batches of
+    the same frames."""
+    import torch
+
+    from rmsf_amd import RMSF
+    from rmsf_amd.synth import motion_table
+    traj = SY.frames(23, n_atoms, 0, 60, motion_table(6, 60))
+    m = np.random.default_rng(3).uniform(1, 16, n_atoms) if masses else None
+    dev = torch.tensor(_soa(traj), device="cuda")
+    for bf, run in ((60, {}), (9, {"start": 2, "stop": 59, "step": 3})):
+        a = RMSF(traj, align=align, masses=m, batch_frames=bf, collect_rmsd=True).run(**run)
+        b = RMSF(dev, align=align, masses=m, layout="soa", batch_frames=bf, collect_rmsd=True).run(**run)
+        _same(a, b)
+        np.testing.assert_array_equal(a.results.rmsd, b.results.rmsd)
