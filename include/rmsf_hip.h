@@ -160,11 +160,12 @@ int rmsf_accumulate_balanced(const float *d_xyz, int64_t frame_stride,
 int rmsf_fold_balanced(const void *d_work, int64_t n_coord, int mode,
                        int64_t acc_n, double *d_acc0, double *d_acc1,
                        void *stream);
-/* The aligned accumulate (d_xform required: RMSF.py:99-103 / 133-138) over
- * frames stored as coordinate planes (see rmsf_superpose_planes), read in
- * place; partials, header and fold as rmsf_accumulate_balanced's.  (The
- * unaligned sweep reads contiguous planes as rows of 3n floats and permutes
- * its statistics with rmsf_planes_to_rows.)                                 */
+/* The accumulate (RMSF.py:99-103 / 133-138 with d_xform, else the raw
+ * frames) over frames stored as coordinate planes (see
+ * rmsf_superpose_planes), read in place, one atom per lane; partials, header
+ * and fold as rmsf_accumulate_balanced's.  (Without a selection, the
+ * unaligned sweep can also read contiguous planes as rows of 3n floats on
+ * the float4 stream and permute its statistics with rmsf_planes_to_rows.)  */
 int rmsf_accumulate_balanced_planes(const float *d_xyz, int64_t frame_stride,
                                     int64_t plane_stride, int64_t n_frames,
                                     int64_t n_sel, const int32_t *d_sel,

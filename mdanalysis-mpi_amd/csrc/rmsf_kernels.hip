@@ -220,10 +220,11 @@ __global__ __launch_bounds__(kBlock) void k_welford_flat(
 
 // accum_atoms_run: one selected atom (12 B) per lane; MODE 0 = WELFORD
 // (m = mean, q = M2), 1 = SUM (m = sum).  xf = the first frame's transform.
-template <int MODE, bool ALIGN, int U>
+template <int MODE, bool ALIGN, int U, bool PLANES = false>
 __device__ __forceinline__ void accum_atoms_run(const float *__restrict__ p, int64_t fstride, int nf,
                                                 const double *__restrict__ xf, double rc0, double rc1, double rc2,
-                                                double (&m)[3], double (&q)[3]) {
+                                                double (&m)[3], double (&q)[3], int64_t ps = 0) {
+  const int64_t cs = PLANES ? ps : 1;  // x -> y -> z of the lane's atom (coordinate planes: ps floats)
 #pragma unroll
   for (int c = 0; c < 3; ++c) m[c] = q[c] = 0.0;
 #if RMSF_SHIFTED_SUMS
@@ -231,7 +232,7 @@ __device__ __forceinline__ void accum_atoms_run(const float *__restrict__ p, int
   // first frame after the transform
   double sh[3] = {0.0, 0.0, 0.0};
   if (MODE == RMSF_MODE_WELFORD && nf > 0) {
-    float x = p[0], y = p[1], z = p[2];
+    float x = p[0], y = p[cs], z = p[2 * cs];
     if (ALIGN) apply_xform(x, y, z, xf, rc0, rc1, rc2);
     sh[0] = (double)x, sh[1] = (double)y, sh[2] = (double)z;
   }
@@ -262,15 +263,15 @@ __device__ __forceinline__ void accum_atoms_run(const float *__restrict__ p, int
     for (int u = 0; u < U; ++u) {
       const float *r = p + (int64_t)(k + u) * fstride;
       vx[u] = __builtin_nontemporal_load(r);
-      vy[u] = __builtin_nontemporal_load(r + 1);
-      vz[u] = __builtin_nontemporal_load(r + 2);
+      vy[u] = __builtin_nontemporal_load(r + cs);
+      vz[u] = __builtin_nontemporal_load(r + 2 * cs);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) consume(vx[u], vy[u], vz[u], k + u);
   }
   for (; k < nf; ++k) {
     const float *r = p + (int64_t)k * fstride;
-    consume(r[0], r[1], r[2], k);
+    consume(r[0], r[cs], r[2 * cs], k);
   }
 #if RMSF_SHIFTED_SUMS
   if (MODE == RMSF_MODE_WELFORD && nf > 0) {
@@ -406,13 +407,13 @@ __global__ __launch_bounds__(kBlock) void k_welford_flat_sk(const float *__restr
   }
 }
 
-template <int MODE, bool ALIGN, bool GATHER, int U>
+template <int MODE, bool ALIGN, bool GATHER, int U, bool PLANES = false>
 __global__ __launch_bounds__(kBlock) void k_accum_atoms_sk(const float *__restrict__ xyz, int64_t fstride,
                                                            const int32_t *__restrict__ sel,
                                                            const double *__restrict__ xform,
                                                            const double *__restrict__ refinfo, SkPlan pl,
                                                            int64_t *__restrict__ hdr, double *__restrict__ parts0,
-                                                           double *__restrict__ parts1) {
+                                                           double *__restrict__ parts1, int64_t ps = 0) {
   const int b = sk_range(pl, blockIdx.x);
   if (blockIdx.x == 0 && threadIdx.x == 0) sk_write_header(hdr, pl);
   const double rc0 = ALIGN ? refinfo[0] : 0.0, rc1 = ALIGN ? refinfo[1] : 0.0, rc2 = ALIGN ? refinfo[2] : 0.0;
@@ -426,10 +427,10 @@ __global__ __launch_bounds__(kBlock) void k_accum_atoms_sk(const float *__restri
     f0 = uni64(f0);
     const int64_t a = c * kBlock + threadIdx.x;
     if (a < pl.lanes) {
-      const int64_t off = GATHER ? 3 * (int64_t)sel[a] : 3 * a;
+      const int64_t off = (PLANES ? 1 : 3) * (GATHER ? (int64_t)sel[a] : a);
       double m[3], q[3];
-      accum_atoms_run<MODE, ALIGN, U>(xyz + f0 * fstride + off, fstride, len, ALIGN ? xform + f0 * kXform : nullptr,
-                                      rc0, rc1, rc2, m, q);
+      accum_atoms_run<MODE, ALIGN, U, PLANES>(xyz + f0 * fstride + off, fstride, len,
+                                              ALIGN ? xform + f0 * kXform : nullptr, rc0, rc1, rc2, m, q, ps);
       const int64_t o = slot * (kBlock * 3) + 3 * threadIdx.x;
       store3<MODE>(parts0 + o, parts1 + o, m, q);
     }
@@ -1871,16 +1872,27 @@ RMSF_EXPORT int rmsf_accumulate_balanced_planes(const float *d_xyz, int64_t fstr
 #if RMSF_SHIFTED_SUMS
   if (mode != RMSF_MODE_WELFORD && mode != RMSF_MODE_SUM)
     return fail(RMSF_EINVAL, "rmsf_accumulate_balanced_planes: bad mode");
-  if (!d_xyz || !d_work || !d_xform || !d_refinfo || n_sel < 1 || n_frames < 1 || pstride < (d_sel ? 1 : n_sel) ||
+  if (!d_xyz || !d_work || (d_xform && !d_refinfo) || n_sel < 1 || n_frames < 1 || pstride < (d_sel ? 1 : n_sel) ||
       fstride < 3 * pstride || reinterpret_cast<uintptr_t>(d_work) % 16 != 0)
-    return fail(RMSF_EINVAL, "rmsf_accumulate_balanced_planes: bad arguments (the aligned sweeps only)");
+    return fail(RMSF_EINVAL, "rmsf_accumulate_balanced_planes: bad arguments");
   hipStream_t s = S(stream);
   const bool two = mode == RMSF_MODE_WELFORD, g = d_sel != nullptr;
-  const SkPlan pl = sk_plan(n_sel, 3, n_frames, n_groups, mode, two ? kSkPerCuSplitWel : kSkPerCuSplitSum);
+  const int per_cu = !d_xform ? kSkPerCuAtoms : two ? kSkPerCuSplitWel : kSkPerCuSplitSum;
+  const SkPlan pl = sk_plan(n_sel, 3, n_frames, n_groups, mode, per_cu);
   if (work_bytes < sk_bytes(pl, two)) return fail(RMSF_ENOMEM, "rmsf_accumulate_balanced_planes: workspace too small");
   int64_t *hdr = static_cast<int64_t *>(d_work);
   double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
   double *p1 = two ? p0 + (size_t)pl.G * pl.P * kBlock * 3 : nullptr;
+  if (!d_xform) {  // unaligned: one atom per lane (k_accum_atoms_sk), the row form's kernel for a selection
+#define SK_LAUNCH(M_, G_) \
+  hipLaunchKernelGGL((k_accum_atoms_sk<M_, false, G_, 4, true>), dim3(pl.G), dim3(kBlock), 0, s, d_xyz, fstride, d_sel, nullptr, nullptr, pl, hdr, p0, p1, pstride)
+    if (two && g) SK_LAUNCH(0, true);
+    else if (two) SK_LAUNCH(0, false);
+    else if (g) SK_LAUNCH(1, true);
+    else SK_LAUNCH(1, false);
+#undef SK_LAUNCH
+    return after_launch("k_accum_atoms_sk");
+  }
 #define SPLIT_LAUNCH(M_, G_, Q_) \
   hipLaunchKernelGGL((k_accum_split_sk<M_, true, G_, 4, Q_, true>), dim3(pl.G), dim3(kBlock * Q_), 0, s, d_xyz, fstride, d_sel, d_xform, d_refinfo, pl, hdr, p0, p1, pstride)
   if (two) {

@@ -370,8 +370,8 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     # in plane order, permuted to (atom, xyz) at the end
     planes = not aligned and not n_splits and bool(getattr(source, "native_planes", False))
     batches_of = source.raw_batches if planes else source.batches
-    if aligned and not n_splits and isinstance(source, DeviceSource) and source.layout == "soa":
-        batches_of = source.plane_batches_in_place  # the aligned kernels' plane variants read HBM planes in place
+    if not planes and not n_splits and isinstance(source, DeviceSource) and source.layout == "soa":
+        batches_of = source.plane_batches_in_place  # the kernels' plane variants read HBM planes in place
     sup = Superposer(eng, n_sel, max_batch, m_dev, timer) if aligned else None
     rmsd = eng.empty(n_local) if (aligned and collect_rmsd) else None
     keep = aligned and collect_transforms
