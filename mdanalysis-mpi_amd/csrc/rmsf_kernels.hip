@@ -103,10 +103,14 @@ typedef double f64x2 __attribute__((ext_vector_type(2)));
 }
 
 // (S1, S2) of n values shifted by sh -> (mean, M2); inv = 1/n.  M2 is
-// clamped at 0 (S2 - S1^2/n can round below it only when M2 ~ 0).
+// clamped at 0 (S2 - S1^2/n can round below it only when M2 ~ 0) -- by a
+// comparison, not fmax, so a NaN (e.g. the undefined rotation of a
+// one-atom superposition, NaN in qcprot too) stays NaN as in RMSF.py.
+__device__ __forceinline__ double clamp0(double v) { return v > 0.0 ? v : (v == v ? 0.0 : v); }
+
 [[maybe_unused]] __device__ __forceinline__ void shifted_to_moments(double &s1, double &s2, double sh, double inv) {
   const double d = s1 * inv;
-  s2 = fmax(0.0, fma(-s1, d, s2));
+  s2 = clamp0(fma(-s1, d, s2));
   s1 = sh + d;
 }
 
@@ -1263,7 +1267,7 @@ __global__ __launch_bounds__(kBlock) void k_chan_shift_finish(const double *__re
     mean[j] = c + t1 / nf;
     // the two sums are of non-negative terms whose difference rounds to
     // >= -eps * T2: clamp so that sqrt below never sees a negative zero-sum
-    q[x] = fmax(t[n + j] - t1 * (t1 / nf), 0.0);
+    q[x] = clamp0(t[n + j] - t1 * (t1 / nf));
     m2[j] = q[x];
   }
   if (rmsf) rmsf[a] = sqrt((q[0] + q[1] + q[2]) / nf);

@@ -78,6 +78,29 @@ def test_edges():
     assert issubclass(RmsfEmptyError, ZeroDivisionError)
 
 
+def test_one_atom_superposition_nan_like_qcprot():
+    """RMSF.py with a one-atom selection: the superposition is undefined --
+    qcprot's Newton step divides 0 by 0, the rotation is NaN and so is the
+    RMSF (the oracle, restating qcprot, gives NaN).  The device propagates
+    the NaN whatever the frame count and batching (M2's clamp at 0 is a
+    comparison, not fmax, which turned NaN into 0 for some segment splits)."""
+    from rmsf_amd import RMSF
+    from rmsf_amd.synth import motion_table
+    traj = SY.frames(5, 191, 0, 11, motion_table(7, 11))
+    planes = torch.tensor(np.ascontiguousarray(traj.transpose(0, 2, 1)), device="cuda")
+    for frames in (np.array([0, 2, 5, 9]), np.arange(11)):
+        exp = O.rmsf_script(traj[frames], np.array([40]), None, size=1, align="frame0")["rmsf"]
+        assert np.isnan(exp).all()
+        for x, kw in ((traj, {}), (torch.tensor(traj, device="cuda"), {}), (planes, {"layout": "soa"})):
+            for bf in (None, 3):
+                r = RMSF(x, select=[40], align="frame0", batch_frames=bf, **kw).run(frames=frames)
+                assert np.isnan(r.results.rmsf).all(), (kw, bf, r.results.rmsf)
+    # without alignment one atom is well defined
+    r = RMSF(traj, select=[40]).run()
+    exp = O.rmsf_script(traj, np.array([40]), None, size=1, align=None)["rmsf"]
+    np.testing.assert_allclose(r.results.rmsf, exp, atol=TOL)
+
+
 def test_rigid_motion_removed():
     """Analytic: rigid copies of one structure -> RMSF at the f32 floor."""
     from rmsf_amd import RMSF
