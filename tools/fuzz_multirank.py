@@ -4,7 +4,8 @@ test): P = 2..4 gloo ranks sharing the GPU, random atoms / selection /
 frames / alignment / batch size, and merge slabs forced on where the flat
 plan allows them -- each rank's RMSF against the oracle's mpirun -n P
 emulation of RMSF.py.  ``--root``: half the cases merge with a reduce to a
-random rank (merge_root).  python tools/fuzz_multirank.py [n_cases [--root]]"""
+random rank (merge_root); ``--planes``: half the shards are HBM coordinate
+planes.  python tools/fuzz_multirank.py [n_cases [--root] [--planes]]"""
 import os
 import sys
 import tempfile
@@ -34,7 +35,10 @@ def _worker(rank, size, init, q, case):
         b0, b1 = parallel.blocks(nf, size)[rank]
         mt = motion_table(case["mseed"], nf) if align else None
         shard = generate(eng, na, b0, max(b1 - b0, 1), seed=case["seed"], motion=mt)[: b1 - b0]
-        src = DeviceSource(shard, sel, offset=b0, n_traj=nf)
+        if case.get("planes"):  # the rank's shard as HBM coordinate planes, read in place
+            src = DeviceSource(shard.transpose(1, 2).contiguous(), sel, offset=b0, n_traj=nf, layout="soa")
+        else:
+            src = DeviceSource(shard, sel, offset=b0, n_traj=nf)
         res = run_pipeline(eng, src, FrameList(nf), align=align, max_batch=batch, merge_slabs=slabs,
                            merge_root=case.get("root"))
         torch.cuda.synchronize()
@@ -85,8 +89,10 @@ def main():
         slabs = int(rng.integers(2, 5)) if big else None
         case = dict(P=P, na=na, nf=nf, align=align, sel=sel, batch=batch, slabs=slabs,
                     seed=int(rng.integers(0, 1000)), mseed=int(rng.integers(0, 1000)))
-        if len(sys.argv) > 2 and sys.argv[2] == "--root" and rng.random() < 0.5:
+        if "--root" in sys.argv[2:] and rng.random() < 0.5:
             case["root"] = int(rng.integers(0, P))  # the merge as a reduce to this rank (RMSF.py:143)
+        if "--planes" in sys.argv[2:] and rng.random() < 0.5:
+            case["planes"] = True
         out = run_case(case)
         if any(o[2] == -1 for o in out):
             print(f"case {k}: FAILED {[o[1] for o in out if o[2] == -1][:1]}", flush=True)
@@ -102,7 +108,8 @@ def main():
         d = max(float(np.abs(o[1] - exp).max()) for o in out if o[1] is not None)
         worst = max(worst, d)
         print(f"case {k:2d}: P={P} {na:7d} atoms {len(cols):7d} sel {nf:4d} frames align={align} "
-              f"batch={batch} slabs={out[0][2]} root={root} max|d|={d:.2e}", flush=True)
+              f"batch={batch} slabs={out[0][2]} root={root} planes={bool(case.get('planes'))} max|d|={d:.2e}",
+              flush=True)
         if d > 1e-6:
             print("EXCEEDS 1e-6", flush=True)
             sys.exit(1)
