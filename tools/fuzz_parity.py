@@ -3,7 +3,7 @@ selections, align modes, frame selections and inputs (HBM tensor / host
 array in rows or coordinate planes / HBM planes / DCD or XTC file / one-process
 gpus=1)
 through RMSF(...).run() vs the oracle's RMSF.py
-restatement on the selected frames.  python tools/fuzz_parity.py [n_cases]"""
+restatement on the selected frames.  python tools/fuzz_parity.py [n_cases [--big]]"""
 import os
 import sys
 import tempfile
@@ -27,9 +27,12 @@ def main():
     rng = np.random.default_rng(2026)
     worst = 0.0
     tmp = tempfile.mkdtemp(prefix="fuzz_")
+    big = "--big" in sys.argv[2:]  # larger shapes: up to 200k atoms / 4,000 frames, <= 2e7 atom-frames
     for k in range(n_cases):
-        na = int(rng.integers(1, 3000))
-        nf = int(rng.integers(1, 200))
+        na = int(rng.integers(1, 200_000 if big else 3000))
+        nf = int(rng.integers(1, 4000 if big else 200))
+        if big:
+            nf = max(1, min(nf, 20_000_000 // na))
         traj = SY.frames(int(rng.integers(0, 1 << 30)), na, 0, nf, motion_table(int(rng.integers(0, 99)), nf))
         sel = np.sort(rng.choice(na, int(rng.integers(1, na + 1)), replace=False))
         align = [None, "frame0", "average"][int(rng.integers(0, 3))]
@@ -59,6 +62,8 @@ def main():
             with XTCFile(x) as f:
                 traj = f.read()
         bf = int(rng.integers(1, 64))
+        if big and rng.random() < 0.4:
+            bf = None  # the whole block in one batch (HBM inputs: one launch per sweep)
         got = RMSF(x, select=sel, align=align, batch_frames=bf, **kw).run(frames=frames).results.rmsf
         exp = O.rmsf_script(traj[frames], sel, None, size=1, align=align)["rmsf"]
         # a one-atom superposition is undefined: NaN in qcprot (and the oracle) -- and on the device
@@ -67,7 +72,7 @@ def main():
         err = float(np.abs(got[ok] - exp[ok]).max()) if ok.any() else 0.0
         worst = max(worst, err)
         print(f"case {k:2d}: {na:5d} atoms {len(sel):5d} sel {len(frames):4d}/{nf:3d} frames align={align} "
-              f"{where:6s} batch={bf:2d} max|d|={err:.2e}", flush=True)
+              f"{where:6s} batch={bf} max|d|={err:.2e}", flush=True)
         assert err < 1e-6, f"case {k}: {err}"
     print(f"all {n_cases} cases within 1e-6 A (worst {worst:.2e})")
 
