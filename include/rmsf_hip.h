@@ -89,6 +89,17 @@ int rmsf_reference_setup(const float *d_frame, const double *d_avg,
                          const double *d_masses, double *d_ref,
                          double *d_refinfo, void *stream);
 
+/* ---- RMSF.py:111 + 113-118 in one call: the sweep-1 average
+ * d_avg[n_sel*3] = d_sum / n_frames (f64) and the reference setup from it, as
+ * rmsf_divide() followed by rmsf_reference_setup(NULL, d_avg, ...) would
+ * write them, bit for bit.  Up to 1,024 selected atoms this is ONE launch
+ * (the division done as the sums are read); otherwise the same launches as
+ * the two calls.                                                            */
+int rmsf_reference_setup_mean(const double *d_sum, double n_frames,
+                              int64_t n_sel, const double *d_masses,
+                              double *d_avg, double *d_ref, double *d_refinfo,
+                              void *stream);
+
 /* ---- superposition: RMSF.py:94-97,127-131 + get_rotation_matrix RMSF.py:43-51
  * For every frame f of the block: mobile COM (mass-weighted, f64), the 3x3
  * inner product A = sum (x-com) (x) ref and E0 against the centred reference

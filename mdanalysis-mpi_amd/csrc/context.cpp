@@ -770,9 +770,8 @@ RMSF_EXPORT int rmsf_set_reference_average(rmsf_ctx *c) {
   if (c->sum.n <= 0) return fail(RMSF_EEMPTY, "rmsf_set_reference_average: no frames summed (RMSF.py:111)");
   DeviceScope ds(c->dev);
   CX_OK(c->avg.ensure(sizeof(double) * c->n_coord, c->stream));
-  CX_OK(rmsf_divide(c->sum.parts0.d(), (double)c->sum.n, c->n_coord, c->avg.d(), c->stream));
-  CX_OK(rmsf_reference_setup(nullptr, c->avg.d(), c->n_sel, nullptr, c->d_masses(), c->ref.d(), c->refinfo.d(),
-                             c->stream));
+  CX_OK(rmsf_reference_setup_mean(c->sum.parts0.d(), (double)c->sum.n, c->n_sel, c->d_masses(), c->avg.d(),
+                                  c->ref.d(), c->refinfo.d(), c->stream));
   c->ref_set = true;
   return digest_reference(c);
 }

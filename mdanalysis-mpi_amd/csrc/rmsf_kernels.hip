@@ -1055,19 +1055,22 @@ constexpr int kRefBlocks = 256;
 constexpr int kRefThreads = 256;
 static_assert(RMSF_REFINFO_DOUBLES >= 16 + 2 * 4 * kRefBlocks, "refinfo scratch");
 
+// f64 path: avg[] / div -- the sweep-1 sums divided by the frame count as
+// they are read (RMSF.py:111, the same IEEE division as k_divide; div = 1 is
+// exact for an average passed in)
 template <bool FROM_F32, bool GATHER>
 __device__ __forceinline__ void ref_load(const float *__restrict__ frame, const double *__restrict__ avg,
                                          const int32_t *__restrict__ sel, int64_t a, double &x, double &y,
-                                         double &z) {
+                                         double &z, double div = 1.0) {
   if (FROM_F32) {
     const float *p = frame + (GATHER ? 3 * (int64_t)sel[a] : 3 * a);
     x = (double)p[0];
     y = (double)p[1];
     z = (double)p[2];
   } else {
-    x = avg[3 * a];
-    y = avg[3 * a + 1];
-    z = avg[3 * a + 2];
+    x = avg[3 * a] / div;
+    y = avg[3 * a + 1] / div;
+    z = avg[3 * a + 2] / div;
   }
 }
 
@@ -1096,43 +1099,47 @@ __device__ __forceinline__ void fold_partials(const double *__restrict__ p, int 
 }
 
 template <bool FROM_F32, bool GATHER, bool MASSES>
-__global__ __launch_bounds__(kRefThreads) void k_ref_com(const float *__restrict__ frame,
-                                                         const double *__restrict__ avg, int64_t n_sel,
-                                                         const int32_t *__restrict__ sel,
-                                                         const double *__restrict__ masses,
-                                                         double *__restrict__ info) {
+__device__ __forceinline__ void ref_com_body(const float *__restrict__ frame, const double *__restrict__ avg,
+                                             int64_t n_sel, const int32_t *__restrict__ sel,
+                                             const double *__restrict__ masses, double *__restrict__ info, int blk,
+                                             int nblk, double div = 1.0) {
   double v[4] = {0, 0, 0, 0};
-  const int64_t stride = (int64_t)gridDim.x * kRefThreads;
-  for (int64_t a = (int64_t)blockIdx.x * kRefThreads + threadIdx.x; a < n_sel; a += stride) {
+  const int64_t stride = (int64_t)nblk * kRefThreads;
+  for (int64_t a = (int64_t)blk * kRefThreads + threadIdx.x; a < n_sel; a += stride) {
     double x, y, z;
-    ref_load<FROM_F32, GATHER>(frame, avg, sel, a, x, y, z);
+    ref_load<FROM_F32, GATHER>(frame, avg, sel, a, x, y, z, div);
     const double m = MASSES ? masses[a] : 1.0;
     v[0] = fma(x, m, v[0]);
     v[1] = fma(y, m, v[1]);
     v[2] = fma(z, m, v[2]);
     v[3] += m;
   }
-  block_sum4(v, info + 16 + 4 * blockIdx.x);
+  block_sum4(v, info + 16 + 4 * blk);
 }
 
 template <bool FROM_F32, bool GATHER>
-__global__ __launch_bounds__(kRefThreads) void k_ref_center(const float *__restrict__ frame,
-                                                            const double *__restrict__ avg, int64_t n_sel,
-                                                            const int32_t *__restrict__ sel,
-                                                            double *__restrict__ ref, double *__restrict__ info) {
+__device__ __forceinline__ void ref_center_body(const float *__restrict__ frame, const double *__restrict__ avg,
+                                                int64_t n_sel, const int32_t *__restrict__ sel,
+                                                double *__restrict__ ref, double *__restrict__ info, int blk,
+                                                int nblk, double div = 1.0, double *__restrict__ avg_out = nullptr) {
   __shared__ double com[4];
   if (threadIdx.x < 64) {
     double t[4];
-    fold_partials(info + 16, gridDim.x, t);
+    fold_partials(info + 16, nblk, t);
     if (threadIdx.x < 4) com[threadIdx.x] = t[threadIdx.x];
   }
   __syncthreads();
   const double c0 = com[0] / com[3], c1 = com[1] / com[3], c2 = com[2] / com[3];
   double w[4] = {0, 0, 0, 0};
-  const int64_t stride = (int64_t)gridDim.x * kRefThreads;
-  for (int64_t a = (int64_t)blockIdx.x * kRefThreads + threadIdx.x; a < n_sel; a += stride) {
+  const int64_t stride = (int64_t)nblk * kRefThreads;
+  for (int64_t a = (int64_t)blk * kRefThreads + threadIdx.x; a < n_sel; a += stride) {
     double x, y, z;
-    ref_load<FROM_F32, GATHER>(frame, avg, sel, a, x, y, z);
+    ref_load<FROM_F32, GATHER>(frame, avg, sel, a, x, y, z, div);
+    if (avg_out) {
+      avg_out[3 * a] = x;
+      avg_out[3 * a + 1] = y;
+      avg_out[3 * a + 2] = z;
+    }
     const double r0 = x - c0, r1 = y - c1, r2 = z - c2;
     ref[3 * a] = r0;
     ref[3 * a + 1] = r1;
@@ -1142,12 +1149,13 @@ __global__ __launch_bounds__(kRefThreads) void k_ref_center(const float *__restr
     w[2] += r2;
     w[3] = fma(r0, r0, fma(r1, r1, fma(r2, r2, w[3])));
   }
-  block_sum4(w, info + 16 + 4 * kRefBlocks + 4 * blockIdx.x);
-  if (blockIdx.x == 0 && threadIdx.x < 3) info[threadIdx.x] = threadIdx.x == 0 ? c0 : (threadIdx.x == 1 ? c1 : c2);
-  if (blockIdx.x == 0 && threadIdx.x == 3) info[7] = com[3];
+  block_sum4(w, info + 16 + 4 * kRefBlocks + 4 * blk);
+  if (blk == 0 && threadIdx.x < 3) info[threadIdx.x] = threadIdx.x == 0 ? c0 : (threadIdx.x == 1 ? c1 : c2);
+  if (blk == 0 && threadIdx.x == 3) info[7] = com[3];
 }
 
-__global__ __launch_bounds__(64) void k_ref_finish(int nb, int64_t n_sel, double *__restrict__ info) {
+// one wave
+__device__ __forceinline__ void ref_finish_body(int nb, int64_t n_sel, double *__restrict__ info) {
   double t[4];
   fold_partials(info + 16 + 4 * kRefBlocks, nb, t);
   if (threadIdx.x < 4) info[3 + threadIdx.x] = t[threadIdx.x];  // sum r (3), sum |r|^2
@@ -1155,6 +1163,48 @@ __global__ __launch_bounds__(64) void k_ref_finish(int nb, int64_t n_sel, double
     info[8] = (double)n_sel;
     for (int j = 9; j < 16; ++j) info[j] = 0.0;
   }
+}
+
+template <bool FROM_F32, bool GATHER, bool MASSES>
+__global__ __launch_bounds__(kRefThreads) void k_ref_com(const float *__restrict__ frame,
+                                                         const double *__restrict__ avg, int64_t n_sel,
+                                                         const int32_t *__restrict__ sel,
+                                                         const double *__restrict__ masses,
+                                                         double *__restrict__ info) {
+  ref_com_body<FROM_F32, GATHER, MASSES>(frame, avg, n_sel, sel, masses, info, blockIdx.x, gridDim.x);
+}
+
+template <bool FROM_F32, bool GATHER>
+__global__ __launch_bounds__(kRefThreads) void k_ref_center(const float *__restrict__ frame,
+                                                            const double *__restrict__ avg, int64_t n_sel,
+                                                            const int32_t *__restrict__ sel,
+                                                            double *__restrict__ ref, double *__restrict__ info) {
+  ref_center_body<FROM_F32, GATHER>(frame, avg, n_sel, sel, ref, info, blockIdx.x, gridDim.x);
+}
+
+__global__ __launch_bounds__(64) void k_ref_finish(int nb, int64_t n_sel, double *__restrict__ info) {
+  ref_finish_body(nb, n_sel, info);
+}
+
+// The three steps of a one-workgroup grid (n_sel <= 4 x 256) in ONE launch:
+// the same code in the same order, the partials passed through the same
+// scratch (each read by the wave that wrote it), so the record is
+// bit-identical to the three launches' -- two launch boundaries fewer per
+// reference (RMSF.py's two sweeps at config C1's size run two of them).
+// With div != 1 (rmsf_reference_setup_mean) it also absorbs k_divide: the
+// average is avg[] / div, written to avg_out as it is read.
+template <bool FROM_F32, bool GATHER, bool MASSES>
+__global__ __launch_bounds__(kRefThreads) void k_ref_setup1(const float *__restrict__ frame,
+                                                            const double *__restrict__ avg, int64_t n_sel,
+                                                            const int32_t *__restrict__ sel,
+                                                            const double *__restrict__ masses,
+                                                            double *__restrict__ ref, double *__restrict__ info,
+                                                            double div = 1.0, double *__restrict__ avg_out = nullptr) {
+  ref_com_body<FROM_F32, GATHER, MASSES>(frame, avg, n_sel, sel, masses, info, 0, 1, div);
+  __syncthreads();
+  ref_center_body<FROM_F32, GATHER>(frame, avg, n_sel, sel, ref, info, 0, 1, div, avg_out);
+  __syncthreads();
+  if (threadIdx.x < 64) ref_finish_body(1, n_sel, info);
 }
 
 // ---------------------------------------------------------------------------
@@ -1519,9 +1569,13 @@ RMSF_EXPORT int rmsf_block_range(int64_t n_frames, int size, int rank, int64_t *
   return RMSF_OK;
 }
 
-RMSF_EXPORT int rmsf_reference_setup(const float *d_frame, const double *d_avg, int64_t n_sel,
-                                     const int32_t *d_sel, const double *d_masses, double *d_ref,
-                                     double *d_refinfo, void *stream) {
+}  // extern "C"
+
+namespace {
+
+int reference_setup_impl(const float *d_frame, const double *d_avg, int64_t n_sel, const int32_t *d_sel,
+                         const double *d_masses, double *d_ref, double *d_refinfo, void *stream, bool one_launch,
+                         double div = 1.0, double *d_avg_out = nullptr) {
   if ((d_frame == nullptr) == (d_avg == nullptr))
     return fail(RMSF_EINVAL, "rmsf_reference_setup: exactly one of d_frame / d_avg");
   if (n_sel < 1 || !d_ref || !d_refinfo) return fail(RMSF_EINVAL, "rmsf_reference_setup: bad arguments");
@@ -1529,6 +1583,24 @@ RMSF_EXPORT int rmsf_reference_setup(const float *d_frame, const double *d_avg, 
   hipStream_t s = S(stream);
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(kRefBlocks, (n_sel + 4 * kRefThreads - 1) / (4 * kRefThreads)));
   const dim3 grid(nb), block(kRefThreads);
+  if (nb == 1 && one_launch) {  // one launch, bit-identical to the three below
+#define ONE_LAUNCH(F, G, M) hipLaunchKernelGGL((k_ref_setup1<F, G, M>), dim3(1), block, 0, s, d_frame, d_avg, n_sel, d_sel, d_masses, d_ref, d_refinfo, div, d_avg_out)
+    if (d_frame) {
+      if (g && m) ONE_LAUNCH(true, true, true);
+      else if (g) ONE_LAUNCH(true, true, false);
+      else if (m) ONE_LAUNCH(true, false, true);
+      else ONE_LAUNCH(true, false, false);
+    } else {
+      if (m) ONE_LAUNCH(false, false, true);
+      else ONE_LAUNCH(false, false, false);
+    }
+#undef ONE_LAUNCH
+    return after_launch("k_ref_setup1");
+  }
+  if (d_avg_out) {  // more than one workgroup: the average first (k_divide), then the setup from it
+    hipLaunchKernelGGL(k_divide, dim3(grid1(3 * n_sel)), dim3(kBlock), 0, s, d_avg, div, 3 * n_sel, d_avg_out);
+    d_avg = d_avg_out;
+  }
 #define COM_LAUNCH(F, G, M) hipLaunchKernelGGL((k_ref_com<F, G, M>), grid, block, 0, s, d_frame, d_avg, n_sel, d_sel, d_masses, d_refinfo)
 #define CEN_LAUNCH(F, G) hipLaunchKernelGGL((k_ref_center<F, G>), grid, block, 0, s, d_frame, d_avg, n_sel, d_sel, d_ref, d_refinfo)
   if (d_frame) {
@@ -1547,6 +1619,32 @@ RMSF_EXPORT int rmsf_reference_setup(const float *d_frame, const double *d_avg, 
 #undef CEN_LAUNCH
   hipLaunchKernelGGL(k_ref_finish, dim3(1), dim3(64), 0, s, nb, n_sel, d_refinfo);
   return after_launch("k_ref_*");
+}
+
+}  // namespace
+
+extern "C" {
+
+RMSF_EXPORT int rmsf_reference_setup(const float *d_frame, const double *d_avg, int64_t n_sel,
+                                     const int32_t *d_sel, const double *d_masses, double *d_ref,
+                                     double *d_refinfo, void *stream) {
+  return reference_setup_impl(d_frame, d_avg, n_sel, d_sel, d_masses, d_ref, d_refinfo, stream, true);
+}
+
+RMSF_EXPORT int rmsf_reference_setup_mean(const double *d_sum, double n_frames, int64_t n_sel,
+                                          const double *d_masses, double *d_avg, double *d_ref, double *d_refinfo,
+                                          void *stream) {
+  if (!d_sum || !d_avg || !(n_frames > 0)) return fail(RMSF_EINVAL, "rmsf_reference_setup_mean: bad arguments");
+  return reference_setup_impl(nullptr, d_sum, n_sel, nullptr, d_masses, d_ref, d_refinfo, stream, true, n_frames,
+                              d_avg);
+}
+
+// test hook (not in the public header): always the three launches, for the
+// bit-identity test of k_ref_setup1
+RMSF_EXPORT int rmsf_internal_reference_setup3(const float *d_frame, const double *d_avg, int64_t n_sel,
+                                               const int32_t *d_sel, const double *d_masses, double *d_ref,
+                                               double *d_refinfo, void *stream) {
+  return reference_setup_impl(d_frame, d_avg, n_sel, d_sel, d_masses, d_ref, d_refinfo, stream, false);
 }
 
 RMSF_EXPORT size_t rmsf_superpose_workspace_bytes(int64_t n_sel, int64_t n_frames) {

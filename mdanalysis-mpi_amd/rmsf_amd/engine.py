@@ -71,6 +71,18 @@ class Engine:
              ref.data_ptr(), info.data_ptr(), self.stream)
         return ref, info
 
+    def reference_setup_mean(self, total: torch.Tensor, n_frames: float, n_sel: int,
+                             masses: torch.Tensor | None = None):
+        """RMSF.py:111 + 113-118: the average total / n_frames and the
+        reference from it (one launch up to 1,024 selected atoms);
+        bit-identical to ``divide`` + ``reference_setup(avg=...)``."""
+        avg = self.empty(3 * n_sel)
+        ref = self.empty(n_sel, 3)
+        info = self.empty(RMSF_REFINFO_DOUBLES)
+        call("rmsf_reference_setup_mean", total.data_ptr(), float(n_frames), n_sel, _ptr(masses), avg.data_ptr(),
+             ref.data_ptr(), info.data_ptr(), self.stream)
+        return avg, ref, info
+
     def workspace_bytes(self, n_sel: int, n_frames: int) -> int:
         return int(self.lib.rmsf_superpose_workspace_bytes(n_sel, n_frames))
 

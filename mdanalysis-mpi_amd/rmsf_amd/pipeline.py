@@ -408,9 +408,8 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
         if n_local:
             sweep(acc1, ref0, info0, xf_first)
         total = parallel.allreduce_sum_(acc1.result0)       # RMSF.py:110
-        average = eng.empty(3 * n_sel)
-        eng.divide(total, float(n_total), average)          # RMSF.py:111
-        ref, info = eng.reference_setup(n_sel, avg=average, masses=m_dev)  # RMSF.py:113-118
+        # RMSF.py:111 + 113-118: the average and the reference from it
+        average, ref, info = eng.reference_setup_mean(total, float(n_total), n_sel, m_dev)
     elif align == "frame0":
         ref, info = reference_from_frame(eng, source, ref_frame, n_sel, m_dev, ref_owner)
     else:

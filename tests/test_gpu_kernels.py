@@ -105,6 +105,59 @@ def test_reference_setup(eng, masses, gather):
     np.testing.assert_allclose(ref2.cpu().numpy(), rc2, atol=1e-12)
 
 
+@pytest.mark.parametrize("n_sel", [1, 214, 1024, 1025])
+def test_reference_setup_one_launch_bitwise(eng, n_sel):
+    """Up to 1,024 selected atoms the reference setup is one launch
+    (k_ref_setup1); its record and centred reference are bit-identical to the
+    three launches it replaces (k_ref_com, k_ref_center, k_ref_finish), for
+    frames and averages, gathered or not, with and without masses."""
+    import ctypes
+
+    L = eng.lib
+    f3 = L.rmsf_internal_reference_setup3
+    f3.restype = ctypes.c_int
+    f3.argtypes = L.rmsf_reference_setup.argtypes
+    rng = np.random.default_rng(n_sel)
+    n_atoms = n_sel + 300
+    frame = torch.tensor(rng.normal(0, 20, (n_atoms, 3)).astype(np.float32), device=eng.device)
+    sel = torch.tensor(np.sort(rng.choice(n_atoms, n_sel, replace=False)).astype(np.int32), device=eng.device)
+    avg = torch.tensor(rng.normal(5, 20, 3 * n_sel), device=eng.device)
+    masses = torch.tensor(rng.uniform(1, 16, n_sel), device=eng.device)
+    for src in ("frame", "frame_gather", "avg"):
+        for m in (None, masses):
+            outs = []
+            for fn in (L.rmsf_reference_setup, f3):
+                ref, info = eng.empty(n_sel, 3), eng.empty(16 + 2 * 4 * 256)
+                info.fill_(7.0)
+                fp = frame.data_ptr() if src != "avg" else None
+                ap = avg.data_ptr() if src == "avg" else None
+                sp = sel.data_ptr() if src == "frame_gather" else None
+                mp = m.data_ptr() if m is not None else None
+                assert fn(fp, ap, n_sel, sp, mp, ref.data_ptr(), info.data_ptr(), eng.stream) == 0
+                outs.append((ref, info[:16].clone()))
+            _sync()
+            for a, b in zip(outs[0], outs[1]):
+                assert torch.equal(a.view(torch.int64), b.view(torch.int64)), (src, m is not None)
+
+
+@pytest.mark.parametrize("n_sel", [1, 214, 1024, 1025, 5000])
+def test_reference_setup_mean_bitwise(eng, n_sel):
+    """rmsf_reference_setup_mean (RMSF.py:111 + 113-118; one launch up to
+    1,024 atoms) writes the average and the reference bit for bit as
+    rmsf_divide + rmsf_reference_setup(avg) do."""
+    rng = np.random.default_rng(n_sel + 1)
+    total = torch.tensor(rng.normal(0, 2000, 3 * n_sel), device=eng.device)
+    masses = torch.tensor(rng.uniform(1, 16, n_sel), device=eng.device)
+    for m in (None, masses):
+        avg, ref, info = eng.reference_setup_mean(total, 98.0, n_sel, m)
+        avg2 = eng.empty(3 * n_sel)
+        eng.divide(total, 98.0, avg2)
+        ref2, info2 = eng.reference_setup(n_sel, avg=avg2, masses=m)
+        _sync()
+        for a, b in ((avg, avg2), (ref, ref2), (info[:16], info2[:16])):
+            assert torch.equal(a.view(torch.int64), b.view(torch.int64)), m is not None
+
+
 @pytest.mark.parametrize("gather", [False, True])
 def test_superpose_vs_oracle(eng, gather):
     from rmsf_amd.synth import generate, motion_table
