@@ -171,6 +171,15 @@ int rmsf_accumulate_balanced(const float *d_xyz, int64_t frame_stride,
 int rmsf_fold_balanced(const void *d_work, int64_t n_coord, int mode,
                        int64_t acc_n, double *d_acc0, double *d_acc1,
                        void *stream);
+/* rmsf_fold_balanced (WELFORD) of the last batch + the finalise of
+ * RMSF.py:146 (d_rmsf[n_sel] over n_total frames) in one launch, bit-identical
+ * to rmsf_fold_balanced + rmsf_finalize.  Needs an atom plan: the aligned
+ * sweep, a gathered selection or planes (one atom per lane).  The flat plan
+ * of an unaligned contiguous selection cannot finalise in the fold: d_rmsf is
+ * then all NaN, and rmsf_finalize is the call to make.                      */
+int rmsf_fold_balanced_finalize(const void *d_work, int64_t n_coord,
+                                int64_t acc_n, double *d_acc0, double *d_acc1,
+                                int64_t n_total, double *d_rmsf, void *stream);
 /* The accumulate (RMSF.py:99-103 / 133-138 with d_xform, else the raw
  * frames) over frames stored as coordinate planes (see
  * rmsf_superpose_planes), read in place, one atom per lane; partials, header

@@ -584,13 +584,18 @@ __device__ __forceinline__ void shift_moments(double mu, double M2, double c, do
   *t2 = __builtin_fma(nk, d * d, M2);
 }
 
-template <int PACK>
+// FIN: also the finalise of RMSF.py:146 for an atom plan (cpl = 3: lane l is
+// atom l), rmsf[l] = sqrt((M2x + M2y + M2z) / n_total) -- k_finalize's
+// expression on the values just stored, so bit-identical to it, one launch
+// fewer.  A flat plan (cpl = 4) cannot: it writes NaN to every atom.
+template <int PACK, bool FIN = false>
 __global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ hdr,
                                                     const double *__restrict__ parts0, int64_t n_coord,
                                                     double acc_n, double *__restrict__ acc0,
                                                     double *__restrict__ acc1, const void *__restrict__ shift,
                                                     const double *__restrict__ off3, double *__restrict__ t,
-                                                    int64_t l_off, int64_t l_end, int64_t t_n) {
+                                                    int64_t l_off, int64_t l_end, int64_t t_n,
+                                                    double *__restrict__ rmsf = nullptr, double n_total = 0.0) {
   // lanes [l_off, l_end) (an atom slab; 0, INT64_MAX = all).  T1/T2 of the
   // slab's coordinates go to t[j - j_lo] and t[t_n + j - j_lo].
   const int64_t l = l_off + (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -710,6 +715,14 @@ __global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ 
     if (x < nx) {
       acc0[j0 + x] = mu[x];
       if (wel) acc1[j0 + x] = M[x];
+    }
+  }
+  if (FIN) {
+    if (cpl == 3) {
+      if (nx == 3) rmsf[l] = sqrt((M[0] + M[1] + M[2]) / n_total);
+    } else {
+      const int64_t n_sel = n_coord / 3;
+      for (int64_t a = 4 * l; a < 4 * l + 4 && a < n_sel; ++a) rmsf[a] = __builtin_nan("");
     }
   }
   if (PACK) {
@@ -2024,6 +2037,18 @@ RMSF_EXPORT int rmsf_fold_balanced(const void *d_work, int64_t n_coord, int mode
   hipLaunchKernelGGL(k_fold_sk<0>, dim3(grid1((n_coord + 2) / 3)), dim3(kBlock), 0, S(stream), hdr, p0, n_coord,
                      (double)acc_n, d_acc0, d_acc1, nullptr, nullptr, nullptr, (int64_t)0, INT64_MAX, n_coord);
   return after_launch("k_fold_sk");
+}
+
+RMSF_EXPORT int rmsf_fold_balanced_finalize(const void *d_work, int64_t n_coord, int64_t acc_n, double *d_acc0,
+                                            double *d_acc1, int64_t n_total, double *d_rmsf, void *stream) {
+  if (!d_work || !d_acc0 || !d_acc1 || !d_rmsf || n_coord < 3 || n_coord % 3 != 0 || acc_n < 0 || n_total < 1)
+    return fail(RMSF_EINVAL, "rmsf_fold_balanced_finalize: bad arguments");
+  const int64_t *hdr = static_cast<const int64_t *>(d_work);
+  const double *p0 = reinterpret_cast<const double *>(hdr + kSkHdr);
+  hipLaunchKernelGGL((k_fold_sk<0, true>), dim3(grid1((n_coord + 2) / 3)), dim3(kBlock), 0, S(stream), hdr, p0,
+                     n_coord, (double)acc_n, d_acc0, d_acc1, nullptr, nullptr, nullptr, (int64_t)0, INT64_MAX, n_coord,
+                     d_rmsf, (double)n_total);
+  return after_launch("k_fold_sk<FIN>");
 }
 
 RMSF_EXPORT int rmsf_fold_balanced_shift(const void *d_work, int64_t n_coord, int64_t acc_n, double *d_acc0,

@@ -55,6 +55,7 @@ SIGNATURES = {
     "rmsf_block_range": (c_int, [c_int64, c_int, c_int, POINTER(c_int64), POINTER(c_int64)]),
     "rmsf_reference_setup": (c_int, [P, P, c_int64, P, P, P, P, P]),
     "rmsf_reference_setup_mean": (c_int, [P, c_double, c_int64, P, P, P, P, P]),
+    "rmsf_fold_balanced_finalize": (c_int, [P, c_int64, c_int64, P, P, c_int64, P, P]),
     "rmsf_superpose_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "rmsf_superpose": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, P, P, P, c_size_t, P]),
     "rmsf_superpose_planes": (c_int, [P, c_int64, c_int64, c_int64, c_int64, P, P, P, P, P, P, c_size_t, P]),

@@ -132,6 +132,13 @@ class Engine:
         (Chan's merge, RMSF.py:36-41, or a sum)."""
         call("rmsf_fold_balanced", work.data_ptr(), n_coord, mode, acc_n, acc0.data_ptr(), _ptr(acc1), self.stream)
 
+    def fold_balanced_finalize(self, work: torch.Tensor, n_coord: int, acc_n: int, acc0: torch.Tensor,
+                               acc1: torch.Tensor, n_total: int, rmsf: torch.Tensor) -> None:
+        """fold_balanced (WELFORD) + finalize (RMSF.py:146) in one launch, for
+        an atom plan (aligned sweeps, gathered selections, planes)."""
+        call("rmsf_fold_balanced_finalize", work.data_ptr(), n_coord, acc_n, acc0.data_ptr(), acc1.data_ptr(),
+             n_total, rmsf.data_ptr(), self.stream)
+
     def fold_balanced_shift(self, work: torch.Tensor, n_coord: int, acc_n: int, acc0: torch.Tensor,
                             acc1: torch.Tensor, shift: torch.Tensor, off3, out: torch.Tensor) -> None:
         """fold_balanced (WELFORD) + chan_shift_pack in one launch: ``out`` =

@@ -105,6 +105,7 @@ class Accumulator:
             self.parts1 = eng.empty(1 + self.s_max, self.n_coord)
         self.n = 0
         self.packed = False
+        self.finalized = False
         self._zeroed = False
         if n_splits:
             self._zero()
@@ -117,11 +118,13 @@ class Accumulator:
             self._zeroed = True
 
     def add(self, b: Batch, xform: torch.Tensor | None = None, refinfo: torch.Tensor | None = None,
-            pack=None) -> None:
+            pack=None, fin=None) -> None:
         """``pack`` = (shift, off3, t, pending broadcast or None): this is the
         rank's last batch before the cross-rank merge; on the balanced grid
         in WELFORD mode the fold also writes the merge's moments about the
-        shift into ``t`` (one launch; ``self.packed`` tells the caller)."""
+        shift into ``t`` (one launch; ``self.packed`` tells the caller).
+        ``fin`` = (rmsf, n_total): the last batch of an aligned single-rank
+        sweep; the fold also finalises (RMSF.py:146, ``self.finalized``)."""
         eng = self.eng
         p1 = None if self.parts1 is None else self.parts1[0]
         if not self.fixed_splits:
@@ -137,6 +140,9 @@ class Accumulator:
                     work.wait()  # the shift's broadcast ran beside the sweep
                 eng.fold_balanced_shift(self.work, self.n_coord, self.n, self.parts0[0], p1, shift, off3, t)
                 self.packed = True
+            elif fin is not None and self.mode == RMSF_MODE_WELFORD and self.aligned:
+                eng.fold_balanced_finalize(self.work, self.n_coord, self.n, self.parts0[0], p1, fin[1], fin[0])
+                self.finalized = True
             else:
                 eng.fold_balanced(self.work, self.n_coord, self.mode, self.n, self.parts0[0], p1)
             self.n += b.n_frames
@@ -379,7 +385,7 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     xf_first = eng.empty(n_local, RMSF_XFORM_DOUBLES) if (keep and align == "average") else None
     average = None
 
-    def sweep(acc: Accumulator, ref=None, info=None, xf_out=None, pack=None, slabs=None):
+    def sweep(acc: Accumulator, ref=None, info=None, xf_out=None, pack=None, slabs=None, fin=None):
         done, slabbed = 0, None
         for b in batches_of(frames, b0, b1, max_batch, eng.stream):
             xf = None
@@ -397,7 +403,7 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                     slabbed = _slab_sweep(eng, acc, b, _slab_bounds(n_chunks, slabs), shift_, off3_, work_, timer,
                                           root)
             if slabbed is None:
-                acc.add(b, xf, info, pack if last else None)
+                acc.add(b, xf, info, pack if last else None, fin if last else None)
             done += b.n_frames
             b.done()
         return slabbed
@@ -435,8 +441,11 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     k_slabs = merge_slabs if merge_slabs is not None else (SLABS_AUTO if n_sel >= SLAB_MIN_ATOMS else 0)
     slabs = k_slabs if (size > 1 and k_slabs > 1 and not aligned and not n_splits) else None
     slabbed = None
+    # one rank, aligned: the last fold also finalises (RMSF.py:146)
+    rmsf_fin = eng.empty(n_sel) if (size == 1 and aligned) else None
     if n_local:
-        slabbed = sweep(acc, ref, info, xf_last, (shift, off3, t, shift_work) if size > 1 else None, slabs)
+        slabbed = sweep(acc, ref, info, xf_last, (shift, off3, t, shift_work) if size > 1 else None, slabs,
+                        (rmsf_fin, n_total) if rmsf_fin is not None else None)
     if slabbed is not None:                                  # RMSF.py:141-143 + 146, slab by slab
         if root is not None and rank != root:
             for *_, work in slabbed:
@@ -470,8 +479,11 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
         mean, m2, rmsf = _rows_from_planes(eng, acc.result0, acc.result1, n_sel, n_total)
     else:
         mean, m2 = acc.result0, acc.result1
-        rmsf = eng.empty(n_sel)
-        eng.finalize(m2, n_sel, n_total, rmsf)               # RMSF.py:146
+        if acc.finalized:                                    # RMSF.py:146, in the last fold
+            rmsf = rmsf_fin
+        else:
+            rmsf = eng.empty(n_sel)
+            eng.finalize(m2, n_sel, n_total, rmsf)           # RMSF.py:146
     return PipelineResult(rmsf=rmsf, mean=mean.view(n_sel, 3), m2=m2.view(n_sel, 3), n_frames=n_total,
                           n_local=n_local, block=(b0, b1),
                           average=None if average is None else average.view(n_sel, 3), rmsd=rmsd,

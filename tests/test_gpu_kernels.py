@@ -310,6 +310,55 @@ def test_balanced_aligned_vs_split_grid(eng, n_sel, nf, groups, gather):
     np.testing.assert_allclose(np.sqrt(Q2.reshape(-1, 3).sum(1) / nf), O.rmsf_two_pass(al), rtol=0, atol=1e-6)
 
 
+@pytest.mark.parametrize("n_sel,nf,gather", [(214, 98, True), (1, 5, False), (3000, 700, False),
+                                             (20000, 64, True)])
+def test_fold_finalize_bitwise(eng, n_sel, nf, gather):
+    """rmsf_fold_balanced_finalize (the aligned sweep's last fold + the
+    RMSF.py:146 finalise, one launch) writes mean, M2 and RMSF bit for bit as
+    rmsf_fold_balanced + rmsf_finalize, after a first batch (acc_n > 0) too;
+    on a flat plan (unaligned contiguous selection) the RMSF is NaN."""
+    from rmsf_amd.synth import generate, motion_table
+    from rmsf_amd._lib import RMSF_MODE_WELFORD
+    n_atoms = n_sel + 5 if gather else n_sel
+    traj = generate(eng, n_atoms, 0, nf, seed=5, motion=motion_table(3, nf))
+    sel = np.sort(np.random.default_rng(6).choice(n_atoms, n_sel, replace=False)) if gather else None
+    sdev = torch.tensor(sel.astype(np.int32), device=eng.device) if gather else None
+    ref, info = eng.reference_setup(n_sel, frame_ptr=traj.data_ptr(), sel=sdev)
+    xf = eng.empty(nf, 16)
+    sw = eng.empty(eng.workspace_bytes(n_sel, nf) // 8 + 1)
+    eng.superpose(traj.data_ptr(), 3 * n_atoms, nf, n_sel, sdev, None, ref, info, xf, sw)
+    nc = 3 * n_sel
+    out = []
+    for fused in (False, True):
+        mean, m2, r = eng.empty(nc), eng.empty(nc), eng.empty(n_sel)
+        acc, cut = 0, nf // 2
+        for f0, f1 in ((0, cut), (cut, nf)):
+            if f1 <= f0:
+                continue
+            n = f1 - f0
+            work = eng.empty(eng.balanced_workspace_bytes(n_sel, n) // 8 + 2)
+            ptr = traj.data_ptr() + f0 * 3 * n_atoms * 4
+            eng.accumulate_balanced(ptr, 3 * n_atoms, n, n_sel, sdev, xf[f0:], info, RMSF_MODE_WELFORD, work)
+            if fused and f1 == nf:
+                eng.fold_balanced_finalize(work, nc, acc, mean, m2, nf, r)
+            else:
+                eng.fold_balanced(work, nc, RMSF_MODE_WELFORD, acc, mean, m2)
+            acc += n
+        if not fused:
+            eng.finalize(m2, n_sel, nf, r)
+        out.append((mean, m2, r))
+    _sync()
+    for a, b in zip(*out):
+        assert torch.equal(a.view(torch.int64), b.view(torch.int64))
+    if not gather and n_sel % 4 == 0:  # the flat plan: no per-atom lanes
+        work = eng.empty(eng.balanced_workspace_bytes(n_sel, nf) // 8 + 2)
+        eng.accumulate_balanced(traj.data_ptr(), 3 * n_atoms, nf, n_sel, None, None, None, RMSF_MODE_WELFORD, work)
+        mean, m2, r = eng.empty(nc), eng.empty(nc), eng.zeros(n_sel)
+        eng.fold_balanced_finalize(work, nc, 0, mean, m2, nf, r)
+        _sync()
+        assert torch.isnan(r).all()
+
+
 def test_balanced_bad_arguments(eng):
     from rmsf_amd import RmsfError
     from rmsf_amd._lib import RMSF_MODE_WELFORD

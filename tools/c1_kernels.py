@@ -38,6 +38,14 @@ def main():
                 return (avg, *eng.reference_setup(n_sel, avg=avg, masses=masses))
 
             Engine.reference_setup_mean = setup_mean
+        if not hasattr(old, "rmsf_fold_balanced_finalize"):  # fold, then finalise
+            del _lib.SIGNATURES["rmsf_fold_balanced_finalize"]
+
+            def fold_finalize(eng, work, n_coord, acc_n, acc0, acc1, n_total, rmsf):
+                eng.fold_balanced(work, n_coord, _lib.RMSF_MODE_WELFORD, acc_n, acc0, acc1)
+                eng.finalize(acc1, n_coord // 3, n_total, rmsf)
+
+            Engine.fold_balanced_finalize = fold_finalize
     reps = int(args[0]) if args else 200
     eng = Engine()
     n_atoms, nf = 3341, 98
