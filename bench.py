@@ -111,9 +111,12 @@ def parse(argv=None):
     ap.add_argument("--merge-slabs", type=int, default=None,
                     help="N>1, no alignment: atom slabs of the final sweep whose all-reduces overlap the next slab "
                          "(default: 2 from 1M atoms, else none; 0 = off)")
-    ap.add_argument("--merge-root", action="store_true",
-                    help="N>1: merge with a reduce to rank 0 (RMSF.py:143's comm.reduce(root=0)) instead of an "
-                         "all-reduce that leaves the result on every rank")
+    ap.add_argument("--merge", choices=["root", "all"], default="root",
+                    help="N>1: the final Chan merge as a reduce to rank 0 (default: RMSF.py:143's "
+                         "comm.reduce(root=0); a ring reduce carries the 6*n_sel doubles over each link once) or as "
+                         "an all-reduce that leaves the result on every rank (twice the link bytes)")
+    ap.add_argument("--merge-root", action="store_const", dest="merge", const="root",
+                    help="same as --merge root (kept for older command lines)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo only "
                                                      "to rehearse several ranks on one GPU)")
     return ap.parse_args(argv)
@@ -456,6 +459,8 @@ def main():
         # even when --warmup 0
         _t = torch.zeros(3 * n_atoms, dtype=torch.float64, device=eng.device)
         dist.all_reduce(_t)
+        if a.merge == "root":
+            dist.reduce(_t, dst=0)
         dist.barrier()
         torch.cuda.synchronize()
         del _t
@@ -507,7 +512,7 @@ def main():
             src.drop_cache()  # every step streams the file again
         return run_pipeline(eng, src, fl, align=align, block=(b0, b1), ref_owner=0, n_splits=a.splits,
                             max_batch=a.batch_frames, timer=timer, merge_slabs=a.merge_slabs,
-                            merge_root=0 if a.merge_root else None)
+                            merge_root=0 if a.merge == "root" else None)
 
     def timed(align, steps, warmup):
         timer = KernelTimer()
@@ -534,7 +539,7 @@ def main():
     out = base_line(a, wl, world, dt, par)
     if world > 1:
         out["config"]["merge_slabs"] = res.extras.get("merge_slabs", 0)
-        out["config"]["merge"] = "reduce to rank 0 (RMSF.py:143)" if a.merge_root else "all-reduce"
+        out["config"]["merge"] = "reduce to rank 0 (RMSF.py:143)" if a.merge == "root" else "all-reduce"
     launches, acc_ms, acc_af = timer.totals("accumulate")
     traffic = load_traffic(a.workload, n_atoms, n_local) if launches == a.steps else None
     kname = (("k_accum_atoms" if wl["align"] else "k_welford_flat") if a.splits
@@ -544,7 +549,7 @@ def main():
     rows = gather_rank_rows([launches, acc_ms, acc_af], coll_dev)
     out["roofline"] = rank_roofline(kname, rows, traffic, f"profiles/pmc_{a.workload}.json" if traffic else None)
     out["cpu_baseline"] = cpu
-    # the merged result, identical on every rank (on rank 0 only with --merge-root)
+    # the merged result (on rank 0 only with the default reduce-to-root merge)
     out["rmsf_checksum"] = float(res.rmsf.sum()) if res.rmsf is not None else None
     # whole-step rate in algorithmic bytes (incl. merges, finalise, launch gaps)
     out["pipeline_hbm_gbs"] = B_PER_ATOM_FRAME * n_atoms * n_local * a.steps / dt / 1e9

@@ -80,3 +80,11 @@ def test_gather_rank_rows_gloo_two_ranks():
     for rank, rows, slow, launches in out:
         assert rows == [[1.0, 0.5, 1.0e6], [2.0, 1.0, 2.0e6]]
         assert launches == 3 and slow in (0, 1)
+
+
+def test_merge_defaults_to_reduce_to_root():
+    # RMSF.py:143's comm.reduce(root=0) is the bench's N>1 merge; --merge all
+    # is the all-reduce, --merge-root the older spelling of the default
+    assert bench.parse([]).merge == "root"
+    assert bench.parse(["--merge", "all"]).merge == "all"
+    assert bench.parse(["--merge", "all", "--merge-root"]).merge == "root"

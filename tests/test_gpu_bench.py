@@ -109,6 +109,7 @@ def test_torchrun_two_ranks_same_result_as_one_gpu(align):
     l1 = json.loads(one.stdout.strip().splitlines()[-1])
     l2 = json.loads(two.stdout.strip().splitlines()[-1])
     assert l2["n_gpus"] == 2 and l2["config"]["n_frames_per_gpu"] == 150
+    assert l2["config"]["merge"] == "reduce to rank 0 (RMSF.py:143)"  # the default, RMSF.py:143's reduce
     # the roofline describes both ranks (KernelTimer totals all-reduced)
     rf = l2["roofline"]
     sweeps = 2 if align == "average" else 1
@@ -150,3 +151,25 @@ def test_torchrun_merge_slabs_same_checksum():
     assert lines["2"]["config"]["merge_slabs"] == 2 and lines["0"]["config"]["merge_slabs"] == 0
     assert lines["2"]["rmsf_checksum"] == lines["0"]["rmsf_checksum"]
     assert lines["2"]["roofline"]["launches"] == 2 * 2 * 2  # 2 ranks x 2 steps x 2 slabs
+
+
+def test_torchrun_merge_all_same_checksum():
+    """``--merge all`` (an all-reduce leaving the result on every rank) and the
+    default reduce to rank 0 (RMSF.py:143) give the same RMSF bit for bit
+    with two ranks (the sum of two packed partials is order-free)."""
+    common = ["--n-atoms", "6000", "--frames", "301", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+              "--no-modes", "--gpus", "2", "--backend", "gloo"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    lines = {}
+    for m in ("root", "all"):
+        for _ in range(3):
+            r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+                                "--merge", m] + common, cwd=ROOT, capture_output=True, text=True, timeout=300,
+                               env=env)
+            if r.returncode == 0 or "EADDRINUSE" not in r.stderr:
+                break
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines[m] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert lines["root"]["config"]["merge"].startswith("reduce") and lines["all"]["config"]["merge"] == "all-reduce"
+    assert lines["root"]["rmsf_checksum"] == lines["all"]["rmsf_checksum"]
