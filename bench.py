@@ -391,6 +391,8 @@ def main_single_process(a, wl, cpu) -> None:
     out = base_line(a, wl, n, dt, par)
     out["devices"] = devs
     out["rehearsal"] = rehearsal
+    if n > 1:  # the context ABI's merge (rmsf_multi_chan_merge) leaves the result on every device
+        out["config"]["merge"] = "all-reduce (one-process contexts; --merge applies to the torchrun form)"
     kname = ("k_accum_split_sk" if align else "k_welford_flat_sk")
     out["roofline"] = rank_roofline(kname, acc)
     if align:
