@@ -175,8 +175,10 @@ int rmsf_fold_balanced(const void *d_work, int64_t n_coord, int mode,
  * RMSF.py:146 (d_rmsf[n_sel] over n_total frames) in one launch, bit-identical
  * to rmsf_fold_balanced + rmsf_finalize.  Needs an atom plan: the aligned
  * sweep, a gathered selection or planes (one atom per lane).  The flat plan
- * of an unaligned contiguous selection cannot finalise in the fold: d_rmsf is
- * then all NaN, and rmsf_finalize is the call to make.                      */
+ * of an unaligned contiguous selection cannot finalise in the fold: the call
+ * then returns RMSF_EINVAL and launches nothing (the library remembers, on the
+ * host, which plan its last accumulate wrote into d_work); rmsf_fold_balanced
+ * + rmsf_finalize are the calls to make.                                   */
 int rmsf_fold_balanced_finalize(const void *d_work, int64_t n_coord,
                                 int64_t acc_n, double *d_acc0, double *d_acc1,
                                 int64_t n_total, double *d_rmsf, void *stream);

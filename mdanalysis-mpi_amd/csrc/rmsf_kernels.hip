@@ -23,7 +23,9 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "rmsf_hip.h"
@@ -1906,6 +1908,25 @@ int fold_shift_launch(const int64_t *hdr, const double *p0, int64_t n_coord, int
   return after_launch("k_fold_sk");
 }
 
+// The layout (coordinates per lane) of the plan each balanced accumulate last
+// wrote into a workspace, kept on the host: the plan header itself is in HBM,
+// and rmsf_fold_balanced_finalize must refuse a flat (4 per lane) plan, which
+// cannot finalise in the fold, instead of writing NaN with RMSF_OK.
+std::mutex g_plan_mu;
+std::unordered_map<const void *, int> g_plan_cpl;
+
+void note_plan(const void *d_work, int cpl) {
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  if (g_plan_cpl.size() > 4096) g_plan_cpl.clear();  // freed workspaces: forget them all
+  g_plan_cpl[d_work] = cpl;
+}
+
+int plan_cpl(const void *d_work) {  // 0 = not written by this library's accumulate
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  const auto it = g_plan_cpl.find(d_work);
+  return it == g_plan_cpl.end() ? 0 : it->second;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1938,9 +1959,11 @@ RMSF_EXPORT int rmsf_accumulate_balanced(const float *d_xyz, int64_t fstride, in
     if (work_bytes < sk_bytes(pl, two)) return fail(RMSF_ENOMEM, "rmsf_accumulate_balanced: workspace too small");
     double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
     double *p1 = p0 + (size_t)pl.G * pl.P * kBlock * 4;
+    note_plan(d_work, 4);
     hipLaunchKernelGGL((k_welford_flat_sk<4>), dim3(pl.G), dim3(kBlock), 0, s, d_xyz, fstride / 4, pl, hdr, p0, p1);
     return after_launch("k_welford_flat_sk");
   }
+  note_plan(d_work, 3);
   const bool g = d_sel != nullptr, al = d_xform != nullptr;
   const bool split = al && RMSF_SHIFTED_SUMS;  // aligned: the frame-split kernel
   const int per_cu = !al ? kSkPerCuAtoms : !split ? kSkPerCuAligned : two ? kSkPerCuSplitWel : kSkPerCuSplitSum;
@@ -1998,6 +2021,7 @@ RMSF_EXPORT int rmsf_accumulate_balanced_planes(const float *d_xyz, int64_t fstr
   int64_t *hdr = static_cast<int64_t *>(d_work);
   double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
   double *p1 = two ? p0 + (size_t)pl.G * pl.P * kBlock * 3 : nullptr;
+  note_plan(d_work, 3);
   if (!d_xform) {  // unaligned: one atom per lane (k_accum_atoms_sk), the row form's kernel for a selection
 #define SK_LAUNCH(M_, G_) \
   hipLaunchKernelGGL((k_accum_atoms_sk<M_, false, G_, 4, true>), dim3(pl.G), dim3(kBlock), 0, s, d_xyz, fstride, d_sel, nullptr, nullptr, pl, hdr, p0, p1, pstride)
@@ -2043,6 +2067,10 @@ RMSF_EXPORT int rmsf_fold_balanced_finalize(const void *d_work, int64_t n_coord,
                                             double *d_acc1, int64_t n_total, double *d_rmsf, void *stream) {
   if (!d_work || !d_acc0 || !d_acc1 || !d_rmsf || n_coord < 3 || n_coord % 3 != 0 || acc_n < 0 || n_total < 1)
     return fail(RMSF_EINVAL, "rmsf_fold_balanced_finalize: bad arguments");
+  if (plan_cpl(d_work) == 4)
+    return fail(RMSF_EINVAL,
+                "rmsf_fold_balanced_finalize: the workspace holds a flat (4 coordinates per lane) plan, which cannot "
+                "finalise in the fold; call rmsf_fold_balanced + rmsf_finalize");
   const int64_t *hdr = static_cast<const int64_t *>(d_work);
   const double *p0 = reinterpret_cast<const double *>(hdr + kSkHdr);
   hipLaunchKernelGGL((k_fold_sk<0, true>), dim3(grid1((n_coord + 2) / 3)), dim3(kBlock), 0, S(stream), hdr, p0,
@@ -2089,6 +2117,7 @@ RMSF_EXPORT int rmsf_accumulate_balanced_slab(const float *d_xyz, int64_t fstrid
   int64_t *hdr = static_cast<int64_t *>(d_work);
   double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
   double *p1 = p0 + (size_t)pl.G * pl.P * kBlock * 4;
+  note_plan(d_work, 4);
   hipLaunchKernelGGL((k_welford_flat_sk<4>), dim3((unsigned)(pl.Cs * pl.S)), dim3(kBlock), 0, S(stream), d_xyz,
                      fstride / 4, pl, hdr, p0, p1);
   return after_launch("k_welford_flat_sk");
@@ -2285,10 +2314,12 @@ RMSF_EXPORT int rmsf_synth_frames(float *d_out, int64_t fstride, int64_t n_atoms
   if (!d_out || n_atoms < 1 || nf < 0 || f0 < 0 || fstride < 3 * n_atoms)
     return fail(RMSF_EINVAL, "rmsf_synth_frames: bad arguments");
   if (nf == 0) return RMSF_OK;
-  const int64_t total = nf * n_atoms;
-  const int64_t per_launch = (int64_t)kBlock * 0x7fffffffLL / 2;
+  // One work-item per (frame, atom).  An AQL dispatch's grid size is a 32-bit
+  // count of WORK-ITEMS (blocks x 256), not of blocks: a 1M-atom x 20k-frame
+  // trajectory (2e10 items) in one launch wraps modulo 2^32 and leaves most
+  // frames unwritten.  Each launch covers at most 2^31 items.
+  const int64_t per_launch = int64_t(1) << 31;
   for (int64_t done = 0; done < nf;) {
-    // keep each launch's element count (frames * atoms) under the grid limit
     int64_t fchunk = std::max<int64_t>(1, per_launch / n_atoms);
     fchunk = std::min(fchunk, nf - done);
     hipLaunchKernelGGL(k_synth, dim3(grid1(fchunk * n_atoms)), dim3(kBlock), 0, S(stream), d_out + done * fstride,
@@ -2297,7 +2328,6 @@ RMSF_EXPORT int rmsf_synth_frames(float *d_out, int64_t fstride, int64_t n_atoms
     if (rc) return rc;
     done += fchunk;
   }
-  (void)total;
   return RMSF_OK;
 }
 

@@ -396,7 +396,9 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                 if xf_out is not None:
                     xf_out[done:done + b.n_frames].copy_(xf)
             last = done + b.n_frames == n_local
-            if slabs and done == 0 and last and b.sel is None and xf is None:
+            # the slab kernels read each frame as 3n contiguous floats: rows,
+            # or unpadded planes (never a plane stride wider than the atoms)
+            if slabs and done == 0 and last and b.sel is None and xf is None and not b.pstride:
                 n_chunks = eng.balanced_slab_chunks(b.ptr, b.fstride, b.n_frames, n_sel)
                 if n_chunks >= 2 * 3:
                     shift_, off3_, _, work_ = pack

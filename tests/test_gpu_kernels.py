@@ -316,7 +316,8 @@ def test_fold_finalize_bitwise(eng, n_sel, nf, gather):
     """rmsf_fold_balanced_finalize (the aligned sweep's last fold + the
     RMSF.py:146 finalise, one launch) writes mean, M2 and RMSF bit for bit as
     rmsf_fold_balanced + rmsf_finalize, after a first batch (acc_n > 0) too;
-    on a flat plan (unaligned contiguous selection) the RMSF is NaN."""
+    on a flat plan (unaligned contiguous selection) the call is refused with
+    RMSF_EINVAL instead of writing NaN."""
     from rmsf_amd.synth import generate, motion_table
     from rmsf_amd._lib import RMSF_MODE_WELFORD
     n_atoms = n_sel + 5 if gather else n_sel
@@ -354,9 +355,11 @@ def test_fold_finalize_bitwise(eng, n_sel, nf, gather):
         work = eng.empty(eng.balanced_workspace_bytes(n_sel, nf) // 8 + 2)
         eng.accumulate_balanced(traj.data_ptr(), 3 * n_atoms, nf, n_sel, None, None, None, RMSF_MODE_WELFORD, work)
         mean, m2, r = eng.empty(nc), eng.empty(nc), eng.zeros(n_sel)
-        eng.fold_balanced_finalize(work, nc, 0, mean, m2, nf, r)
+        from rmsf_amd import RmsfError
+        with pytest.raises(RmsfError, match="flat"):  # refused on the host, nothing launched
+            eng.fold_balanced_finalize(work, nc, 0, mean, m2, nf, r)
         _sync()
-        assert torch.isnan(r).all()
+        assert (r == 0).all()
 
 
 def test_balanced_bad_arguments(eng):

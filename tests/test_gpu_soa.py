@@ -205,7 +205,7 @@ def test_device_planes_in_place(n_atoms):
             np.testing.assert_allclose(a.results[k], b.results[k], rtol=1e-13, atol=1e-13)
 
 
-def _planes_rank_worker(rank, size, init, q, n_atoms, n_frames, root):
+def _planes_rank_worker(rank, size, init, q, n_atoms, n_frames, root, pad=0, slabs=None):
     import sys
 
     from conftest import PKG, ROOT
@@ -223,10 +223,12 @@ def _planes_rank_worker(rank, size, init, q, n_atoms, n_frames, root):
         from rmsf_amd.synth import generate
         eng = Engine(torch.device("cuda", 0))
         b0, b1 = parallel.blocks(n_frames, size)[rank]
-        planes = generate(eng, n_atoms, b0, b1 - b0, seed=19).transpose(1, 2).contiguous()
+        planes = generate(eng, n_atoms + pad, b0, b1 - b0, seed=19).transpose(1, 2).contiguous()
+        if pad:  # padded planes: a view of the first n_atoms of each wider plane (plane stride > n_atoms)
+            planes = planes[:, :, :n_atoms]
         src = DeviceSource(planes, offset=b0, n_traj=n_frames, layout="soa")
-        assert src.native_planes
-        res = run_pipeline(eng, src, FrameList(n_frames), merge_root=root)
+        assert src.native_planes == (pad == 0)
+        res = run_pipeline(eng, src, FrameList(n_frames), merge_root=root, merge_slabs=slabs)
         torch.cuda.synchronize()
         q.put((rank, None if res.rmsf is None else res.rmsf.cpu().numpy(), res.extras.get("merge_slabs", 0)))
     except Exception as e:  # noqa: BLE001
@@ -235,16 +237,22 @@ def _planes_rank_worker(rank, size, init, q, n_atoms, n_frames, root):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("size,n_atoms,root", [(2, 4000, None), (3, 4000, 0), (2, 1_000_000, None)])
-def test_device_planes_in_place_ranks(size, n_atoms, root):
+@pytest.mark.parametrize("size,n_atoms,root,pad,slabs", [(2, 4000, None, 0, None), (3, 4000, 0, 0, None),
+                                                         (2, 1_000_000, None, 0, None), (2, 1_000_000, None, 36, None),
+                                                         (2, 300_000, 0, 4, 2), (3, 4000, None, 8, 2)])
+def test_device_planes_in_place_ranks(size, n_atoms, root, pad, slabs):
     """The same over gloo ranks sharing the GPU: the merge's shift (frame 0 of
     the list, broadcast) stays in plane order with the statistics; 1M atoms:
-    the merge in atom slabs.  Against a two-pass variance of the regenerated
-    frames on sampled atoms."""
+    the merge in atom slabs.  Padded planes (a plane stride wider than the
+    atom count) are read through the plane kernels and never take
+    the flat slab path, which reads each frame as 3n contiguous floats; their
+    merge runs unslabbed.  Against a two-pass variance of the regenerated
+    frames on sampled atoms (the generator's atoms 0..n-1 of the wider
+    trajectory are the same values)."""
     from conftest import spawn_ranks
     n_frames = 20 * size + 3
-    out = spawn_ranks(_planes_rank_worker, size, lambda r, init, q: (r, size, init, q, n_atoms, n_frames, root),
-                      timeout=200)
+    out = spawn_ranks(_planes_rank_worker, size,
+                      lambda r, init, q: (r, size, init, q, n_atoms, n_frames, root, pad, slabs), timeout=200)
     atoms = np.sort(np.random.default_rng(2).choice(n_atoms, 64, replace=False))
     host = SY.frames(19, n_atoms, 0, n_frames, atoms=atoms).astype(np.float64)
     exp = np.sqrt(((host - host.mean(0)) ** 2).sum(0).sum(1) / n_frames)
@@ -254,7 +262,9 @@ def test_device_planes_in_place_ranks(size, n_atoms, root):
             assert rmsf is None
             continue
         np.testing.assert_allclose(rmsf[atoms], exp, rtol=0, atol=1e-9)
-        if n_atoms >= 1_000_000:
+        if pad:
+            assert k == 0
+        elif n_atoms >= 1_000_000:
             assert k == 2
 
 
