@@ -86,6 +86,9 @@ def parse(argv=None):
     ap.add_argument("--frames-per-gpu", type=int, default=None, help="shorthand for --scaling weak --frames F")
     ap.add_argument("--rehearse", action="store_true",
                     help="one-process --gpus N with fewer devices: list device 0 N times (rehearsal)")
+    ap.add_argument("--rehearse-transport", choices=["fold", "noop"], default="fold",
+                    help="--rehearse: exchanges by the in-process host fold (exact, synchronising) or by a no-op "
+                         "(host-cost timing only: the merged result is not the global one)")
     ap.add_argument("--splits", type=int, default=None)
     ap.add_argument("--batch-frames", type=int, default=None, help="aligned modes: frames per superpose batch")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -313,15 +316,18 @@ def base_line(a, wl, n_gpus: int, dt: float, parallelism: str) -> dict:
 
 def main_single_process(a, wl, cpu) -> None:
     """``--gpus N`` with no WORLD_SIZE: one context per device, each device's
-    RMSF.py:65-69 block generated in its HBM, pushed from its own host
-    thread; the exchanges over ncclCommInitAll communicators (the in-process
-    fold for a --rehearse device list)."""
-    from concurrent.futures import ThreadPoolExecutor
-
+    RMSF.py:65-69 block generated in its HBM; every step pushes all blocks at
+    once (rmsf_multi_push_frames: one host thread per context, no host
+    synchronisation), then the contexts' merge -- the torchrun rank step's
+    shape: one collective of moments about frame 0 (unaligned) or the
+    reference (aligned), a reduce to context 0 with ``--merge root``
+    (RMSF.py:143), atom slabs from 1M atoms.  Exchanges over ncclCommInitAll
+    communicators; a --rehearse device list uses the in-process host fold, or
+    a no-op transport for host-cost timing."""
     import torch
 
     from rmsf_amd import parallel
-    from rmsf_amd.context import PUSH_ALIGN_SUM, PUSH_ALIGN_WELFORD, PUSH_WELFORD, Context
+    from rmsf_amd.context import (PUSH_ALIGN_SUM, PUSH_ALIGN_WELFORD, PUSH_WELFORD, TRANSPORT_NOOP, Context)
     from rmsf_amd.engine import Engine
     from rmsf_amd.synth import generate, motion_table
 
@@ -332,67 +338,70 @@ def main_single_process(a, wl, cpu) -> None:
     n_atoms, n_total, align = wl["n_atoms"], wl["n_total"], wl["align"]
     blocks = parallel.blocks(n_total, n)
     motion = motion_table(1, n_total) if align else None
-    ctxs, trajs, refs = [], [], []
+    ctxs, trajs, frame0 = [], [], []
     for d, (b0, b1) in zip(devs, blocks):
         with torch.cuda.device(d):
             eng = Engine(torch.device("cuda", d))
             trajs.append(generate(eng, n_atoms, b0, b1 - b0, seed=0, motion=motion))
-            # every rank reads frame 0 itself (RMSF.py:80-87): an input, like the block
-            refs.append(generate(eng, n_atoms, 0, 1, seed=0, motion=motion) if align else None)
+            # every rank reads frame 0 itself (RMSF.py:80-87): an input, like
+            # the block -- the reference (aligned) or the merge's shift
+            frame0.append(generate(eng, n_atoms, 0, 1, seed=0, motion=motion)[0])
             torch.cuda.synchronize(d)
         c = Context(n_atoms, device=d)
         c.set_timing(True)
         ctxs.append(c)
     if not rehearsal and n > 1:
         Context.init_all(ctxs)
-    pool = ThreadPoolExecutor(n)
-
-    def each(fn):
-        for f in [pool.submit(fn, i) for i in range(n)]:
-            f.result()
+    noop = rehearsal and a.rehearse_transport == "noop"
+    if noop:
+        Context.multi_set_transport(ctxs, TRANSPORT_NOOP)
+    root = 0 if (a.merge == "root" and n > 1) else None
+    slabs = 0 if a.merge_slabs is None else max(1, a.merge_slabs)   # C ABI: 0 = auto, 1 = off
+    kw = dict(after_torch=False)  # the blocks were generated and synchronised above
 
     def step():
-        def sweep1(i):
-            c = ctxs[i]
-            c.reset()
-            if align:
-                c.set_reference_frame(refs[i][0])
-            if align == "average":
-                c.push(trajs[i], PUSH_ALIGN_SUM)                            # RMSF.py:89-105
-            else:
-                c.push(trajs[i], PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD)
-
-        each(sweep1)
         if align == "average":
-            Context.multi_allreduce_sum(ctxs)                               # RMSF.py:107-110
-
-            def sweep2(i):
-                ctxs[i].set_reference_average()                             # RMSF.py:111-118
-                ctxs[i].push(trajs[i], PUSH_ALIGN_WELFORD)                  # RMSF.py:120-138
-            each(sweep2)
-        Context.multi_chan_merge(ctxs)                                      # RMSF.py:140-143
-        return ctxs[0].rmsf()                                               # RMSF.py:145-146
+            Context.multi_push_frames(ctxs, trajs, PUSH_ALIGN_SUM, ref_frames=frame0, **kw)   # RMSF.py:80-105
+            Context.multi_allreduce_sum(ctxs)                                                 # RMSF.py:107-110
+            for c in ctxs:
+                c.set_reference_average()                                                     # RMSF.py:111-118
+            Context.multi_push_frames(ctxs, trajs, PUSH_ALIGN_WELFORD, **kw)                  # RMSF.py:120-138
+        elif align == "frame0":
+            Context.multi_push_frames(ctxs, trajs, PUSH_ALIGN_WELFORD, ref_frames=frame0, **kw)
+        else:
+            Context.multi_push_frames(ctxs, trajs, PUSH_WELFORD, shift_frames=frame0 if n > 1 else None,
+                                      merge_slabs=slabs, **kw)
+        Context.multi_chan_merge(ctxs, root=root)                                             # RMSF.py:140-143
+        # RMSF.py:145-146: finalised in the merge (n > 1) / by rmsf() below
 
     for _ in range(a.warmup):
         step()
-    for c in ctxs:  # drop the warm-up's launch records
+    for c in ctxs:  # drop the warm-up's launch records (synchronises)
         c.kernel_time("accumulate"), c.kernel_time("superpose")
+        c.synchronize()
     t0 = time.perf_counter()
+    host_s = 0.0
     for _ in range(a.steps):
-        rmsf = step()
+        h0 = time.perf_counter()
+        step()
+        host_s += time.perf_counter() - h0
     for c in ctxs:
         c.synchronize()
     dt = time.perf_counter() - t0
     acc = [c.kernel_time("accumulate") for c in ctxs]
     sup = [c.kernel_time("superpose") for c in ctxs]
-    par = (f"one process, {n} device contexts (RMSF.py:65-69 blocks), "
-           + ("REHEARSAL: device 0 listed %d times, in-process fold" % n if rehearsal
-              else "RCCL via ncclCommInitAll") + ", exact k-way Chan merge")
+    rmsf = ctxs[root or 0].rmsf()
+    transport = ("REHEARSAL: device 0 listed %d times, %s" % (n, "no-op exchanges (host-cost timing; the merged "
+                 "result is not global)" if noop else "in-process host fold") if rehearsal
+                 else "RCCL via ncclCommInitAll")
+    par = f"one process, {n} device contexts (RMSF.py:65-69 blocks), {transport}, exact k-way Chan merge"
     out = base_line(a, wl, n, dt, par)
     out["devices"] = devs
     out["rehearsal"] = rehearsal
-    if n > 1:  # the context ABI's merge (rmsf_multi_chan_merge) leaves the result on every device
-        out["config"]["merge"] = "all-reduce (one-process contexts; --merge applies to the torchrun form)"
+    out["host_enqueue_ms_per_step"] = host_s / a.steps * 1e3
+    if n > 1:
+        out["config"]["merge"] = ("reduce to context 0 (RMSF.py:143)" if root == 0 else "all-reduce") + \
+            " of moments about a common shift (one collective)"
     kname = ("k_accum_split_sk" if align else "k_welford_flat_sk")
     out["roofline"] = rank_roofline(kname, acc)
     if align:
@@ -402,7 +411,6 @@ def main_single_process(a, wl, cpu) -> None:
     out["cpu_baseline"] = cpu
     out["rmsf_checksum"] = float(rmsf.sum())
     print(json.dumps(out), flush=True)
-    pool.shutdown()
     for c in ctxs:
         c.close()
 

@@ -615,6 +615,49 @@ int rmsf_multi_init_all(rmsf_ctx **ctxs, int n);
 int rmsf_multi_allreduce_sum(rmsf_ctx **ctxs, int n);
 int rmsf_multi_chan_merge(rmsf_ctx **ctxs, int n);
 
+/* ---- one process, several contexts: the torchrun rank step's shape --------
+ * The merge's shift for UNALIGNED Welford state (RMSF.py:141-143 as one
+ * collective of moments about a shift every rank holds; aligned state uses
+ * the reference): frame 0 of the frame list, n_atoms float32 atoms, host or
+ * device pointer; the context keeps its selected rows (f32) and a digest.
+ * rmsf_multi_chan_merge[_root] merges unaligned contexts in one collective
+ * when all hold the same shift frame, else in the two-pass form.           */
+int rmsf_set_merge_shift_frame(rmsf_ctx *ctx, const float *xyz,
+                               int is_device_ptr);
+/* rmsf_multi_chan_merge with RMSF.py:143's shape: root >= 0 reduces the
+ * moments to context `root` only (half the link bytes of an all-reduce);
+ * the other contexts then refuse rmsf_get_rmsf / rmsf_get_partial with
+ * RMSF_EINVAL until they are reset.  root = -1: every context gets the
+ * result (rmsf_multi_chan_merge).  Only the one-collective (shifted) merge
+ * can reduce to a root; the two-pass form leaves the result everywhere.
+ * Replaces RMSF.py:140-143 (comm.Barrier + comm.reduce(root=0)).           */
+int rmsf_multi_chan_merge_root(rmsf_ctx **ctxs, int n, int root);
+/* Push each context's HBM frames d_frames[i] (n_frames[i] frames,
+ * frame_stride floats apart, 0 = 3*n_atoms) in `mode`, the n contexts'
+ * launches enqueued from one host thread per context (asynchronous: the
+ * frames must stay valid until the contexts are synchronised).  Per context,
+ * first: flags & RMSF_MULTI_RESET resets the state `mode` accumulates into;
+ * d_ref_frames[i] (device frame, may be NULL) sets the reference
+ * (rmsf_set_reference_frame); d_shift_frames[i] the merge shift frame.
+ * merge_slabs (unaligned Welford, no selection, one launch group whose flat
+ * plan is chunk-aligned, a shift frame set, fresh state): 0 = auto (2 slabs
+ * from 1M atoms, as the torchrun pipeline), 1 = off, k >= 2 = k slabs -- the
+ * push is then recorded, and the next rmsf_multi_chan_merge_root streams it
+ * slab by slab with each slab's collective (on a communicator stream, RCCL)
+ * beside the next slab's accumulate; any other call runs it whole.          */
+#define RMSF_MULTI_RESET 1
+int rmsf_multi_push_frames(rmsf_ctx **ctxs, int n, const float *const *d_frames,
+                           const int64_t *n_frames, int64_t frame_stride,
+                           int mode, int flags, const float *const *d_ref_frames,
+                           const float *const *d_shift_frames, int merge_slabs);
+/* Transport of the contexts' exchanges: AUTO = RCCL when every context has a
+ * communicator, else the in-process host fold; NOOP = a timing rehearsal of
+ * N contexts on fewer devices -- the exchanges move no data, so the merged
+ * statistics are NOT the global ones (measurement only).                    */
+#define RMSF_TRANSPORT_AUTO 0
+#define RMSF_TRANSPORT_NOOP 1
+int rmsf_multi_set_transport(rmsf_ctx **ctxs, int n, int transport);
+
 #ifdef __cplusplus
 }
 #endif

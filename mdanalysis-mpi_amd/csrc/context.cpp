@@ -18,11 +18,13 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
 #include <functional>
 #include <mutex>
-#include <type_traits>
 #include <string>
+#include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "rmsf_hip.h"
@@ -48,6 +50,8 @@ int fail(int code, const std::string &m) { return rmsf_internal_set_error(code, 
   } while (0)
 
 constexpr int64_t kChunkFrames = 16384;         // frames per superpose/accumulate launch group
+constexpr int64_t kSlabMinAtoms = 1000000;      // auto atom slabs from 1M atoms (pipeline.SLAB_MIN_ATOMS)
+constexpr int kSlabsAuto = 2;                   // pipeline.SLABS_AUTO
 constexpr int64_t kStageBytes = 64ll << 20;     // default pinned slot size
 
 // ---- RCCL, resolved at first use (the library torch already loaded, if any,
@@ -59,6 +63,8 @@ struct Rccl {
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
   ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                             hipStream_t) = nullptr;
+  ncclResult_t (*Reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, int, ncclComm_t,
+                         hipStream_t) = nullptr;
   ncclResult_t (*GroupStart)() = nullptr;
   ncclResult_t (*GroupEnd)() = nullptr;
   const char *(*GetErrorString)(ncclResult_t) = nullptr;
@@ -86,6 +92,7 @@ const Rccl &rccl() {
     sym(r.CommInitAll, "ncclCommInitAll");
     sym(r.CommDestroy, "ncclCommDestroy");
     sym(r.AllReduce, "ncclAllReduce");
+    sym(r.Reduce, "ncclReduce");
     sym(r.GroupStart, "ncclGroupStart");
     sym(r.GroupEnd, "ncclGroupEnd");
     sym(r.GetErrorString, "ncclGetErrorString");
@@ -144,6 +151,66 @@ struct DevBuf {
 struct Running {
   DevBuf parts0, parts1;
   int64_t n = 0;
+  bool stale = false;  // reset lazily: zeroed only if read before a fold overwrites it
+};
+
+// One host thread per context for the multi-context calls
+// (rmsf_multi_push_frames, the slab merge): each context's launches are
+// enqueued from its own thread, so N devices start their sweeps together
+// instead of one after another behind a single thread's launch latency.
+struct Worker {
+  std::thread th;
+  std::mutex m;
+  std::condition_variable cv;
+  std::function<int()> job;
+  bool has = false, done = true, quit = false;
+  int rc = 0;
+  std::string err;
+  Worker() : th([this] { loop(); }) {}
+  ~Worker() {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      quit = true;
+    }
+    cv.notify_all();
+    th.join();
+  }
+  void loop() {
+    for (;;) {
+      std::function<int()> j;
+      {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return has || quit; });
+        if (!has) return;
+        j = std::move(job);
+        has = false;
+      }
+      const int r = j();
+      std::string e = r ? std::string(rmsf_last_error()) : std::string();
+      {
+        std::lock_guard<std::mutex> lk(m);
+        rc = r;
+        err = std::move(e);
+        done = true;
+      }
+      cv.notify_all();
+    }
+  }
+  void post(std::function<int()> f) {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      job = std::move(f);
+      has = true;
+      done = false;
+    }
+    cv.notify_all();
+  }
+  int wait(std::string *e) {
+    std::unique_lock<std::mutex> lk(m);
+    cv.wait(lk, [&] { return done; });
+    *e = err;
+    return rc;
+  }
 };
 
 // Order-independent 64-bit digest of a reference structure: the bit patterns
@@ -160,13 +227,13 @@ __host__ __device__ inline uint64_t dig_mix(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-__global__ __launch_bounds__(256) void k_ref_digest(const uint64_t *__restrict__ ref, int64_t n,
-                                                    const uint64_t *__restrict__ info,
-                                                    unsigned long long *__restrict__ out) {
+template <class W>
+__global__ __launch_bounds__(256) void k_digest(const W *__restrict__ a, int64_t n, const uint64_t *__restrict__ info,
+                                                int64_t n_info, unsigned long long *__restrict__ out) {
   uint64_t acc = 0;
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n + 3; j += stride) {
-    const uint64_t w = j < n ? ref[j] : info[j - n];
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n + n_info; j += stride) {
+    const uint64_t w = j < n ? (uint64_t)a[j] : info[j - n];
     acc += dig_mix(w ^ dig_mix((uint64_t)j));
   }
 #pragma unroll
@@ -207,6 +274,40 @@ struct rmsf_ctx {
   bool collect_rmsd = false;
   DevBuf rmsd;
   int64_t n_rmsd = 0;
+  // the merge's shift for unaligned Welford state (rmsf_set_merge_shift_frame):
+  // a selected frame, f32 [n_sel][3], with its digest
+  DevBuf shift, zidx, shiftdig;
+  bool shift_set = false, zidx_set = false;
+  // each digest is also copied to pinned host memory, an event after it: the
+  // merge reads it without waiting for the sweep queued behind the setter
+  unsigned long long *h_dig[2] = {nullptr, nullptr};  // [reference, shift frame]
+  hipEvent_t ev_dig[2] = {nullptr, nullptr};
+  // side stream for the digests and the shift frame's gather: they run beside
+  // the sweep instead of in front of it (the merge waits for ev_dig[1])
+  hipStream_t side = nullptr;
+  hipEvent_t ev_main = nullptr;
+  bool wel_aligned = false;  // the Welford state came from aligned pushes
+  // the last balanced accumulate's fold, deferred until the state is next
+  // used, so a merge can fold and pack in one launch (rmsf_fold_balanced_shift)
+  struct PendingFold {
+    bool on = false, welford = false;
+    int mode_k = 0;
+    int64_t acc_n = 0;
+  } pend;
+  // a device push recorded by rmsf_multi_push_frames for the atom-slab merge
+  // (run by the next rmsf_multi_chan_merge_root, or whole by any other call)
+  struct SlabPush {
+    bool on = false;
+    const float *d = nullptr;
+    int64_t stride = 0, n_frames = 0, chunks = 0;
+    int k = 0;
+  } slab;
+  bool merged_away = false;  // a reduce-to-root merge left the result on another context
+  bool rmsf_valid = false;   // rmsf holds the finalised result of the current state
+  int transport = RMSF_TRANSPORT_AUTO;
+  hipStream_t comm_stream = nullptr;  // the slab merge's RCCL calls (beside the next slab)
+  std::vector<hipEvent_t> ev_pack, ev_done;
+  Worker *worker = nullptr;
 
   const int32_t *d_sel() const { return h_sel.empty() ? nullptr : static_cast<const int32_t *>(sel.p); }
   const double *d_masses() const { return has_masses ? masses.d() : nullptr; }
@@ -228,6 +329,14 @@ int zero_running(rmsf_ctx *c, Running &r, bool two) {
     CX_HIP(hipMemsetAsync(r.parts1.p, 0, row, c->stream));
   }
   r.n = 0;
+  r.stale = false;
+  return RMSF_OK;
+}
+
+// A reset state is zeroed only when it is read with no frame folded in (an
+// empty block): the first balanced fold of a push overwrites it otherwise.
+int ensure_zeroed(rmsf_ctx *c, Running &r, bool two) {
+  if (r.parts0.bytes == 0 || (r.n == 0 && r.stale)) return zero_running(c, r, two);
   return RMSF_OK;
 }
 
@@ -261,10 +370,21 @@ void drop_spans(rmsf_ctx *c, int which) {
   c->spans.swap(keep);
 }
 
-// one launch group over n_frames device frames: [superpose] + accumulate + fold
+// the deferred fold of the last accumulate (plain: into the running state)
+int flush_fold(rmsf_ctx *c) {
+  if (!c->pend.on) return RMSF_OK;
+  c->pend.on = false;
+  Running &r = c->pend.welford ? c->wel : c->sum;
+  return rmsf_fold_balanced(c->accwork.p, c->n_coord, c->pend.mode_k, c->pend.acc_n, r.parts0.d(),
+                            c->pend.welford ? r.parts1.d() : nullptr, c->stream);
+}
+
+// one launch group over n_frames device frames: [superpose] + accumulate; its
+// fold is deferred (flush_fold / the merge's fused fold + pack)
 int process(rmsf_ctx *c, const float *d_xyz, int64_t stride, int64_t n_frames, const int32_t *d_sel, int mode) {
   const bool aligned = mode == RMSF_PUSH_ALIGN_SUM || mode == RMSF_PUSH_ALIGN_WELFORD;
   const bool welford = mode == RMSF_PUSH_WELFORD || mode == RMSF_PUSH_ALIGN_WELFORD;
+  CX_OK(flush_fold(c));  // the workspace is about to be rewritten
   const double *xf = nullptr;
   if (aligned) {
     if (!c->ref_set) return fail(RMSF_EINVAL, "rmsf_push: aligned mode before a reference was set");
@@ -299,37 +419,92 @@ int process(rmsf_ctx *c, const float *d_xyz, int64_t stride, int64_t n_frames, c
                                     aligned ? c->refinfo.d() : nullptr, mode_k, 0, c->accwork.p, c->accwork.bytes,
                                     c->stream);
   }));
-  CX_OK(rmsf_fold_balanced(c->accwork.p, c->n_coord, mode_k, r.n, r.parts0.d(), welford ? r.parts1.d() : nullptr,
-                           c->stream));
+  c->pend.on = true;
+  c->pend.welford = welford;
+  c->pend.mode_k = mode_k;
+  c->pend.acc_n = r.n;
   r.n += n_frames;
+  r.stale = false;  // the (deferred) fold with acc_n = 0 overwrites the state
+  if (welford) {
+    c->wel_aligned = aligned;
+    c->rmsf_valid = false;
+    c->merged_away = false;
+  }
   return RMSF_OK;
 }
 
-// queue the digest of the context's current reference (after every setter)
-int digest_reference(rmsf_ctx *c) {
-  CX_OK(c->refdig.ensure(sizeof(unsigned long long), c->stream));
-  CX_HIP(hipMemsetAsync(c->refdig.p, 0, sizeof(unsigned long long), c->stream));
-  const int64_t n = c->n_coord;
-  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (n + 3 + 1023) / 1024));
-  hipLaunchKernelGGL(k_ref_digest, dim3(blocks), dim3(256), 0, c->stream, static_cast<const uint64_t *>(c->ref.p), n,
-                     static_cast<const uint64_t *>(c->refinfo.p), static_cast<unsigned long long *>(c->refdig.p));
+// a recorded slab push that no slab merge consumed runs whole
+int flush_slab(rmsf_ctx *c) {
+  if (!c->slab.on) return RMSF_OK;
+  c->slab.on = false;
+  return process(c, c->slab.d, c->slab.stride, c->slab.n_frames, c->d_sel(), RMSF_PUSH_WELFORD);
+}
+
+// everything queued for the running state is in it
+int settle(rmsf_ctx *c) {
+  CX_OK(flush_slab(c));
+  return flush_fold(c);
+}
+
+// order the side stream after everything queued on the context stream so far
+int side_begin(rmsf_ctx *c) {
+  if (!c->side) CX_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+  if (!c->ev_main) CX_HIP(hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming));
+  CX_HIP(hipEventRecord(c->ev_main, c->stream));
+  CX_HIP(hipStreamWaitEvent(c->side, c->ev_main, 0));
+  return RMSF_OK;
+}
+
+// queue, on the side stream (after side_begin), the digest of a reference
+// (which = 0) or merge shift frame (1), its copy to pinned host memory and an
+// event after them
+int digest_into(rmsf_ctx *c, int which, const void *a, bool words32, int64_t n, const void *info, int64_t n_info) {
+  DevBuf &out = which ? c->shiftdig : c->refdig;
+  CX_OK(out.ensure(sizeof(unsigned long long), c->side));
+  if (!c->h_dig[which]) {
+    void *h = nullptr;
+    CX_HIP(hipHostMalloc(&h, sizeof(unsigned long long), hipHostMallocDefault));
+    c->h_dig[which] = static_cast<unsigned long long *>(h);
+  }
+  if (!c->ev_dig[which]) CX_HIP(hipEventCreateWithFlags(&c->ev_dig[which], hipEventDisableTiming));
+  CX_HIP(hipMemsetAsync(out.p, 0, sizeof(unsigned long long), c->side));
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (n + n_info + 1023) / 1024));
+  auto *o = static_cast<unsigned long long *>(out.p);
+  auto *in = static_cast<const uint64_t *>(info);
+  if (words32)
+    hipLaunchKernelGGL(k_digest<uint32_t>, dim3(blocks), dim3(256), 0, c->side, static_cast<const uint32_t *>(a), n,
+                       in, n_info, o);
+  else
+    hipLaunchKernelGGL(k_digest<uint64_t>, dim3(blocks), dim3(256), 0, c->side, static_cast<const uint64_t *>(a), n,
+                       in, n_info, o);
   CX_HIP(hipGetLastError());
+  CX_HIP(hipMemcpyAsync(c->h_dig[which], out.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->side));
+  CX_HIP(hipEventRecord(c->ev_dig[which], c->side));
   return RMSF_OK;
 }
 
-// true when every context holds a reference with the same digest
-int same_references(rmsf_ctx **cs, int n, bool *same) {
+// queue the digest of the context's current reference (after every setter):
+// the centred reference and its COM, what the shifted merge uses as its shift
+int digest_reference(rmsf_ctx *c) {
+  CX_OK(side_begin(c));
+  return digest_into(c, 0, c->ref.p, false, c->n_coord, c->refinfo.p, 3);
+}
+
+// true when every context holds a reference (shift = false) or a merge shift
+// frame (shift = true) with the same digest; waits for the digests only
+int same_digests(rmsf_ctx **cs, int n, bool shift, bool *same) {
   *same = true;
   unsigned long long d0 = 0;
+  const int w = shift ? 1 : 0;
   for (int i = 0; i < n; ++i) {
-    if (!cs[i]->ref_set || !cs[i]->refdig.p) {
+    const bool set = shift ? cs[i]->shift_set : cs[i]->ref_set;
+    if (!set || !cs[i]->ev_dig[w]) {
       *same = false;
       return RMSF_OK;
     }
     DeviceScope ds(cs[i]->dev);
-    unsigned long long d = 0;
-    CX_HIP(hipMemcpyAsync(&d, cs[i]->refdig.p, sizeof d, hipMemcpyDeviceToHost, cs[i]->stream));
-    CX_HIP(hipStreamSynchronize(cs[i]->stream));
+    CX_HIP(hipEventSynchronize(cs[i]->ev_dig[w]));
+    const unsigned long long d = *cs[i]->h_dig[w];
     if (i == 0) d0 = d;
     else if (d != d0) *same = false;
   }
@@ -356,10 +531,33 @@ int ensure_stager(rmsf_ctx *c) {
   return RMSF_OK;
 }
 
+// fn(i) for every context, each on its own worker thread (context 0 on the
+// calling thread); the first failure is reported on the calling thread.
+int for_each_ctx(rmsf_ctx **cs, int n, const std::function<int(int)> &fn) {
+  if (n == 1) return fn(0);
+  for (int i = 1; i < n; ++i) {
+    if (!cs[i]->worker) cs[i]->worker = new (std::nothrow) Worker;
+    if (!cs[i]->worker) return fail(RMSF_ENOMEM, "rmsf_multi: cannot start a worker thread");
+    cs[i]->worker->post([&fn, i] { return fn(i); });
+  }
+  int rc = fn(0);
+  std::string msg = rc ? std::string(rmsf_last_error()) : std::string();
+  for (int i = 1; i < n; ++i) {
+    std::string e;
+    const int r = cs[i]->worker->wait(&e);
+    if (r && !rc) {
+      rc = r;
+      msg = e;
+    }
+  }
+  return rc ? fail(rc, msg) : RMSF_OK;
+}
+
 // ---- cross-rank exchange ----------------------------------------------------
-// reduce(count, bufs): sum bufs[i][0..count) over all ranks, in place, for the
-// n local contexts (each buffer on its context's stream).
-using Reduce = std::function<int(int64_t, double *const *)>;
+// reduce(count, bufs, root): sum bufs[i][0..count) over all ranks, in place,
+// for the n local contexts (each buffer on its context's stream); root >= 0:
+// only that rank's buffer must hold the sum afterwards.
+using Reduce = std::function<int(int64_t, double *const *, int)>;
 
 // The contexts of this process are every rank of the exchange (RCCL
 // communicators of size n from rmsf_multi_init_all, or no communicator at
@@ -387,7 +585,7 @@ int count_exchange(rmsf_ctx **cs, int n, const Reduce &red, const std::vector<in
     CX_HIP(hipStreamSynchronize(cs[i]->stream));
     bufs[i] = cs[i]->cnt.d();
   }
-  CX_OK(red(1, bufs.data()));
+  CX_OK(red(1, bufs.data(), -1));
   double t = 0.0;
   for (int i = 0; i < n; ++i) {
     DeviceScope ds(cs[i]->dev);
@@ -404,17 +602,16 @@ int count_exchange(rmsf_ctx **cs, int n, const Reduce &red, const std::vector<in
 int exchange_sum(rmsf_ctx **cs, int n, const Reduce &red, bool host_counts) {
   std::vector<int64_t> local(n);
   for (int i = 0; i < n; ++i) {
-    if (cs[i]->sum.parts0.bytes == 0) {
-      DeviceScope ds(cs[i]->dev);
-      CX_OK(zero_running(cs[i], cs[i]->sum, false));
-    }
+    DeviceScope ds(cs[i]->dev);
+    CX_OK(settle(cs[i]));
+    CX_OK(ensure_zeroed(cs[i], cs[i]->sum, false));
     local[i] = cs[i]->sum.n;
   }
   int64_t total = 0;
   CX_OK(count_exchange(cs, n, red, local, &total, host_counts));
   std::vector<double *> bufs(n);
   for (int i = 0; i < n; ++i) bufs[i] = cs[i]->sum.parts0.d();
-  CX_OK(red(cs[0]->n_coord, bufs.data()));
+  CX_OK(red(cs[0]->n_coord, bufs.data(), -1));
   for (int i = 0; i < n; ++i) cs[i]->sum.n = total;
   return RMSF_OK;
 }
@@ -422,10 +619,9 @@ int exchange_sum(rmsf_ctx **cs, int n, const Reduce &red, bool host_counts) {
 int exchange_chan(rmsf_ctx **cs, int n, const Reduce &red, bool host_counts) {
   std::vector<int64_t> local(n);
   for (int i = 0; i < n; ++i) {
-    if (cs[i]->wel.parts0.bytes == 0) {
-      DeviceScope ds(cs[i]->dev);
-      CX_OK(zero_running(cs[i], cs[i]->wel, true));
-    }
+    DeviceScope ds(cs[i]->dev);
+    CX_OK(settle(cs[i]));
+    CX_OK(ensure_zeroed(cs[i], cs[i]->wel, true));
     local[i] = cs[i]->wel.n;
   }
   int64_t total = 0;
@@ -443,7 +639,7 @@ int exchange_chan(rmsf_ctx **cs, int n, const Reduce &red, bool host_counts) {
     a[i] = c->xa.d();
     b[i] = c->xb.d();
   }
-  CX_OK(red(nc, a.data()));
+  CX_OK(red(nc, a.data(), -1));
   // step 2: global M2 = sum_k M2_k + n_k (mean_k - mean)^2
   for (int i = 0; i < n; ++i) {
     rmsf_ctx *c = cs[i];
@@ -451,29 +647,54 @@ int exchange_chan(rmsf_ctx **cs, int n, const Reduce &red, bool host_counts) {
     CX_OK(rmsf_chan_deviation(c->wel.parts0.d(), c->wel.parts1.d(), c->xa.d(), (double)local[i], nc, c->xb.d(),
                               c->stream));
   }
-  CX_OK(red(nc, b.data()));
+  CX_OK(red(nc, b.data(), -1));
   for (int i = 0; i < n; ++i) {
     rmsf_ctx *c = cs[i];
     DeviceScope ds(c->dev);
     CX_HIP(hipMemcpyAsync(c->wel.parts0.p, c->xa.p, sizeof(double) * nc, hipMemcpyDeviceToDevice, c->stream));
     CX_HIP(hipMemcpyAsync(c->wel.parts1.p, c->xb.p, sizeof(double) * nc, hipMemcpyDeviceToDevice, c->stream));
     c->wel.n = total;
+    c->rmsf_valid = false;
   }
   return RMSF_OK;
 }
 
-// The same merge in ONE data all-reduce (rmsf_chan_shift_pack/_finish):
-// moments about the contexts' common reference structure (centred reference
-// + its COM), which every rank of RMSF.py holds identically (the frame-0
-// reference, RMSF.py:80-87, or the average, :113-118).  The caller
-// guarantees that every context of the exchange holds the same reference.
-int exchange_chan_shifted(rmsf_ctx **cs, int n, const Reduce &red, bool host_counts) {
+// What the one-collective merge shifts the moments by: the contexts' common
+// reference structure (centred reference + its COM), which every rank of
+// RMSF.py holds identically (the frame-0 reference, RMSF.py:80-87, or the
+// average, :113-118), or -- unaligned Welford state -- a common merge shift
+// frame (rmsf_set_merge_shift_frame: frame 0 of the frame list, f32).
+enum class Shift { REF, FRAME };
+
+struct ShiftArgs {
+  const void *p;
+  int f32;
+  const double *off3;
+};
+
+ShiftArgs shift_of(rmsf_ctx *c, Shift kind) {
+  if (kind == Shift::REF) return {c->ref.p, 0, c->refinfo.d()};
+  return {c->shift.p, 1, nullptr};
+}
+
+// The k-way Chan merge in ONE data collective (rmsf_chan_shift_pack/_finish):
+// T1 = sum n_k (mean_k - c), T2 = sum M2_k + n_k (mean_k - c)^2 about the
+// common shift c.  A context whose last fold is still deferred folds and
+// packs in one launch (rmsf_fold_balanced_shift).  root >= 0: a reduce to
+// that context (RMSF.py:143); the others are left `merged_away`.  The caller
+// guarantees that every context holds the same shift.
+int exchange_chan_shifted(rmsf_ctx **cs, int n, const Reduce &red, bool host_counts, Shift kind, int root) {
   std::vector<int64_t> local(n);
   for (int i = 0; i < n; ++i) {
-    if (!cs[i]->ref_set) return fail(RMSF_EINVAL, "rmsf shifted chan merge: a context holds no reference");
-    if (cs[i]->wel.parts0.bytes == 0) {
-      DeviceScope ds(cs[i]->dev);
-      CX_OK(zero_running(cs[i], cs[i]->wel, true));
+    if (kind == Shift::REF && !cs[i]->ref_set)
+      return fail(RMSF_EINVAL, "rmsf shifted chan merge: a context holds no reference");
+    if (kind == Shift::FRAME && !cs[i]->shift_set)
+      return fail(RMSF_EINVAL, "rmsf shifted chan merge: a context holds no merge shift frame");
+    DeviceScope ds(cs[i]->dev);
+    CX_OK(flush_slab(cs[i]));
+    if (!(cs[i]->pend.on && cs[i]->pend.welford)) {
+      CX_OK(flush_fold(cs[i]));
+      CX_OK(ensure_zeroed(cs[i], cs[i]->wel, true));
     }
     local[i] = cs[i]->wel.n;
   }
@@ -485,24 +706,41 @@ int exchange_chan_shifted(rmsf_ctx **cs, int n, const Reduce &red, bool host_cou
   for (int i = 0; i < n; ++i) {
     rmsf_ctx *c = cs[i];
     DeviceScope ds(c->dev);
+    const ShiftArgs sh = shift_of(c, kind);
     CX_OK(c->xa.ensure(sizeof(double) * 2 * nc, c->stream));
-    CX_OK(rmsf_chan_shift_pack(c->wel.parts0.d(), c->wel.parts1.d(), c->ref.d(), 0, c->refinfo.d(),
-                               (double)local[i], nc, c->xa.d(), c->stream));
+    if (kind == Shift::FRAME) CX_HIP(hipStreamWaitEvent(c->stream, c->ev_dig[1], 0));  // the side gather
+    if (c->pend.on && c->pend.welford) {  // fold + pack, one launch
+      c->pend.on = false;
+      CX_OK(rmsf_fold_balanced_shift(c->accwork.p, nc, c->pend.acc_n, c->wel.parts0.d(), c->wel.parts1.d(), sh.p,
+                                     sh.f32, sh.off3, c->xa.d(), c->stream));
+    } else {
+      CX_OK(rmsf_chan_shift_pack(c->wel.parts0.d(), c->wel.parts1.d(), sh.p, sh.f32, sh.off3, (double)local[i], nc,
+                                 c->xa.d(), c->stream));
+    }
     t[i] = c->xa.d();
   }
-  CX_OK(red(2 * nc, t.data()));
+  CX_OK(red(2 * nc, t.data(), root));
   for (int i = 0; i < n; ++i) {
     rmsf_ctx *c = cs[i];
+    if (root >= 0 && i != root) {
+      c->merged_away = true;
+      c->rmsf_valid = false;
+      continue;
+    }
     DeviceScope ds(c->dev);
-    CX_OK(rmsf_chan_shift_finish(c->xa.d(), c->ref.d(), 0, c->refinfo.d(), c->n_sel, total, c->wel.parts0.d(),
-                                 c->wel.parts1.d(), nullptr, c->stream));
+    const ShiftArgs sh = shift_of(c, kind);
+    CX_OK(c->rmsf.ensure(sizeof(double) * c->n_sel, c->stream));
+    CX_OK(rmsf_chan_shift_finish(c->xa.d(), sh.p, sh.f32, sh.off3, c->n_sel, total, c->wel.parts0.d(),
+                                 c->wel.parts1.d(), c->rmsf.d(), c->stream));
     c->wel.n = total;
+    c->rmsf_valid = true;
+    c->merged_away = false;
   }
   return RMSF_OK;
 }
 
 Reduce callback_reduce(rmsf_ctx *c, rmsf_allreduce_fn fn, void *user) {
-  return [c, fn, user](int64_t count, double *const *bufs) -> int {
+  return [c, fn, user](int64_t count, double *const *bufs, int) -> int {
     DeviceScope ds(c->dev);
     int rc = fn(bufs[0], count, (void *)c->stream, user);
     if (rc != 0) return fail(RMSF_EINVAL, "allreduce callback returned " + std::to_string(rc));
@@ -510,28 +748,37 @@ Reduce callback_reduce(rmsf_ctx *c, rmsf_allreduce_fn fn, void *user) {
   };
 }
 
-Reduce rccl_reduce(rmsf_ctx **cs, int n) {
-  return [cs, n](int64_t count, double *const *bufs) -> int {
-    const Rccl &r = rccl();
-    ncclResult_t e = r.GroupStart();
-    if (e != ncclSuccess) return nccl_fail("ncclGroupStart", e);
-    for (int i = 0; i < n; ++i) {
-      DeviceScope ds(cs[i]->dev);
-      e = r.AllReduce(bufs[i], bufs[i], (size_t)count, ncclFloat64, ncclSum, cs[i]->comm, cs[i]->stream);
-      if (e != ncclSuccess) {
-        (void)r.GroupEnd();
-        return nccl_fail("ncclAllReduce", e);
-      }
+// one RCCL collective per context on `streams[i]` (the context streams, or
+// the slab merge's comm streams), grouped: one thread drives every device
+int rccl_collective(rmsf_ctx **cs, int n, int64_t count, double *const *bufs, int root, const hipStream_t *streams) {
+  const Rccl &r = rccl();
+  ncclResult_t e = r.GroupStart();
+  if (e != ncclSuccess) return nccl_fail("ncclGroupStart", e);
+  for (int i = 0; i < n; ++i) {
+    DeviceScope ds(cs[i]->dev);
+    e = root < 0 ? r.AllReduce(bufs[i], bufs[i], (size_t)count, ncclFloat64, ncclSum, cs[i]->comm, streams[i])
+                 : r.Reduce(bufs[i], bufs[i], (size_t)count, ncclFloat64, ncclSum, root, cs[i]->comm, streams[i]);
+    if (e != ncclSuccess) {
+      (void)r.GroupEnd();
+      return nccl_fail(root < 0 ? "ncclAllReduce" : "ncclReduce", e);
     }
-    e = r.GroupEnd();
-    if (e != ncclSuccess) return nccl_fail("ncclGroupEnd", e);
-    return RMSF_OK;
+  }
+  e = r.GroupEnd();
+  if (e != ncclSuccess) return nccl_fail("ncclGroupEnd", e);
+  return RMSF_OK;
+}
+
+Reduce rccl_reduce(rmsf_ctx **cs, int n) {
+  return [cs, n](int64_t count, double *const *bufs, int root) -> int {
+    std::vector<hipStream_t> st(n);
+    for (int i = 0; i < n; ++i) st[i] = cs[i]->stream;
+    return rccl_collective(cs, n, count, bufs, root, st.data());
   };
 }
 
 // contexts of one process, no communicator: fold on the host in context order
 Reduce local_reduce(rmsf_ctx **cs, int n) {
-  return [cs, n](int64_t count, double *const *bufs) -> int {
+  return [cs, n](int64_t count, double *const *bufs, int root) -> int {
     std::vector<double> acc((size_t)count, 0.0), tmp((size_t)count);
     for (int i = 0; i < n; ++i) {
       DeviceScope ds(cs[i]->dev);
@@ -540,6 +787,7 @@ Reduce local_reduce(rmsf_ctx **cs, int n) {
       for (int64_t j = 0; j < count; ++j) acc[j] += tmp[j];
     }
     for (int i = 0; i < n; ++i) {
+      if (root >= 0 && i != root) continue;
       DeviceScope ds(cs[i]->dev);
       CX_HIP(hipMemcpyAsync(bufs[i], acc.data(), sizeof(double) * count, hipMemcpyHostToDevice, cs[i]->stream));
       CX_HIP(hipStreamSynchronize(cs[i]->stream));
@@ -548,20 +796,153 @@ Reduce local_reduce(rmsf_ctx **cs, int n) {
   };
 }
 
-int multi_reduce(rmsf_ctx **cs, int n, const char *fn, Reduce *out) {
+// timing rehearsal (RMSF_TRANSPORT_NOOP): the exchanges move nothing
+Reduce noop_reduce() {
+  return [](int64_t, double *const *, int) -> int { return RMSF_OK; };
+}
+
+int multi_reduce(rmsf_ctx **cs, int n, const char *fn, Reduce *out, int *kind = nullptr) {
   if (!cs || n <= 0) return fail(RMSF_EINVAL, std::string(fn) + ": no contexts");
-  int with = 0;
+  int with = 0, noop = 0;
   for (int i = 0; i < n; ++i) {
     CX_OK(check_ctx(cs[i], fn));
     if (cs[i]->n_coord != cs[0]->n_coord) return fail(RMSF_EINVAL, std::string(fn) + ": contexts differ in n_sel");
+    for (int j = 0; j < i; ++j)
+      if (cs[j] == cs[i]) return fail(RMSF_EINVAL, std::string(fn) + ": a context is listed twice");
     with += cs[i]->comm != nullptr;
+    noop += cs[i]->transport == RMSF_TRANSPORT_NOOP;
   }
-  if (with == n) {
+  if (noop && noop != n) return fail(RMSF_EINVAL, std::string(fn) + ": mixed transports");
+  int k = 0;
+  if (noop) {
+    *out = noop_reduce();
+    k = 2;
+  } else if (with == n) {
     *out = rccl_reduce(cs, n);
+    k = 1;
   } else if (with == 0) {
     *out = local_reduce(cs, n);
   } else {
     return fail(RMSF_EINVAL, std::string(fn) + ": some contexts have an RCCL communicator and some do not");
+  }
+  if (kind) *kind = k;
+  return RMSF_OK;
+}
+
+// k atom slabs of a flat plan's chunks, cut at multiples of 3 chunks (3 x 1024
+// coordinates = whole atoms) -- pipeline._slab_bounds
+std::vector<std::pair<int64_t, int64_t>> slab_bounds(int64_t n_chunks, int k) {
+  std::vector<int64_t> cuts;
+  for (int i = 1; i < k; ++i) {
+    double x = (double)i * (double)n_chunks / k / 3.0;
+    int64_t c = 3 * (int64_t)std::nearbyint(x);
+    c = std::min(n_chunks, std::max<int64_t>(0, c));
+    if (c > 0 && c < n_chunks && (cuts.empty() || cuts.back() != c)) cuts.push_back(c);
+  }
+  std::sort(cuts.begin(), cuts.end());
+  cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+  std::vector<std::pair<int64_t, int64_t>> out;
+  int64_t lo = 0;
+  for (int64_t c : cuts) {
+    out.push_back({lo, c});
+    lo = c;
+  }
+  out.push_back({lo, n_chunks});
+  return out;
+}
+
+// The recorded slab pushes of every context and the merge, slab by slab
+// (pipeline._slab_sweep): slab s's accumulate + fold-pack on each context
+// stream, then its collective -- RCCL: on the context's comm stream after an
+// event, so slab s+1 streams while slab s's reduce runs; host transports: in
+// turn -- and the finish of every slab.  Bit-identical per rank to the
+// unslabbed fold + pack (every slab replays the whole plan's segments).
+int slab_merge(rmsf_ctx **cs, int n, int kind, const Reduce &red, int root) {
+  const int64_t nc = cs[0]->n_coord;
+  const auto bounds = slab_bounds(cs[0]->slab.chunks, cs[0]->slab.k);
+  const size_t ns = bounds.size();
+  int64_t total = 0;
+  for (int i = 0; i < n; ++i) total += cs[i]->wel.n + cs[i]->slab.n_frames;
+  if (total == 0) return fail(RMSF_EEMPTY, "rmsf chan merge: no frames on any rank (RMSF.py:39 ZeroDivisionError)");
+  const bool rc_l = kind == 1;
+  CX_OK(for_each_ctx(cs, n, [&](int i) -> int {
+    rmsf_ctx *c = cs[i];
+    DeviceScope ds(c->dev);
+    CX_OK(flush_fold(c));
+    CX_OK(ensure_zeroed(c, c->wel, true));
+    const auto sp = c->slab;
+    c->slab.on = false;
+    const size_t wb = rmsf_accumulate_balanced_workspace_bytes(c->n_sel, sp.n_frames, 0);
+    CX_OK(c->accwork.ensure(std::max<size_t>(wb, 16), c->stream));
+    CX_OK(c->xa.ensure(sizeof(double) * 2 * nc, c->stream));
+    if (rc_l) {
+      if (!c->comm_stream) CX_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+      while (c->ev_pack.size() < ns) {
+        hipEvent_t a = nullptr, b = nullptr;
+        CX_HIP(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+        CX_HIP(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+        c->ev_pack.push_back(a);
+        c->ev_done.push_back(b);
+      }
+    }
+    for (size_t s = 0; s < ns; ++s) {
+      const int64_t c0 = bounds[s].first, c1 = bounds[s].second;
+      const int64_t j0 = 1024 * c0, j1 = std::min(1024 * c1, nc);
+      CX_OK(timed(c, RMSF_TIME_ACCUMULATE, sp.n_frames * (j1 - j0) / 3, [&] {
+        return rmsf_accumulate_balanced_slab(sp.d, sp.stride, sp.n_frames, c->n_sel, c0, c1, c->accwork.p,
+                                             c->accwork.bytes, c->stream);
+      }));
+      if (s == 0) CX_HIP(hipStreamWaitEvent(c->stream, c->ev_dig[1], 0));  // the side gather, before the first pack
+      CX_OK(rmsf_fold_balanced_shift_slab(c->accwork.p, nc, c->wel.n, c->wel.parts0.d(), c->wel.parts1.d(),
+                                          c->shift.p, 1, nullptr, c->xa.d() + 2 * j0, c0, c1, c->stream));
+      if (rc_l) CX_HIP(hipEventRecord(c->ev_pack[s], c->stream));
+    }
+    c->wel.n += sp.n_frames;
+    c->wel.stale = false;
+    c->wel_aligned = false;
+    return RMSF_OK;
+  }));
+  std::vector<double *> bufs(n);
+  std::vector<hipStream_t> st(n);
+  for (size_t s = 0; s < ns; ++s) {
+    const int64_t j0 = 1024 * bounds[s].first, j1 = std::min(1024 * bounds[s].second, nc);
+    for (int i = 0; i < n; ++i) {
+      bufs[i] = cs[i]->xa.d() + 2 * j0;
+      st[i] = cs[i]->comm_stream;
+      if (rc_l) {
+        DeviceScope ds(cs[i]->dev);
+        CX_HIP(hipStreamWaitEvent(cs[i]->comm_stream, cs[i]->ev_pack[s], 0));
+      }
+    }
+    if (rc_l) {
+      CX_OK(rccl_collective(cs, n, 2 * (j1 - j0), bufs.data(), root, st.data()));
+      for (int i = 0; i < n; ++i) {
+        DeviceScope ds(cs[i]->dev);
+        CX_HIP(hipEventRecord(cs[i]->ev_done[s], cs[i]->comm_stream));
+      }
+    } else {
+      CX_OK(red(2 * (j1 - j0), bufs.data(), root));
+    }
+  }
+  for (int i = 0; i < n; ++i) {
+    rmsf_ctx *c = cs[i];
+    if (root >= 0 && i != root) {
+      c->merged_away = true;
+      c->rmsf_valid = false;
+      continue;
+    }
+    DeviceScope ds(c->dev);
+    CX_OK(c->rmsf.ensure(sizeof(double) * c->n_sel, c->stream));
+    for (size_t s = 0; s < ns; ++s) {
+      const int64_t j0 = 1024 * bounds[s].first, j1 = std::min(1024 * bounds[s].second, nc);
+      if (rc_l) CX_HIP(hipStreamWaitEvent(c->stream, c->ev_done[s], 0));
+      CX_OK(rmsf_chan_shift_finish(c->xa.d() + 2 * j0, static_cast<const float *>(c->shift.p) + j0, 1, nullptr,
+                                   (j1 - j0) / 3, total, c->wel.parts0.d() + j0, c->wel.parts1.d() + j0,
+                                   c->rmsf.d() + j0 / 3, c->stream));
+    }
+    c->wel.n = total;
+    c->rmsf_valid = true;
+    c->merged_away = false;
   }
   return RMSF_OK;
 }
@@ -633,10 +1014,23 @@ RMSF_EXPORT int rmsf_ctx_destroy(rmsf_ctx *c) {
   {
     DeviceScope ds(c->dev);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->side) (void)hipStreamSynchronize(c->side);  // digests copy into pinned memory freed below
     if (c->stager) rmsf_stager_destroy(c->stager);
     if (c->xdec) rmsf_xtcdec_destroy(c->xdec);
+    delete c->worker;  // joins its thread
+    c->worker = nullptr;
+    if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     if (c->comm && rccl().ok) rccl().CommDestroy(c->comm);
     drop_spans(c, -1);
+    for (hipEvent_t e : c->ev_pack) (void)hipEventDestroy(e);
+    for (int w = 0; w < 2; ++w) {
+      if (c->ev_dig[w]) (void)hipEventDestroy(c->ev_dig[w]);
+      if (c->h_dig[w]) (void)hipHostFree(c->h_dig[w]);
+    }
+    for (hipEvent_t e : c->ev_done) (void)hipEventDestroy(e);
+    if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
+    if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->ev_main) (void)hipEventDestroy(c->ev_main);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;  // DevBufs free on the context's device
   }
@@ -654,6 +1048,8 @@ RMSF_EXPORT int rmsf_ctx_synchronize(rmsf_ctx *c) {
   CX_OK(check_ctx(c, "rmsf_ctx_synchronize"));
   DeviceScope ds(c->dev);
   CX_HIP(hipStreamSynchronize(c->stream));
+  if (c->side) CX_HIP(hipStreamSynchronize(c->side));  // a shift frame's gather reads the caller's frame
+  if (c->comm_stream) CX_HIP(hipStreamSynchronize(c->comm_stream));
   return RMSF_OK;
 }
 
@@ -716,10 +1112,23 @@ RMSF_EXPORT int rmsf_get_rmsd(rmsf_ctx *c, int64_t *n, double *h_rmsd, int64_t c
 
 RMSF_EXPORT int rmsf_ctx_reset(rmsf_ctx *c, int what) {
   CX_OK(check_ctx(c, "rmsf_ctx_reset"));
-  DeviceScope ds(c->dev);
-  if (what & 1) c->n_rmsd = 0;
-  if (what & 1) CX_OK(zero_running(c, c->wel, true));
-  if (what & 2) CX_OK(zero_running(c, c->sum, false));
+  // lazily: a reset state is zeroed only if it is read before a fold
+  // overwrites it (ensure_zeroed); queued work for it is dropped
+  if (what & 1) {
+    c->n_rmsd = 0;
+    c->wel.n = 0;
+    c->wel.stale = true;
+    c->wel_aligned = false;
+    c->merged_away = false;
+    c->rmsf_valid = false;
+    c->slab.on = false;
+    if (c->pend.on && c->pend.welford) c->pend.on = false;
+  }
+  if (what & 2) {
+    c->sum.n = 0;
+    c->sum.stale = true;
+    if (c->pend.on && !c->pend.welford) c->pend.on = false;
+  }
   return RMSF_OK;
 }
 
@@ -769,6 +1178,7 @@ RMSF_EXPORT int rmsf_set_reference_average(rmsf_ctx *c) {
   CX_OK(check_ctx(c, "rmsf_set_reference_average"));
   if (c->sum.n <= 0) return fail(RMSF_EEMPTY, "rmsf_set_reference_average: no frames summed (RMSF.py:111)");
   DeviceScope ds(c->dev);
+  CX_OK(settle(c));
   CX_OK(c->avg.ensure(sizeof(double) * c->n_coord, c->stream));
   CX_OK(rmsf_reference_setup_mean(c->sum.parts0.d(), (double)c->sum.n, c->n_sel, c->d_masses(), c->avg.d(),
                                   c->ref.d(), c->refinfo.d(), c->stream));
@@ -787,6 +1197,7 @@ RMSF_EXPORT int rmsf_push_frames(rmsf_ctx *c, const float *xyz, int64_t n_frames
   if (stride < 3 * c->n_atoms) return fail(RMSF_EINVAL, "rmsf_push_frames: frame_stride < 3*n_atoms");
   DeviceScope ds(c->dev);
   if (ds.err != hipSuccess) return fail(RMSF_EHIP, "rmsf_push_frames: hipSetDevice failed");
+  CX_OK(flush_slab(c));  // an earlier recorded slab push comes first
   if (is_device_ptr) {
     for (int64_t f = 0; f < n_frames; f += kChunkFrames) {
       const int64_t nf = std::min(kChunkFrames, n_frames - f);
@@ -865,6 +1276,7 @@ RMSF_EXPORT int rmsf_push_xtc(rmsf_ctx *c, const rmsf_xtc *x, int64_t f0, int64_
   if (n_frames == 0) return RMSF_OK;
   if (x->n_atoms != c->n_atoms) return fail(RMSF_EINVAL, "rmsf_push_xtc: the file's atom count differs");
   DeviceScope ds(c->dev);
+  CX_OK(flush_slab(c));
   // the records are decompressed on the GPU (csrc/xtc_gpu.hip) into full
   // frames; the accumulate kernels gather the selection
   int64_t batch = 0;
@@ -882,6 +1294,7 @@ RMSF_EXPORT int rmsf_push_xtc_frames(rmsf_ctx *c, const rmsf_xtc *x, const int64
   if (n_frames == 0) return RMSF_OK;
   if (x->n_atoms != c->n_atoms) return fail(RMSF_EINVAL, "rmsf_push_xtc_frames: the file's atom count differs");
   DeviceScope ds(c->dev);
+  CX_OK(flush_slab(c));
   int64_t batch = 0;
   CX_OK(ensure_xdec(c, x, 3, &batch));
   return push_decoded(c, n_frames, batch, mode, [&](int64_t i, int64_t n, int *slot, float **d) {
@@ -896,6 +1309,7 @@ RMSF_EXPORT int rmsf_push_frame_ptrs(rmsf_ctx *c, const float *const *h_ptrs, in
   if (n_frames == 0) return RMSF_OK;
   DeviceScope ds(c->dev);
   if (ds.err != hipSuccess) return fail(RMSF_EHIP, "rmsf_push_frame_ptrs: hipSetDevice failed");
+  CX_OK(flush_slab(c));
   CX_OK(ensure_stager(c));
   for (int64_t f = 0; f < n_frames; f += c->stage_batch) {
     const int64_t nf = std::min(c->stage_batch, n_frames - f);
@@ -919,6 +1333,7 @@ RMSF_EXPORT int rmsf_push_frame_planes(rmsf_ctx *c, const float *const *h_ptrs, 
   if (n_frames == 0) return RMSF_OK;
   DeviceScope ds(c->dev);
   if (ds.err != hipSuccess) return fail(RMSF_EHIP, "rmsf_push_frame_planes: hipSetDevice failed");
+  CX_OK(flush_slab(c));
   CX_OK(ensure_stager(c));
   for (int64_t f = 0; f < n_frames; f += c->stage_batch) {
     const int64_t nf = std::min(c->stage_batch, n_frames - f);
@@ -935,7 +1350,11 @@ RMSF_EXPORT int rmsf_push_frame_planes(rmsf_ctx *c, const float *const *h_ptrs, 
 
 RMSF_EXPORT int rmsf_get_partial(rmsf_ctx *c, int64_t *n, double *h_mean, double *h_m2) {
   CX_OK(check_ctx(c, "rmsf_get_partial"));
+  if (c->merged_away)
+    return fail(RMSF_EINVAL, "rmsf_get_partial: a reduce-to-root merge left the result on another context");
   DeviceScope ds(c->dev);
+  CX_OK(settle(c));
+  CX_OK(ensure_zeroed(c, c->wel, true));
   const size_t row = sizeof(double) * c->n_coord;
   if (h_mean) CX_HIP(hipMemcpyAsync(h_mean, c->wel.parts0.p, row, hipMemcpyDeviceToHost, c->stream));
   if (h_m2) CX_HIP(hipMemcpyAsync(h_m2, c->wel.parts1.p, row, hipMemcpyDeviceToHost, c->stream));
@@ -947,6 +1366,8 @@ RMSF_EXPORT int rmsf_get_partial(rmsf_ctx *c, int64_t *n, double *h_mean, double
 RMSF_EXPORT int rmsf_get_sum(rmsf_ctx *c, int64_t *n, double *h_sum) {
   CX_OK(check_ctx(c, "rmsf_get_sum"));
   DeviceScope ds(c->dev);
+  CX_OK(settle(c));
+  CX_OK(ensure_zeroed(c, c->sum, false));
   if (h_sum)
     CX_HIP(hipMemcpyAsync(h_sum, c->sum.parts0.p, sizeof(double) * c->n_coord, hipMemcpyDeviceToHost, c->stream));
   CX_HIP(hipStreamSynchronize(c->stream));
@@ -959,6 +1380,7 @@ RMSF_EXPORT int rmsf_get_average(rmsf_ctx *c, double *h_avg) {
   if (!h_avg) return fail(RMSF_EINVAL, "rmsf_get_average: NULL output");
   if (c->sum.n <= 0) return fail(RMSF_EEMPTY, "rmsf_get_average: no frames summed");
   DeviceScope ds(c->dev);
+  CX_OK(settle(c));
   CX_OK(c->avg.ensure(sizeof(double) * c->n_coord, c->stream));
   CX_OK(rmsf_divide(c->sum.parts0.d(), (double)c->sum.n, c->n_coord, c->avg.d(), c->stream));
   CX_HIP(hipMemcpyAsync(h_avg, c->avg.p, sizeof(double) * c->n_coord, hipMemcpyDeviceToHost, c->stream));
@@ -969,10 +1391,16 @@ RMSF_EXPORT int rmsf_get_average(rmsf_ctx *c, double *h_avg) {
 RMSF_EXPORT int rmsf_get_rmsf(rmsf_ctx *c, double *h_rmsf) {
   CX_OK(check_ctx(c, "rmsf_get_rmsf"));
   if (!h_rmsf) return fail(RMSF_EINVAL, "rmsf_get_rmsf: NULL output");
-  if (c->wel.n <= 0) return fail(RMSF_EEMPTY, "rmsf_get_rmsf: no frames accumulated");
+  if (c->merged_away)
+    return fail(RMSF_EINVAL, "rmsf_get_rmsf: a reduce-to-root merge left the result on another context");
+  if (c->wel.n <= 0 && !c->slab.on) return fail(RMSF_EEMPTY, "rmsf_get_rmsf: no frames accumulated");
   DeviceScope ds(c->dev);
-  CX_OK(c->rmsf.ensure(sizeof(double) * c->n_sel, c->stream));
-  CX_OK(rmsf_finalize(c->wel.parts1.d(), c->n_sel, c->wel.n, c->rmsf.d(), c->stream));
+  CX_OK(settle(c));
+  if (!c->rmsf_valid) {  // the shifted merges finalise as they unpack
+    CX_OK(c->rmsf.ensure(sizeof(double) * c->n_sel, c->stream));
+    CX_OK(rmsf_finalize(c->wel.parts1.d(), c->n_sel, c->wel.n, c->rmsf.d(), c->stream));
+    c->rmsf_valid = true;
+  }
   CX_HIP(hipMemcpyAsync(h_rmsf, c->rmsf.p, sizeof(double) * c->n_sel, hipMemcpyDeviceToHost, c->stream));
   CX_HIP(hipStreamSynchronize(c->stream));
   return RMSF_OK;
@@ -982,6 +1410,10 @@ RMSF_EXPORT int rmsf_set_partial(rmsf_ctx *c, int64_t n, const double *h_mean, c
   CX_OK(check_ctx(c, "rmsf_set_partial"));
   if (n < 0 || (n > 0 && (!h_mean || !h_m2))) return fail(RMSF_EINVAL, "rmsf_set_partial: bad arguments");
   DeviceScope ds(c->dev);
+  c->slab.on = false;  // the state is replaced: queued work for it is moot
+  if (c->pend.on && c->pend.welford) c->pend.on = false;
+  c->merged_away = false;
+  c->rmsf_valid = false;
   CX_OK(zero_running(c, c->wel, true));
   if (n > 0) {
     const size_t row = sizeof(double) * c->n_coord;
@@ -1008,7 +1440,7 @@ RMSF_EXPORT int rmsf_ctx_chan_merge(rmsf_ctx *c, rmsf_allreduce_fn fn, void *use
 RMSF_EXPORT int rmsf_ctx_chan_merge_shifted(rmsf_ctx *c, rmsf_allreduce_fn fn, void *user) {
   CX_OK(check_ctx(c, "rmsf_ctx_chan_merge_shifted"));
   if (!fn) return fail(RMSF_EINVAL, "rmsf_ctx_chan_merge_shifted: NULL callback");
-  return exchange_chan_shifted(&c, 1, callback_reduce(c, fn, user), false);
+  return exchange_chan_shifted(&c, 1, callback_reduce(c, fn, user), false, Shift::REF, -1);
 }
 
 RMSF_EXPORT int rmsf_multi_unique_id(void *id_out) {
@@ -1067,24 +1499,117 @@ RMSF_EXPORT int rmsf_multi_allreduce_sum(rmsf_ctx **cs, int n) {
   return exchange_sum(cs, n, red, whole_group_here(cs, n));
 }
 
-RMSF_EXPORT int rmsf_multi_chan_merge(rmsf_ctx **cs, int n) {
+RMSF_EXPORT int rmsf_multi_chan_merge_root(rmsf_ctx **cs, int n, int root) {
   Reduce red;
-  CX_OK(multi_reduce(cs, n, "rmsf_multi_chan_merge", &red));
-  // every rank of the exchange is a context of this process and each holds
-  // a reference (aligned sweeps: the same one, as RMSF.py's ranks hold it):
-  // one data all-reduce instead of two.  Ranks in other processes could
-  // decide differently, so a communicator spanning processes keeps the
-  // two-pass form (rmsf_ctx_chan_merge_shifted is the explicit choice there).
-  // The shifted form is exact only when every context holds the SAME
-  // reference (T1 = sum n_k (mean_k - c) needs one c): contexts aligned to
-  // references of their own keep the two-pass merge (reference digests,
-  // k_ref_digest, compared here).
+  int kind = 0;
+  CX_OK(multi_reduce(cs, n, "rmsf_multi_chan_merge_root", &red, &kind));
+  if (root < -1 || root >= n) return fail(RMSF_EINVAL, "rmsf_multi_chan_merge_root: root outside the contexts");
+  // Every rank of the exchange is a context of this process: the merge is ONE
+  // data collective of moments about a shift every context holds -- the
+  // reference of aligned state (RMSF.py's ranks hold the same one), or the
+  // merge shift frame of unaligned state -- with the reference / frame
+  // digests compared here (k_digest: one shift c for T1 = sum n_k (mean_k -
+  // c)).  Ranks in other processes could decide differently, so a
+  // communicator spanning processes keeps the two-pass form
+  // (rmsf_ctx_chan_merge_shifted is the explicit choice there), as do
+  // contexts without a common shift.  The two-pass form leaves the result on
+  // every context whatever `root` asks.
   const bool here = whole_group_here(cs, n);
-  bool all_ref = here;
-  for (int i = 0; i < n; ++i) all_ref = all_ref && cs[i]->ref_set;
-  if (all_ref) CX_OK(same_references(cs, n, &all_ref));
-  if (all_ref) return exchange_chan_shifted(cs, n, red, here);
-  return exchange_chan(cs, n, red, whole_group_here(cs, n));
+  bool unaligned = true;  // the Welford state of every context came from unaligned pushes
+  for (int i = 0; i < n; ++i) unaligned = unaligned && (cs[i]->slab.on || !cs[i]->wel_aligned);
+  bool use_ref = false, use_frame = false;
+  if (here && unaligned) CX_OK(same_digests(cs, n, true, &use_frame));
+  if (here && !use_frame) CX_OK(same_digests(cs, n, false, &use_ref));
+  if (use_frame) {
+    bool slabs = true;
+    for (int i = 0; i < n; ++i)
+      slabs = slabs && cs[i]->slab.on && cs[i]->slab.chunks == cs[0]->slab.chunks && cs[i]->slab.k == cs[0]->slab.k;
+    if (slabs) return slab_merge(cs, n, kind, red, root);
+    return exchange_chan_shifted(cs, n, red, here, Shift::FRAME, root);
+  }
+  if (use_ref) return exchange_chan_shifted(cs, n, red, here, Shift::REF, root);
+  return exchange_chan(cs, n, red, here);
+}
+
+RMSF_EXPORT int rmsf_multi_chan_merge(rmsf_ctx **cs, int n) { return rmsf_multi_chan_merge_root(cs, n, -1); }
+
+RMSF_EXPORT int rmsf_multi_set_transport(rmsf_ctx **cs, int n, int transport) {
+  if (!cs || n < 1) return fail(RMSF_EINVAL, "rmsf_multi_set_transport: no contexts");
+  if (transport != RMSF_TRANSPORT_AUTO && transport != RMSF_TRANSPORT_NOOP)
+    return fail(RMSF_EINVAL, "rmsf_multi_set_transport: unknown transport");
+  for (int i = 0; i < n; ++i) CX_OK(check_ctx(cs[i], "rmsf_multi_set_transport"));
+  for (int i = 0; i < n; ++i) cs[i]->transport = transport;
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_set_merge_shift_frame(rmsf_ctx *c, const float *xyz, int is_device_ptr) {
+  CX_OK(check_ctx(c, "rmsf_set_merge_shift_frame"));
+  if (!xyz) return fail(RMSF_EINVAL, "rmsf_set_merge_shift_frame: NULL frame");
+  DeviceScope ds(c->dev);
+  const float *d = xyz;
+  if (!is_device_ptr) {
+    const size_t bytes = sizeof(float) * 3 * (size_t)c->n_atoms;
+    CX_OK(c->frame.ensure(bytes, c->stream));
+    CX_HIP(hipMemcpyAsync(c->frame.p, xyz, bytes, hipMemcpyHostToDevice, c->stream));
+    CX_HIP(hipStreamSynchronize(c->stream));
+    d = static_cast<const float *>(c->frame.p);
+  }
+  CX_OK(c->shift.ensure(sizeof(float) * c->n_coord, c->stream));
+  if (!c->zidx_set) {
+    CX_OK(c->zidx.ensure(sizeof(int64_t), c->stream));
+    CX_HIP(hipMemsetAsync(c->zidx.p, 0, sizeof(int64_t), c->stream));
+    c->zidx_set = true;
+  }
+  // on the side stream, after the work queued so far (a previous merge still
+  // reading the old shift); the merge waits for ev_dig[1]
+  CX_OK(side_begin(c));
+  CX_OK(rmsf_gather_frames(d, 3 * c->n_atoms, static_cast<const int64_t *>(c->zidx.p), 1, c->n_sel, c->d_sel(),
+                           static_cast<float *>(c->shift.p), c->side));
+  c->shift_set = true;
+  return digest_into(c, 1, c->shift.p, true, c->n_coord, nullptr, 0);
+}
+
+RMSF_EXPORT int rmsf_multi_push_frames(rmsf_ctx **cs, int n, const float *const *d_frames, const int64_t *n_frames,
+                                       int64_t frame_stride, int mode, int flags, const float *const *d_ref_frames,
+                                       const float *const *d_shift_frames, int merge_slabs) {
+  if (!cs || n < 1 || !d_frames || !n_frames) return fail(RMSF_EINVAL, "rmsf_multi_push_frames: bad arguments");
+  CX_OK(check_mode(mode, "rmsf_multi_push_frames"));
+  if (merge_slabs < 0) return fail(RMSF_EINVAL, "rmsf_multi_push_frames: merge_slabs < 0");
+  for (int i = 0; i < n; ++i) {
+    CX_OK(check_ctx(cs[i], "rmsf_multi_push_frames"));
+    if (n_frames[i] < 0 || (n_frames[i] > 0 && !d_frames[i]))
+      return fail(RMSF_EINVAL, "rmsf_multi_push_frames: bad frames");
+    for (int j = 0; j < i; ++j)
+      if (cs[j] == cs[i]) return fail(RMSF_EINVAL, "rmsf_multi_push_frames: a context is listed twice");
+  }
+  return for_each_ctx(cs, n, [&](int i) -> int {
+    rmsf_ctx *c = cs[i];
+    if (flags & RMSF_MULTI_RESET)
+      CX_OK(rmsf_ctx_reset(c, (mode == RMSF_PUSH_WELFORD || mode == RMSF_PUSH_ALIGN_WELFORD) ? 1 : 2));
+    if (d_ref_frames && d_ref_frames[i]) CX_OK(rmsf_set_reference_frame(c, d_ref_frames[i], 1));
+    if (d_shift_frames && d_shift_frames[i]) CX_OK(rmsf_set_merge_shift_frame(c, d_shift_frames[i], 1));
+    const int64_t nf = n_frames[i];
+    if (nf == 0) return RMSF_OK;
+    const int64_t stride = frame_stride ? frame_stride : 3 * c->n_atoms;
+    // the atom-slab merge (C4's size): a single unaligned launch group over
+    // all atoms whose flat plan is chunk-aligned, recorded here and streamed
+    // slab by slab by the next rmsf_multi_chan_merge_root
+    const int k = merge_slabs == 0 ? (c->n_sel >= kSlabMinAtoms ? kSlabsAuto : 1) : merge_slabs;
+    if (k >= 2 && mode == RMSF_PUSH_WELFORD && !c->d_sel() && c->shift_set && nf <= kChunkFrames &&
+        c->wel.n == 0 && !c->slab.on && stride >= 3 * c->n_atoms) {
+      int64_t chunks = 0;
+      DeviceScope ds(c->dev);
+      CX_OK(rmsf_balanced_slab_chunks(d_frames[i], stride, nf, c->n_sel, &chunks));
+      if (chunks >= 2 * 3) {
+        CX_OK(flush_fold(c));
+        c->slab = {true, d_frames[i], stride, nf, chunks, k};
+        c->rmsf_valid = false;
+        c->merged_away = false;
+        return RMSF_OK;
+      }
+    }
+    return rmsf_push_frames(c, d_frames[i], nf, stride, mode, 1);
+  });
 }
 
 }  // extern "C"

@@ -140,6 +140,10 @@ SIGNATURES = {
     "rmsf_multi_init_all": (c_int, [P, c_int]),
     "rmsf_multi_allreduce_sum": (c_int, [P, c_int]),
     "rmsf_multi_chan_merge": (c_int, [P, c_int]),
+    "rmsf_set_merge_shift_frame": (c_int, [P, P, c_int]),
+    "rmsf_multi_chan_merge_root": (c_int, [P, c_int, c_int]),
+    "rmsf_multi_push_frames": (c_int, [P, c_int, P, P, c_int64, c_int, c_int, P, P, c_int]),
+    "rmsf_multi_set_transport": (c_int, [P, c_int, c_int]),
 }
 
 # int (*rmsf_allreduce_fn)(double *d_buf, int64_t count, void *stream, void *user)
@@ -147,6 +151,8 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int64, c_void_p, c_void_p)
 RMSF_PUSH_WELFORD, RMSF_PUSH_ALIGN_SUM, RMSF_PUSH_ALIGN_WELFORD, RMSF_PUSH_SUM = 0, 1, 2, 3
 RMSF_UNIQUE_ID_BYTES = 128
 RMSF_TIME_ACCUMULATE, RMSF_TIME_SUPERPOSE = 0, 1
+RMSF_MULTI_RESET = 1
+RMSF_TRANSPORT_AUTO, RMSF_TRANSPORT_NOOP = 0, 1
 
 _lib = None
 

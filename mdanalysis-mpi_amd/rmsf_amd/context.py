@@ -27,13 +27,16 @@ import ctypes
 
 import numpy as np
 
-from ._lib import (ALLREDUCE_FN, RMSF_PUSH_ALIGN_SUM, RMSF_PUSH_ALIGN_WELFORD, RMSF_PUSH_SUM, RMSF_PUSH_WELFORD,
-                   RMSF_TIME_ACCUMULATE, RMSF_TIME_SUPERPOSE, RMSF_UNIQUE_ID_BYTES, call, load)
+from ._lib import (ALLREDUCE_FN, RMSF_MULTI_RESET, RMSF_PUSH_ALIGN_SUM, RMSF_PUSH_ALIGN_WELFORD, RMSF_PUSH_SUM,
+                   RMSF_PUSH_WELFORD, RMSF_TIME_ACCUMULATE, RMSF_TIME_SUPERPOSE, RMSF_TRANSPORT_AUTO,
+                   RMSF_TRANSPORT_NOOP, RMSF_UNIQUE_ID_BYTES, call, load)
 
 PUSH_WELFORD = RMSF_PUSH_WELFORD
 PUSH_ALIGN_SUM = RMSF_PUSH_ALIGN_SUM
 PUSH_ALIGN_WELFORD = RMSF_PUSH_ALIGN_WELFORD
 PUSH_SUM = RMSF_PUSH_SUM
+TRANSPORT_AUTO = RMSF_TRANSPORT_AUTO
+TRANSPORT_NOOP = RMSF_TRANSPORT_NOOP
 
 
 def _f64(a, n: int, name: str) -> np.ndarray:
@@ -85,6 +88,8 @@ class Context:
         self.n_sel = len(self._sel) if self._sel is not None else int(n_sel if n_sel is not None else n_atoms)
         m = None if masses is None else _f64(masses, self.n_sel, "masses")
         self.device = device
+        self._alive = []     # device tensors read by queued work (released at the next synchronisation)
+        self._ext = None     # torch's view of the context stream (cached)
         self._h = ctypes.c_void_p()
         call("rmsf_ctx_create", device, self.n_atoms, self.n_sel,
              None if self._sel is None else self._sel.ctypes.data, None if m is None else m.ctypes.data, 0,
@@ -103,8 +108,9 @@ class Context:
 
     def close(self) -> None:
         if self._h:
-            call("rmsf_ctx_destroy", self._h)
+            call("rmsf_ctx_destroy", self._h)  # synchronises the context stream first
             self._h = ctypes.c_void_p()
+        self._alive.clear()
 
     def __del__(self):
         try:
@@ -120,6 +126,7 @@ class Context:
 
     def synchronize(self) -> None:
         call("rmsf_ctx_synchronize", self._h)
+        self._alive.clear()
 
     def set_staging(self, batch_frames: int = 0, n_slots: int = 2, n_threads: int = 4) -> None:
         call("rmsf_ctx_set_staging", self._h, batch_frames, n_slots, n_threads)
@@ -134,6 +141,7 @@ class Context:
         k = {"accumulate": RMSF_TIME_ACCUMULATE, "superpose": RMSF_TIME_SUPERPOSE}[which]
         n, ms, af = ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
         call("rmsf_ctx_kernel_time", self._h, k, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(af))
+        self._alive.clear()  # kernel_time synchronised the stream
         return n.value, ms.value, af.value
 
     def collect_rmsd(self, on: bool = True) -> None:
@@ -164,8 +172,16 @@ class Context:
             # the setup kernels read the frame asynchronously on the context
             # stream: a temporary (e.g. a copy from another device) must
             # outlive them
-            self.synchronize()
-        del keep
+            self._alive.append(keep)
+
+    def set_merge_shift_frame(self, frame) -> None:
+        """The merge's shift for unaligned Welford state: frame 0 of the frame
+        list (all n_atoms atoms; the context keeps its selected rows), the
+        same on every context (rmsf_set_merge_shift_frame)."""
+        ptr, dev, keep = self._frames_ptr(frame, 1)
+        call("rmsf_set_merge_shift_frame", self._h, ptr, dev)
+        if dev:
+            self._alive.append(keep)
 
     def set_reference_average(self) -> None:
         call("rmsf_set_reference_average", self._h)
@@ -193,9 +209,10 @@ class Context:
         orders behind torch's current stream.  An event wait, no host sync."""
         import torch
 
-        with torch.cuda.device(self.device):
-            ext = torch.cuda.ExternalStream(self.stream, device=torch.device("cuda", self.device))
-        ext.wait_stream(torch.cuda.current_stream(t.device))
+        if self._ext is None:
+            with torch.cuda.device(self.device):
+                self._ext = torch.cuda.ExternalStream(self.stream, device=torch.device("cuda", self.device))
+        self._ext.wait_stream(torch.cuda.current_stream(t.device))
 
     def push(self, frames, mode: int = PUSH_WELFORD, step: int = 1) -> None:
         """Push frames [n, n_atoms, 3] (every ``step``-th one)."""
@@ -205,10 +222,9 @@ class Context:
         n = len(range(0, n_all, step))
         call("rmsf_push_frames", self._h, ptr, n, 3 * self.n_atoms * step, mode, dev)
         if dev:
-            # device frames are read asynchronously: the caller's tensor must
-            # outlive the queued work
-            self.synchronize()
-        del keep
+            # device frames are read asynchronously: the tensor is kept alive
+            # until the context is next synchronised (no host sync here)
+            self._alive.append(keep)
 
     def push_xtc(self, xtc, start: int = 0, stop: int | None = None, step: int = 1, mode: int = PUSH_WELFORD):
         stop = xtc.n_frames if stop is None else min(stop, xtc.n_frames)
@@ -252,22 +268,26 @@ class Context:
         mean = np.empty((self.n_sel, 3))
         m2 = np.empty((self.n_sel, 3))
         call("rmsf_get_partial", self._h, ctypes.byref(n), mean.ctypes.data, m2.ctypes.data)
+        self._alive.clear()  # the getters synchronise the context stream
         return n.value, mean, m2
 
     def sum(self):
         n = ctypes.c_int64()
         s = np.empty((self.n_sel, 3))
         call("rmsf_get_sum", self._h, ctypes.byref(n), s.ctypes.data)
+        self._alive.clear()  # the getters synchronise the context stream
         return n.value, s
 
     def average(self) -> np.ndarray:
         out = np.empty((self.n_sel, 3))
         call("rmsf_get_average", self._h, out.ctypes.data)
+        self._alive.clear()  # the getters synchronise the context stream
         return out
 
     def rmsf(self) -> np.ndarray:
         out = np.empty(self.n_sel)
         call("rmsf_get_rmsf", self._h, out.ctypes.data)
+        self._alive.clear()  # the getters synchronise the context stream
         return out
 
     def set_partial(self, n: int, mean, m2) -> None:
@@ -327,5 +347,61 @@ class Context:
         call("rmsf_multi_allreduce_sum", *Context._handles(ctxs))
 
     @staticmethod
-    def multi_chan_merge(ctxs) -> None:
-        call("rmsf_multi_chan_merge", *Context._handles(ctxs))
+    def multi_chan_merge(ctxs, root: int | None = None) -> None:
+        """RMSF.py:140-143 over the contexts: root=None leaves the result in
+        every context (rmsf_multi_chan_merge); root=r reduces it to context
+        r only, as RMSF.py:143's comm.reduce(root=0) (the others then refuse
+        rmsf() until reset)."""
+        h, n = Context._handles(ctxs)
+        call("rmsf_multi_chan_merge_root", h, n, -1 if root is None else int(root))
+
+    @staticmethod
+    def multi_set_transport(ctxs, transport: int) -> None:
+        """TRANSPORT_AUTO (RCCL / host fold) or TRANSPORT_NOOP (timing
+        rehearsal: the exchanges move nothing, results are not global)."""
+        call("rmsf_multi_set_transport", *Context._handles(ctxs), int(transport))
+
+    @staticmethod
+    def multi_push_frames(ctxs, frames, mode: int = PUSH_WELFORD, *, reset: bool = True, ref_frames=None,
+                          shift_frames=None, merge_slabs: int = 0, after_torch: bool = True) -> None:
+        """Push HIP tensor ``frames[i]`` ([n_i, n_atoms, 3] float32,
+        contiguous) to context i, every context's launches enqueued from its
+        own host thread (rmsf_multi_push_frames; no host synchronisation).
+        ``reset``: reset the state ``mode`` accumulates into first;
+        ``ref_frames[i]`` / ``shift_frames[i]``: device frames set as the
+        reference / merge shift frame first; ``merge_slabs``: 0 = auto (atom
+        slabs from 1M atoms, run by the next multi_chan_merge), 1 = off.
+        ``after_torch``: order each context stream after torch's current
+        stream of the tensor's device (skip when the frames are known ready)."""
+        import torch
+
+        n = len(ctxs)
+        if len(frames) != n:
+            raise ValueError("one frame tensor per context")
+        ptrs, counts = (ctypes.c_void_p * n)(), (ctypes.c_int64 * n)()
+        refs = (ctypes.c_void_p * n)() if ref_frames is not None else None
+        shifts = (ctypes.c_void_p * n)() if shift_frames is not None else None
+        for i, (c, t) in enumerate(zip(ctxs, frames)):
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+                raise ValueError("multi_push_frames: contiguous float32 HIP tensors expected")
+            if t.numel() % (3 * c.n_atoms):
+                raise ValueError(f"device frames: not a whole number of {c.n_atoms}-atom frames")
+            if t.device.index != c.device:
+                raise ValueError(f"context {i} is on device {c.device}, its frames on {t.device}")
+            ptrs[i], counts[i] = t.data_ptr(), t.numel() // (3 * c.n_atoms)
+            keep = [t]
+            for arr, src in ((refs, ref_frames), (shifts, shift_frames)):
+                if arr is not None and src[i] is not None:
+                    f = src[i]
+                    if not (f.is_cuda and f.dtype == torch.float32 and f.is_contiguous()
+                            and f.numel() == 3 * c.n_atoms and f.device.index == c.device):
+                        raise ValueError("reference / shift frames: one contiguous float32 frame on the "
+                                         "context's device")
+                    arr[i] = f.data_ptr()
+                    keep.append(f)
+            if after_torch:
+                c._after_torch(t)
+            c._alive.extend(keep)
+        h, _ = Context._handles(ctxs)
+        call("rmsf_multi_push_frames", h, n, ptrs, counts, 0, int(mode), RMSF_MULTI_RESET if reset else 0,
+             refs, shifts, int(merge_slabs))

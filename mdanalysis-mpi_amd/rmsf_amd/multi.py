@@ -17,10 +17,12 @@ Per context, RMSF.py's rank loop in context-ABI terms:
     multi_allreduce_sum(all)                             RMSF.py:107-110
     set_reference_average()                              RMSF.py:111-118
     push(block, ALIGN_WELFORD)                           RMSF.py:120-138
-    multi_chan_merge(all)                                RMSF.py:140-143
+    multi_chan_merge(all[, root])                        RMSF.py:140-143
     get_rmsf                                             RMSF.py:145-146
 
-(``align=None``: one Welford push; ``"frame0"``: reference + aligned Welford.)
+(``align=None``: one Welford push, with frame 0 of the frame list set on
+every context as the merge's shift -- the one-collective merge, as the
+torchrun pipeline's; ``"frame0"``: reference + aligned Welford.)
 """
 from __future__ import annotations
 
@@ -330,13 +332,29 @@ def _frames_of(inp, sel, batch_frames, layout: str = "fac"):
                     "tensors -- one shard per device)")
 
 
+def _set_frame(c: Context, fr, setter: str) -> None:
+    """``setter`` (set_reference_frame / set_merge_shift_frame) of a frame
+    that may live on another device: copied over xGMI on torch's stream of
+    c's device; the setter orders the context stream after the copy and keeps
+    the copy alive until the context is synchronised."""
+    if hasattr(fr, "is_cuda") and fr.device.index != c.device:
+        import torch
+        with torch.cuda.device(c.device):
+            getattr(c, setter)(fr.to(torch.device("cuda", c.device)))
+    else:
+        getattr(c, setter)(fr)
+
+
 def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int = 0, start=None, stop=None,
               step=None, batch_frames: int | None = None, frames=None, collect_rmsd: bool = False,
-              layout: str = "fac") -> dict:
+              layout: str = "fac", merge_root: int | None = None) -> dict:
     """RMSF.py's computation over the devices ``gpus`` from one process.
     Returns the ``results`` fields (rmsf, mean, sumsquares, n_frames, ...;
     ``rmsd`` with ``collect_rmsd``: per-frame QCP rmsd of the last sweep in
-    frame-list order, the by-product RMSF.py:48 discards)."""
+    frame-list order, the by-product RMSF.py:48 discards).  ``merge_root``:
+    the final merge is a reduce to that device index (RMSF.py:143's shape)
+    and the results are read from it; None = an all-reduce, read from
+    device index 0 (the same numbers)."""
     if align not in (None, "frame0", "average"):
         raise ValueError(f"align must be one of (None, 'frame0', 'average'), got {align!r}")
     if parallel.world()[1] > 1:
@@ -347,6 +365,9 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
     if layout == "soa" and not isinstance(inp, np.ndarray):
         raise NotImplementedError("gpus=: SoA input is supported for host numpy arrays [F, 3, n_atoms]")
     src = _frames_of(inp, select, batch_frames, layout)
+    n_dev = len(src.parts) if isinstance(src, _DeviceShards) else len(device_list(gpus))
+    if merge_root is not None and not 0 <= merge_root < n_dev:
+        raise ValueError(f"merge_root {merge_root} is not one of the {n_dev} devices")
     fl = FrameList(src.n_traj, start, stop, step, frames=frames)
     if len(fl) == 0:
         raise RmsfEmptyError(-4, "RMSF.run", "no frames selected")
@@ -399,15 +420,13 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
             if staged and getattr(src, "sel", None) is not None:
                 ref = ref[src.sel]
             for c in ctxs:  # every rank reads the reference frame (RMSF.py:80-87)
-                if hasattr(ref, "is_cuda") and ref.device.index != c.device:
-                    import torch
-                    # one frame over xGMI, copied on torch's stream of c's
-                    # device; set_reference_frame orders the context stream
-                    # after it and keeps the copy alive until the setup ran
-                    with torch.cuda.device(c.device):
-                        c.set_reference_frame(ref.to(torch.device("cuda", c.device)))
-                else:
-                    c.set_reference_frame(ref)
+                _set_frame(c, ref, "set_reference_frame")
+        elif len(ctxs) > 1:
+            # the merge's shift: frame 0 of the frame list on every context
+            # (the one-collective merge, as the torchrun pipeline's)
+            shift = src.reference(fl[0])
+            for c in ctxs:
+                _set_frame(c, shift, "set_merge_shift_frame")
         cached = {}
         if staged:
             def stage(i):
@@ -438,9 +457,10 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
             for c in ctxs:  # the last sweep's rmsd only, as the pipeline reports it
                 c.collect_rmsd(True)
         each(lambda i: push(i, PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD))
-        Context.multi_chan_merge(ctxs)
-        n, mean, m2 = ctxs[0].partial()
-        out.update(rmsf=ctxs[0].rmsf(), mean=mean, sumsquares=m2, n_frames=n,
+        Context.multi_chan_merge(ctxs, root=merge_root)
+        home = ctxs[merge_root or 0]
+        n, mean, m2 = home.partial()
+        out.update(rmsf=home.rmsf(), mean=mean, sumsquares=m2, n_frames=n,
                    blocks=[(int(b0), int(b1)) for b0, b1 in spans], devices=devs)
         if collect_rmsd:
             out["rmsd"] = np.concatenate([c.rmsd() for c in ctxs])

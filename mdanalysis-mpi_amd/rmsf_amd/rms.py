@@ -80,7 +80,9 @@ class RMSF:
         Under ``torch.distributed``: merge the ranks' statistics with a
         reduce to this rank only, as RMSF.py:143 (``comm.reduce(root=0)``)
         does; the other ranks' ``results.rmsf`` / ``mean`` / ``sumsquares``
-        are None.  Default: every rank receives the merged result.
+        are None.  Default: every rank receives the merged result.  With
+        ``gpus=``: the merge is a reduce to that device index and the
+        results (which this one process returns either way) come from it.
     gpus : int | list of int, optional
         Drive this many devices (or these device ids) from one process: each
         takes the RMSF.py:65-69 block of its index and the blocks merge over
@@ -167,7 +169,7 @@ class RMSF:
         out = run_multi(self._input, self.gpus, select=self.select, align=self.align, masses=self.masses,
                         ref_frame=self.ref_frame, start=start, stop=stop, step=step,
                         batch_frames=self.batch_frames, frames=frames, collect_rmsd=self.collect_rmsd,
-                        layout=self.layout)
+                        layout=self.layout, merge_root=self.merge_root)
         r = self.results
         r.update(out)
         r.m2 = r.sumsquares
