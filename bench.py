@@ -114,10 +114,12 @@ def parse(argv=None):
     ap.add_argument("--merge-slabs", type=int, default=None,
                     help="N>1, no alignment: atom slabs of the final sweep whose all-reduces overlap the next slab "
                          "(default: 2 from 1M atoms, else none; 0 = off)")
-    ap.add_argument("--merge", choices=["root", "all"], default="root",
+    ap.add_argument("--merge", choices=["root", "all", "scatter"], default="root",
                     help="N>1: the final Chan merge as a reduce to rank 0 (default: RMSF.py:143's "
-                         "comm.reduce(root=0); a ring reduce carries the 6*n_sel doubles over each link once) or as "
-                         "an all-reduce that leaves the result on every rank (twice the link bytes)")
+                         "comm.reduce(root=0); a ring reduce carries the 6*n_sel doubles over each link once), as "
+                         "an all-reduce that leaves the result on every rank (twice the link bytes), or as a "
+                         "reduce-scatter by atom slices with each rank finishing its slice and only the RMSF "
+                         "gathered to rank 0 (torchrun form; the one-process form treats it as root)")
     ap.add_argument("--merge-root", action="store_const", dest="merge", const="root",
                     help="same as --merge root (kept for older command lines)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL; gloo only "
@@ -471,6 +473,14 @@ def main():
         dist.all_reduce(_t)
         if a.merge == "root":
             dist.reduce(_t, dst=0)
+        if a.merge == "scatter":
+            _per = -(-n_atoms // world)
+            _o = torch.zeros(6 * _per, dtype=torch.float64, device=eng.device)
+            parallel_rs = torch.zeros(6 * _per * world, dtype=torch.float64, device=eng.device)
+            from rmsf_amd import parallel as _p
+            _p.reduce_scatter_sum_(_o, parallel_rs)
+            _p.gather_(_o[:_per], 0)
+            del _o, parallel_rs
         dist.barrier()
         torch.cuda.synchronize()
         del _t
@@ -522,7 +532,8 @@ def main():
             src.drop_cache()  # every step streams the file again
         return run_pipeline(eng, src, fl, align=align, block=(b0, b1), ref_owner=0, n_splits=a.splits,
                             max_batch=a.batch_frames, timer=timer, merge_slabs=a.merge_slabs,
-                            merge_root=0 if a.merge == "root" else None)
+                            merge_root=0 if a.merge in ("root", "scatter") else None,
+                            merge_scatter=a.merge == "scatter")
 
     def timed(align, steps, warmup):
         timer = KernelTimer()
@@ -549,7 +560,9 @@ def main():
     out = base_line(a, wl, world, dt, par)
     if world > 1:
         out["config"]["merge_slabs"] = res.extras.get("merge_slabs", 0)
-        out["config"]["merge"] = "reduce to rank 0 (RMSF.py:143)" if a.merge == "root" else "all-reduce"
+        out["config"]["merge"] = {"root": "reduce to rank 0 (RMSF.py:143)", "all": "all-reduce",
+                                  "scatter": "reduce-scatter by atom slices, each rank finishes its slice, RMSF "
+                                             "gathered to rank 0 (RMSF.py:143's result)"}[a.merge]
     launches, acc_ms, acc_af = timer.totals("accumulate")
     traffic = load_traffic(a.workload, n_atoms, n_local) if launches == a.steps else None
     kname = (("k_accum_atoms" if wl["align"] else "k_welford_flat") if a.splits

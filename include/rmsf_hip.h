@@ -249,6 +249,34 @@ int rmsf_fold_balanced_shift(const void *d_work, int64_t n_coord,
                              const void *d_shift, int shift_is_f32,
                              const double *d_off3, double *d_t, void *stream);
 
+/* The reduce-scatter form of the merge (RMSF.py:140-143 with :146 on each
+ * rank's atom slice, then only the RMSF gathered to the root): the same
+ * T1/T2 in the ATOM-SLICED layout -- for slice_coords = 3 x atoms per rank,
+ * slice r = j / slice_coords holds [T1 | T2] of its slice_coords
+ * coordinates at d_t + 2 r slice_coords (T2 slice_coords after T1), so a
+ * reduce-scatter of equal chunks gives rank r its slice; coordinates past n
+ * in the last slice are not written (the caller zeroes that padding).
+ * rmsf_chan_shift_finish_slice unpacks one reduced slice [T1 | T2] of width
+ * slice_coords for its n_sel atoms (d_shift, d_mean, d_m2, d_rmsf point at
+ * the slice's first atom).  Bit-identical per coordinate to the plain
+ * layout's pack and finish.                                                 */
+int rmsf_fold_balanced_shift_sliced(const void *d_work, int64_t n_coord,
+                                    int64_t acc_n, double *d_acc0,
+                                    double *d_acc1, const void *d_shift,
+                                    int shift_is_f32, const double *d_off3,
+                                    int64_t slice_coords, double *d_t,
+                                    void *stream);
+int rmsf_chan_shift_pack_sliced(const double *d_mean_k, const double *d_m2_k,
+                                const void *d_shift, int shift_is_f32,
+                                const double *d_off3, double n_k, int64_t n,
+                                int64_t slice_coords, double *d_t,
+                                void *stream);
+int rmsf_chan_shift_finish_slice(const double *d_t, int64_t slice_coords,
+                                 const void *d_shift, int shift_is_f32,
+                                 const double *d_off3, int64_t n_sel,
+                                 int64_t n_frames, double *d_mean, double *d_m2,
+                                 double *d_rmsf, void *stream);
+
 /* Atom slabs of the flat WELFORD plan (no selection, no transform, 16-B
  * aligned float4 columns), so a rank's cross-rank merge can start on the
  * first slab while the next one streams (large n_sel; RMSF.py:140-143).

@@ -586,6 +586,15 @@ __device__ __forceinline__ void shift_moments(double mu, double M2, double c, do
   *t2 = __builtin_fma(nk, d * d, M2);
 }
 
+// Where coordinate j's T1 goes in a merge buffer: the plain layout [T1 | T2]
+// (t_slice = 0: T1 at j, T2 at j + n), or the atom-sliced layout of the
+// reduce-scatter merge (t_slice = 3 x atoms per rank): slice r = j / t_slice
+// holds [T1 | T2] of its t_slice coordinates, T2 t_slice after T1.
+__device__ __forceinline__ int64_t slice_t1(int64_t j, int64_t t_slice) {
+  const int64_t r = j / t_slice;
+  return 2 * r * t_slice + (j - r * t_slice);
+}
+
 // FIN: also the finalise of RMSF.py:146 for an atom plan (cpl = 3: lane l is
 // atom l), rmsf[l] = sqrt((M2x + M2y + M2z) / n_total) -- k_finalize's
 // expression on the values just stored, so bit-identical to it, one launch
@@ -596,10 +605,11 @@ __global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ 
                                                     double acc_n, double *__restrict__ acc0,
                                                     double *__restrict__ acc1, const void *__restrict__ shift,
                                                     const double *__restrict__ off3, double *__restrict__ t,
-                                                    int64_t l_off, int64_t l_end, int64_t t_n,
+                                                    int64_t l_off, int64_t l_end, int64_t t_n, int64_t t_slice,
                                                     double *__restrict__ rmsf = nullptr, double n_total = 0.0) {
   // lanes [l_off, l_end) (an atom slab; 0, INT64_MAX = all).  T1/T2 of the
-  // slab's coordinates go to t[j - j_lo] and t[t_n + j - j_lo].
+  // slab's coordinates go to t[j - j_lo] and t[t_n + j - j_lo]; with t_slice
+  // (whole range only) to the atom-sliced layout of slice_t1.
   const int64_t l = l_off + (int64_t)blockIdx.x * kBlock + threadIdx.x;
   SkPlan pl;
   pl.lanes = hdr[0];
@@ -729,10 +739,20 @@ __global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ 
   }
   if (PACK) {
     const double nk = acc_n + (double)pl.nf;  // frames folded in: this rank's n_k
-    double *t1 = t + (j0 - l_off * cpl), *t2 = t1 + t_n;
+    if (t_slice > 0) {
 #pragma unroll
-    for (int x = 0; x < 4; ++x)
-      if (x < nx) shift_moments(mu[x], M[x], cs[x], nk, t1 + x, t2 + x);
+      for (int x = 0; x < 4; ++x) {
+        if (x < nx) {
+          double *t1 = t + slice_t1(j0 + x, t_slice);
+          shift_moments(mu[x], M[x], cs[x], nk, t1, t1 + t_slice);
+        }
+      }
+    } else {
+      double *t1 = t + (j0 - l_off * cpl), *t2 = t1 + t_n;
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+        if (x < nx) shift_moments(mu[x], M[x], cs[x], nk, t1 + x, t2 + x);
+    }
   }
 }
 
@@ -1305,12 +1325,17 @@ __global__ __launch_bounds__(kBlock) void k_chan_shift_pack(const double *__rest
                                                             const double *__restrict__ qk,
                                                             const ShiftT *__restrict__ shift,
                                                             const double *__restrict__ off3, double nk, int64_t n,
-                                                            double *__restrict__ t) {
+                                                            double *__restrict__ t, int64_t t_slice) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= n) return;
   double c = (double)shift[j];
   if (off3) c += off3[j % 3];
-  shift_moments(mk[j], qk[j], c, nk, t + j, t + n + j);
+  if (t_slice > 0) {
+    double *t1 = t + slice_t1(j, t_slice);
+    shift_moments(mk[j], qk[j], c, nk, t1, t1 + t_slice);
+  } else {
+    shift_moments(mk[j], qk[j], c, nk, t + j, t + n + j);
+  }
 }
 
 template <typename ShiftT>
@@ -1318,10 +1343,13 @@ __global__ __launch_bounds__(kBlock) void k_chan_shift_finish(const double *__re
                                                               const ShiftT *__restrict__ shift,
                                                               const double *__restrict__ off3, int64_t n_sel,
                                                               double nf, double *__restrict__ mean,
-                                                              double *__restrict__ m2, double *__restrict__ rmsf) {
+                                                              double *__restrict__ m2, double *__restrict__ rmsf,
+                                                              int64_t t2_off) {
+  // T2 at t + t2_off (3 n_sel for [T1 | T2]; the slice width for a
+  // reduce-scatter slice whose last rank holds fewer atoms)
   const int64_t a = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (a >= n_sel) return;
-  const int64_t n = 3 * n_sel;
+  const int64_t n = t2_off;
   double q[3];
 #pragma unroll
   for (int x = 0; x < 3; ++x) {
@@ -1898,13 +1926,13 @@ bool flat_layout(const float *d_xyz, int64_t fstride, int64_t n_sel, const int32
 
 int fold_shift_launch(const int64_t *hdr, const double *p0, int64_t n_coord, int64_t acc_n, double *acc0, double *acc1,
                       const void *shift, int shift_is_f32, const double *off3, double *t, int64_t l0, int64_t l1,
-                      int64_t t_n, int64_t threads, hipStream_t s) {
+                      int64_t t_n, int64_t threads, hipStream_t s, int64_t t_slice = 0) {
   if (shift_is_f32)
     hipLaunchKernelGGL(k_fold_sk<1>, dim3(grid1(threads)), dim3(kBlock), 0, s, hdr, p0, n_coord, (double)acc_n, acc0,
-                       acc1, shift, off3, t, l0, l1, t_n);
+                       acc1, shift, off3, t, l0, l1, t_n, t_slice);
   else
     hipLaunchKernelGGL(k_fold_sk<2>, dim3(grid1(threads)), dim3(kBlock), 0, s, hdr, p0, n_coord, (double)acc_n, acc0,
-                       acc1, shift, off3, t, l0, l1, t_n);
+                       acc1, shift, off3, t, l0, l1, t_n, t_slice);
   return after_launch("k_fold_sk");
 }
 
@@ -2059,7 +2087,8 @@ RMSF_EXPORT int rmsf_fold_balanced(const void *d_work, int64_t n_coord, int mode
   // accumulate kernel wrote
   // one thread per lane of >= 3 coordinates (the plan's cpl is on the device)
   hipLaunchKernelGGL(k_fold_sk<0>, dim3(grid1((n_coord + 2) / 3)), dim3(kBlock), 0, S(stream), hdr, p0, n_coord,
-                     (double)acc_n, d_acc0, d_acc1, nullptr, nullptr, nullptr, (int64_t)0, INT64_MAX, n_coord);
+                     (double)acc_n, d_acc0, d_acc1, nullptr, nullptr, nullptr, (int64_t)0, INT64_MAX, n_coord,
+                     (int64_t)0);
   return after_launch("k_fold_sk");
 }
 
@@ -2075,7 +2104,7 @@ RMSF_EXPORT int rmsf_fold_balanced_finalize(const void *d_work, int64_t n_coord,
   const double *p0 = reinterpret_cast<const double *>(hdr + kSkHdr);
   hipLaunchKernelGGL((k_fold_sk<0, true>), dim3(grid1((n_coord + 2) / 3)), dim3(kBlock), 0, S(stream), hdr, p0,
                      n_coord, (double)acc_n, d_acc0, d_acc1, nullptr, nullptr, nullptr, (int64_t)0, INT64_MAX, n_coord,
-                     d_rmsf, (double)n_total);
+                     (int64_t)0, d_rmsf, (double)n_total);
   return after_launch("k_fold_sk<FIN>");
 }
 
@@ -2088,6 +2117,19 @@ RMSF_EXPORT int rmsf_fold_balanced_shift(const void *d_work, int64_t n_coord, in
   const double *p0 = reinterpret_cast<const double *>(hdr + kSkHdr);
   return fold_shift_launch(hdr, p0, n_coord, acc_n, d_acc0, d_acc1, d_shift, shift_is_f32, d_off3, d_t, 0, INT64_MAX,
                            n_coord, (n_coord + 2) / 3, S(stream));
+}
+
+RMSF_EXPORT int rmsf_fold_balanced_shift_sliced(const void *d_work, int64_t n_coord, int64_t acc_n, double *d_acc0,
+                                                double *d_acc1, const void *d_shift, int shift_is_f32,
+                                                const double *d_off3, int64_t slice_coords, double *d_t,
+                                                void *stream) {
+  if (!d_work || !d_acc0 || !d_acc1 || !d_shift || !d_t || n_coord < 1 || acc_n < 0 || slice_coords < 3 ||
+      slice_coords % 3)
+    return fail(RMSF_EINVAL, "rmsf_fold_balanced_shift_sliced: bad arguments");
+  const int64_t *hdr = static_cast<const int64_t *>(d_work);
+  const double *p0 = reinterpret_cast<const double *>(hdr + kSkHdr);
+  return fold_shift_launch(hdr, p0, n_coord, acc_n, d_acc0, d_acc1, d_shift, shift_is_f32, d_off3, d_t, 0, INT64_MAX,
+                           n_coord, (n_coord + 2) / 3, S(stream), slice_coords);
 }
 
 // ---- atom slabs of the flat balanced plan (C4's merge overlap) ------------
@@ -2193,32 +2235,61 @@ RMSF_EXPORT int rmsf_chan_deviation(const double *d_mean_k, const double *d_m2_k
   return after_launch("k_chan_deviation");
 }
 
-RMSF_EXPORT int rmsf_chan_shift_pack(const double *d_mean_k, const double *d_m2_k, const void *d_shift,
-                                     int shift_is_f32, const double *d_off3, double n_k, int64_t n, double *d_t,
-                                     void *stream) {
-  if (!d_mean_k || !d_m2_k || !d_shift || !d_t || n < 1 || n_k < 0)
+namespace {
+int shift_pack(const double *d_mean_k, const double *d_m2_k, const void *d_shift, int shift_is_f32,
+               const double *d_off3, double n_k, int64_t n, double *d_t, int64_t t_slice, void *stream) {
+  if (!d_mean_k || !d_m2_k || !d_shift || !d_t || n < 1 || n_k < 0 || t_slice < 0)
     return fail(RMSF_EINVAL, "rmsf_chan_shift_pack: bad arguments");
   if (shift_is_f32)
     hipLaunchKernelGGL(k_chan_shift_pack<float>, dim3(grid1(n)), dim3(kBlock), 0, S(stream), d_mean_k, d_m2_k,
-                       static_cast<const float *>(d_shift), d_off3, n_k, n, d_t);
+                       static_cast<const float *>(d_shift), d_off3, n_k, n, d_t, t_slice);
   else
     hipLaunchKernelGGL(k_chan_shift_pack<double>, dim3(grid1(n)), dim3(kBlock), 0, S(stream), d_mean_k, d_m2_k,
-                       static_cast<const double *>(d_shift), d_off3, n_k, n, d_t);
+                       static_cast<const double *>(d_shift), d_off3, n_k, n, d_t, t_slice);
   return after_launch("k_chan_shift_pack");
+}
+
+int shift_finish(const double *d_t, int64_t t2_off, const void *d_shift, int shift_is_f32, const double *d_off3,
+                 int64_t n_sel, int64_t n_frames, double *d_mean, double *d_m2, double *d_rmsf, void *stream) {
+  if (!d_t || !d_shift || !d_mean || !d_m2 || n_sel < 1 || t2_off < 3 * n_sel)
+    return fail(RMSF_EINVAL, "rmsf_chan_shift_finish: bad arguments");
+  if (n_frames < 1) return fail(RMSF_EEMPTY, "rmsf_chan_shift_finish: no frames");
+  if (shift_is_f32)
+    hipLaunchKernelGGL(k_chan_shift_finish<float>, dim3(grid1(n_sel)), dim3(kBlock), 0, S(stream), d_t,
+                       static_cast<const float *>(d_shift), d_off3, n_sel, (double)n_frames, d_mean, d_m2, d_rmsf,
+                       t2_off);
+  else
+    hipLaunchKernelGGL(k_chan_shift_finish<double>, dim3(grid1(n_sel)), dim3(kBlock), 0, S(stream), d_t,
+                       static_cast<const double *>(d_shift), d_off3, n_sel, (double)n_frames, d_mean, d_m2, d_rmsf,
+                       t2_off);
+  return after_launch("k_chan_shift_finish");
+}
+}  // namespace
+
+RMSF_EXPORT int rmsf_chan_shift_pack(const double *d_mean_k, const double *d_m2_k, const void *d_shift,
+                                     int shift_is_f32, const double *d_off3, double n_k, int64_t n, double *d_t,
+                                     void *stream) {
+  return shift_pack(d_mean_k, d_m2_k, d_shift, shift_is_f32, d_off3, n_k, n, d_t, 0, stream);
+}
+
+RMSF_EXPORT int rmsf_chan_shift_pack_sliced(const double *d_mean_k, const double *d_m2_k, const void *d_shift,
+                                            int shift_is_f32, const double *d_off3, double n_k, int64_t n,
+                                            int64_t slice_coords, double *d_t, void *stream) {
+  if (slice_coords < 3 || slice_coords % 3) return fail(RMSF_EINVAL, "rmsf_chan_shift_pack_sliced: bad slice width");
+  return shift_pack(d_mean_k, d_m2_k, d_shift, shift_is_f32, d_off3, n_k, n, d_t, slice_coords, stream);
 }
 
 RMSF_EXPORT int rmsf_chan_shift_finish(const double *d_t, const void *d_shift, int shift_is_f32, const double *d_off3,
                                        int64_t n_sel, int64_t n_frames, double *d_mean, double *d_m2,
                                        double *d_rmsf, void *stream) {
-  if (!d_t || !d_shift || !d_mean || !d_m2 || n_sel < 1) return fail(RMSF_EINVAL, "rmsf_chan_shift_finish: bad arguments");
-  if (n_frames < 1) return fail(RMSF_EEMPTY, "rmsf_chan_shift_finish: no frames");
-  if (shift_is_f32)
-    hipLaunchKernelGGL(k_chan_shift_finish<float>, dim3(grid1(n_sel)), dim3(kBlock), 0, S(stream), d_t,
-                       static_cast<const float *>(d_shift), d_off3, n_sel, (double)n_frames, d_mean, d_m2, d_rmsf);
-  else
-    hipLaunchKernelGGL(k_chan_shift_finish<double>, dim3(grid1(n_sel)), dim3(kBlock), 0, S(stream), d_t,
-                       static_cast<const double *>(d_shift), d_off3, n_sel, (double)n_frames, d_mean, d_m2, d_rmsf);
-  return after_launch("k_chan_shift_finish");
+  return shift_finish(d_t, 3 * n_sel, d_shift, shift_is_f32, d_off3, n_sel, n_frames, d_mean, d_m2, d_rmsf, stream);
+}
+
+RMSF_EXPORT int rmsf_chan_shift_finish_slice(const double *d_t, int64_t slice_coords, const void *d_shift,
+                                             int shift_is_f32, const double *d_off3, int64_t n_sel, int64_t n_frames,
+                                             double *d_mean, double *d_m2, double *d_rmsf, void *stream) {
+  return shift_finish(d_t, slice_coords, d_shift, shift_is_f32, d_off3, n_sel, n_frames, d_mean, d_m2, d_rmsf,
+                      stream);
 }
 
 RMSF_EXPORT int rmsf_finalize(const double *d_m2, int64_t n_sel, int64_t n_frames, double *d_rmsf, void *stream) {

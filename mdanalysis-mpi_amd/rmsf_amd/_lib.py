@@ -75,6 +75,9 @@ SIGNATURES = {
     "rmsf_finalize": (c_int, [P, c_int64, c_int64, P, P]),
     "rmsf_chan_shift_pack": (c_int, [P, P, P, c_int, P, c_double, c_int64, P, P]),
     "rmsf_fold_balanced_shift": (c_int, [P, c_int64, c_int64, P, P, P, c_int, P, P, P]),
+    "rmsf_fold_balanced_shift_sliced": (c_int, [P, c_int64, c_int64, P, P, P, c_int, P, c_int64, P, P]),
+    "rmsf_chan_shift_pack_sliced": (c_int, [P, P, P, c_int, P, c_double, c_int64, c_int64, P, P]),
+    "rmsf_chan_shift_finish_slice": (c_int, [P, c_int64, P, c_int, P, c_int64, c_int64, P, P, P, P]),
     "rmsf_balanced_slab_chunks": (c_int, [P, c_int64, c_int64, c_int64, P]),
     "rmsf_accumulate_balanced_slab": (c_int, [P, c_int64, c_int64, c_int64, c_int64, c_int64, P, c_size_t, P]),
     "rmsf_fold_balanced_shift_slab": (c_int, [P, c_int64, c_int64, P, P, P, c_int, P, P, c_int64, c_int64, P]),

@@ -148,6 +148,19 @@ class Engine:
         call("rmsf_fold_balanced_shift", work.data_ptr(), n_coord, acc_n, acc0.data_ptr(), acc1.data_ptr(),
              shift.data_ptr(), int(shift.dtype == torch.float32), _ptr(off3), out.data_ptr(), self.stream)
 
+    def fold_balanced_shift_sliced(self, work: torch.Tensor, n_coord: int, acc_n: int, acc0: torch.Tensor,
+                                   acc1: torch.Tensor, shift: torch.Tensor, off3, slice_coords: int,
+                                   out: torch.Tensor) -> None:
+        """fold_balanced_shift writing the reduce-scatter merge's atom-sliced
+        layout: slice r (slice_coords coordinates) as [T1 | T2] at
+        out[2 r slice_coords:]."""
+        n_slices = -(-n_coord // slice_coords)
+        if out.numel() < 2 * slice_coords * n_slices or shift.numel() < n_coord:
+            raise ValueError("fold_balanced_shift_sliced: buffer sizes")
+        call("rmsf_fold_balanced_shift_sliced", work.data_ptr(), n_coord, acc_n, acc0.data_ptr(), acc1.data_ptr(),
+             shift.data_ptr(), int(shift.dtype == torch.float32), _ptr(off3), slice_coords, out.data_ptr(),
+             self.stream)
+
     def balanced_slab_chunks(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int) -> int:
         """Chunks (1024 coordinates each) of the flat balanced plan when it is
         chunk-aligned (atom slabs possible), else 0."""
@@ -206,6 +219,26 @@ class Engine:
             raise ValueError("chan_shift_finish: buffer sizes")
         call("rmsf_chan_shift_finish", t.data_ptr(), shift.data_ptr(), int(shift.dtype == torch.float32), _ptr(off3),
              n_sel, n_frames, mean.data_ptr(), m2.data_ptr(), _ptr(rmsf), self.stream)
+
+    def chan_shift_pack_sliced(self, mean_k, m2_k, shift, off3, n_k: float, slice_coords: int, out) -> None:
+        """chan_shift_pack into the atom-sliced layout (see
+        fold_balanced_shift_sliced)."""
+        n = mean_k.numel()
+        if out.numel() < 2 * slice_coords * -(-n // slice_coords) or shift.numel() < n:
+            raise ValueError("chan_shift_pack_sliced: buffer sizes")
+        call("rmsf_chan_shift_pack_sliced", mean_k.data_ptr(), m2_k.data_ptr(), shift.data_ptr(),
+             int(shift.dtype == torch.float32), _ptr(off3), float(n_k), n, slice_coords, out.data_ptr(), self.stream)
+
+    def chan_shift_finish_slice(self, t, slice_coords: int, shift, off3, n_sel: int, n_frames: int, mean, m2,
+                                rmsf) -> None:
+        """Unpack one reduced slice [T1 | T2] (width slice_coords) for its
+        n_sel atoms; shift / mean / m2 / rmsf start at the slice's first atom."""
+        if (t.numel() < 2 * slice_coords or 3 * n_sel > slice_coords or shift.numel() < 3 * n_sel
+                or mean.numel() < 3 * n_sel or m2.numel() < 3 * n_sel):
+            raise ValueError("chan_shift_finish_slice: buffer sizes")
+        call("rmsf_chan_shift_finish_slice", t.data_ptr(), slice_coords, shift.data_ptr(),
+             int(shift.dtype == torch.float32), _ptr(off3), n_sel, n_frames, mean.data_ptr(), m2.data_ptr(),
+             _ptr(rmsf), self.stream)
 
     def zero_index(self) -> torch.Tensor:
         """A resident int64 [0] (row index for gathering one frame); made once."""

@@ -8,8 +8,10 @@ Replaces the mpi4py layer of RMSF.py:
            of moments about a shift every rank holds (the pipeline's form;
            ``root=r``: a reduce to rank r, RMSF.py:143's own shape), or
            ``global_chan``: the same merge as two all-reduce(SUM) passes
-           (mean, then deviations) -- over RCCL (torch.distributed "nccl"
-           backend = RCCL on ROCm).
+           (mean, then deviations), or ``global_chan_scatter``: a
+           reduce-scatter of the same moments by atom slices, each rank
+           finishing its slice, and only the RMSF gathered to the root --
+           over RCCL (torch.distributed "nccl" backend = RCCL on ROCm).
 
 One process per GPU (torch.distributed.run); the frames shard with no data
 path collective except these exchange steps.  The merges take an ``ops``
@@ -143,6 +145,97 @@ def global_chan_shifted(ops, mean_k: torch.Tensor, m2_k: torch.Tensor, n_k: int,
     rmsf = torch.empty(n // 3, dtype=mean_k.dtype, device=mean_k.device)
     ops.chan_shift_finish(t, shift, off3, n // 3, n_total, mean, m2, rmsf)
     return mean, m2, rmsf
+
+
+def _staged(t: torch.Tensor) -> bool:
+    """gloo moves CUDA tensors through host memory for some collectives and
+    not at all for others: stage those through the host ourselves (rehearsal
+    transport only; RCCL takes device tensors directly)."""
+    return t.is_cuda and dist.get_backend() == "gloo"
+
+
+def reduce_scatter_sum_(out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+    """``out`` (rank r) = sum over ranks of ``inp``'s r-th of ``size`` equal
+    chunks (RCCL reduce-scatter); ``out`` = ``inp`` for a single process."""
+    _, size = world()
+    if size == 1:
+        out.copy_(inp[:out.numel()])
+    elif _staged(inp):
+        h = torch.empty(out.numel(), dtype=out.dtype)
+        dist.reduce_scatter_tensor(h, inp.cpu())
+        out.copy_(h)
+    else:
+        dist.reduce_scatter_tensor(out, inp)
+    return out
+
+
+def gather_(t: torch.Tensor, root: int):
+    """Every rank's ``t`` (equal sizes) concatenated in rank order on
+    ``root``; None on the other ranks."""
+    rank, size = world()
+    if size == 1:
+        return t
+    staged = _staged(t)
+    src = t.cpu() if staged else t
+    parts = [torch.empty_like(src) for _ in range(size)] if rank == root else None
+    dist.gather(src, parts, dst=root)
+    if rank != root:
+        return None
+    out = torch.cat(parts)
+    return out.to(t.device) if staged else out
+
+
+def global_chan_scatter(ops, mean_k: torch.Tensor, m2_k: torch.Tensor, n_k: int, n_total: int, shift: torch.Tensor,
+                        off3: torch.Tensor | None = None, shift_work=None, packed: torch.Tensor | None = None,
+                        slice_coords: int | None = None, root: int = 0):
+    """The one-collective merge as a REDUCE-SCATTER by atom slices: rank r
+    receives the summed T1/T2 of atoms [r p, (r+1) p) (p = ceil(n_sel/size)),
+    finishes them (mean, M2 and RMSF.py:146 for its atoms), and only the RMSF
+    (8 B per atom) is gathered to ``root`` -- RMSF.py:143's result on the
+    root, with each rank's link carrying (size-1)/size of the moments plus
+    the RMSF instead of the whole moments (reduce) or twice (all-reduce).
+    ``packed``: the T1/T2 already written in the atom-sliced layout by the
+    last fold (``slice_coords`` = 3 p).  Returns (rmsf on root else None,
+    mean slice, M2 slice, (a0, a1)) -- the statistics stay sliced."""
+    rank, size = world()
+    if n_total <= 0:
+        raise ZeroDivisionError("global_chan_scatter: no frames on any rank")
+    n = mean_k.numel()
+    n_sel = n // 3
+    per = -(-n_sel // size)
+    sc = 3 * per
+    if slice_coords is not None and slice_coords != sc:
+        raise ValueError(f"global_chan_scatter: packed with slice width {slice_coords}, expected {sc}")
+    if packed is not None:
+        t = packed
+    else:
+        t = torch.empty(2 * sc * size, dtype=mean_k.dtype, device=mean_k.device)
+        if shift_work is not None:
+            shift_work.wait()
+        ops.chan_shift_pack_sliced(mean_k, m2_k, shift, off3, float(n_k), sc, t)
+    zero_slice_padding(t, n, sc, size)
+    out = torch.empty(2 * sc, dtype=t.dtype, device=t.device)
+    reduce_scatter_sum_(out, t)
+    a0, a1 = min(rank * per, n_sel), min((rank + 1) * per, n_sel)
+    mean_s = torch.empty(3 * (a1 - a0), dtype=mean_k.dtype, device=mean_k.device)
+    m2_s = torch.empty_like(mean_s)
+    rmsf_s = torch.zeros(per, dtype=mean_k.dtype, device=mean_k.device)
+    if a1 > a0:
+        ops.chan_shift_finish_slice(out, sc, shift.reshape(-1)[3 * a0:], off3, a1 - a0, n_total, mean_s, m2_s,
+                                    rmsf_s)
+    full = gather_(rmsf_s, root)
+    return (None if full is None else full[:n_sel]), mean_s, m2_s, (a0, a1)
+
+
+def zero_slice_padding(t: torch.Tensor, n: int, sc: int, size: int) -> None:
+    """Zero the never-written coordinates of the atom-sliced layout (past the
+    n real ones, in the last slices), so the reduce-scatter sums zeros there."""
+    for r in range(size):
+        valid = max(0, min(sc, n - r * sc))
+        if valid < sc:
+            base = 2 * r * sc
+            t[base + valid:base + sc].zero_()
+            t[base + sc + valid:base + 2 * sc].zero_()
 
 
 def barrier() -> None:

@@ -119,10 +119,12 @@ class Accumulator:
 
     def add(self, b: Batch, xform: torch.Tensor | None = None, refinfo: torch.Tensor | None = None,
             pack=None, fin=None) -> None:
-        """``pack`` = (shift, off3, t, pending broadcast or None): this is the
-        rank's last batch before the cross-rank merge; on the balanced grid
-        in WELFORD mode the fold also writes the merge's moments about the
-        shift into ``t`` (one launch; ``self.packed`` tells the caller).
+        """``pack`` = (shift, off3, t, pending broadcast or None[, slice
+        width]): this is the rank's last batch before the cross-rank merge;
+        on the balanced grid in WELFORD mode the fold also writes the merge's
+        moments about the shift into ``t`` (one launch; ``self.packed`` tells
+        the caller) -- in the reduce-scatter merge's atom-sliced layout when a
+        slice width is given.
         ``fin`` = (rmsf, n_total): the last batch of an aligned single-rank
         sweep; the fold also finalises (RMSF.py:146, ``self.finalized``)."""
         eng = self.eng
@@ -135,10 +137,15 @@ class Accumulator:
                 eng.accumulate_balanced(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, xform, refinfo, self.mode,
                                         self.work, pstride=b.pstride)
             if pack is not None and self.mode == RMSF_MODE_WELFORD:
-                shift, off3, t, work = pack
+                shift, off3, t, work = pack[:4]
+                sc = pack[4] if len(pack) > 4 else None
                 if work is not None:
                     work.wait()  # the shift's broadcast ran beside the sweep
-                eng.fold_balanced_shift(self.work, self.n_coord, self.n, self.parts0[0], p1, shift, off3, t)
+                if sc:
+                    eng.fold_balanced_shift_sliced(self.work, self.n_coord, self.n, self.parts0[0], p1, shift, off3,
+                                                   sc, t)
+                else:
+                    eng.fold_balanced_shift(self.work, self.n_coord, self.n, self.parts0[0], p1, shift, off3, t)
                 self.packed = True
             elif fin is not None and self.mode == RMSF_MODE_WELFORD and self.aligned:
                 eng.fold_balanced_finalize(self.work, self.n_coord, self.n, self.parts0[0], p1, fin[1], fin[0])
@@ -338,14 +345,20 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                  max_batch: int | None = None, n_splits: int | None = None, collect_rmsd: bool = False,
                  ref_owner: int | None = None, block: tuple[int, int] | None = None,
                  timer: KernelTimer | None = None, collect_transforms: bool = False,
-                 merge_slabs: int | None = None, merge_root: int | None = None) -> PipelineResult:
+                 merge_slabs: int | None = None, merge_root: int | None = None,
+                 merge_scatter: bool = False) -> PipelineResult:
     """``merge_slabs`` (N > 1, no alignment, HBM-resident block in one batch,
     flat chunk-aligned plan): cut the final sweep into that many atom slabs
     so each slab's cross-rank all-reduce overlaps the next slab's stream;
     None = SLABS_AUTO from SLAB_MIN_ATOMS selected atoms, 0/1 = off.
     ``merge_root`` (N > 1): the final merge is a reduce to that rank, as
     RMSF.py:143's ``comm.reduce(root=0)``; the other ranks' results are None
-    (rmsf, mean, m2), like RMSF.py's non-root ranks."""
+    (rmsf, mean, m2), like RMSF.py's non-root ranks.
+    ``merge_scatter`` (N > 1): the merge as a reduce-scatter by atom slices
+    (parallel.global_chan_scatter): each rank finishes its slice and only
+    the RMSF is gathered to ``merge_root`` (default 0); ``mean``/``m2`` are
+    None and each rank's slice of them is in ``extras`` ("atom_slice",
+    "slice_mean", "slice_m2")."""
     if align not in ALIGN_MODES:
         raise ValueError(f"align must be one of {ALIGN_MODES}, got {align!r}")
     rank, size = parallel.world()
@@ -355,6 +368,9 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     if merge_root is not None and not 0 <= merge_root < size:
         raise ValueError(f"merge_root {merge_root} is not a rank of this {size}-rank group")
     root = merge_root if size > 1 else None
+    scatter = bool(merge_scatter) and size > 1
+    if scatter and root is None:
+        root = 0
     std = parallel.blocks(n_total, size)[rank]
     if block is not None and size > 1 and tuple(block) != std:
         # the merge's shift frame (and RMSF.py's decomposition) is defined by
@@ -375,6 +391,9 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     # coordinate planes read in place by the unaligned accumulate: statistics
     # in plane order, permuted to (atom, xyz) at the end
     planes = not aligned and not n_splits and bool(getattr(source, "native_planes", False))
+    if scatter and planes:
+        raise ValueError("merge_scatter: the statistics of coordinate planes read in place are in plane order, "
+                         "not atom order; use merge_root")
     batches_of = source.raw_batches if planes else source.batches
     if not planes and not n_splits and isinstance(source, DeviceSource) and source.layout == "soa":
         batches_of = source.plane_batches_in_place  # the kernels' plane variants read HBM planes in place
@@ -401,7 +420,7 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
             if slabs and done == 0 and last and b.sel is None and xf is None and not b.pstride:
                 n_chunks = eng.balanced_slab_chunks(b.ptr, b.fstride, b.n_frames, n_sel)
                 if n_chunks >= 2 * 3:
-                    shift_, off3_, _, work_ = pack
+                    shift_, off3_, _, work_ = pack[:4]
                     slabbed = _slab_sweep(eng, acc, b, _slab_bounds(n_chunks, slabs), shift_, off3_, work_, timer,
                                           root)
             if slabbed is None:
@@ -439,14 +458,16 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     acc = Accumulator(eng, n_sel, RMSF_MODE_WELFORD, max_batch, aligned, n_splits, timer)
     # N > 1: the last batch's fold also packs the merge's moments (one launch);
     # large selections in one resident batch run as overlapped atom slabs
-    t = torch.empty(6 * n_sel, dtype=torch.float64, device=eng.device) if size > 1 else None
+    sc = 3 * -(-n_sel // size) if scatter else None   # the reduce-scatter's slice width (coordinates)
+    t = (torch.empty(2 * sc * size if scatter else 6 * n_sel, dtype=torch.float64, device=eng.device)
+         if size > 1 else None)
     k_slabs = merge_slabs if merge_slabs is not None else (SLABS_AUTO if n_sel >= SLAB_MIN_ATOMS else 0)
-    slabs = k_slabs if (size > 1 and k_slabs > 1 and not aligned and not n_splits) else None
+    slabs = k_slabs if (size > 1 and k_slabs > 1 and not aligned and not n_splits and not scatter) else None
     slabbed = None
     # one rank, aligned: the last fold also finalises (RMSF.py:146)
     rmsf_fin = eng.empty(n_sel) if (size == 1 and aligned) else None
     if n_local:
-        slabbed = sweep(acc, ref, info, xf_last, (shift, off3, t, shift_work) if size > 1 else None, slabs,
+        slabbed = sweep(acc, ref, info, xf_last, (shift, off3, t, shift_work, sc) if size > 1 else None, slabs,
                         (rmsf_fin, n_total) if rmsf_fin is not None else None)
     if slabbed is not None:                                  # RMSF.py:141-143 + 146, slab by slab
         if root is not None and rank != root:
@@ -466,6 +487,15 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
         return PipelineResult(rmsf=rmsf, mean=mean.view(n_sel, 3), m2=m2.view(n_sel, 3), n_frames=n_total,
                               n_local=n_local, block=(b0, b1), average=None, rmsd=rmsd,
                               extras={"merge_slabs": len(slabbed), "merge_root": root})
+    if scatter:                                              # RMSF.py:141-143 + 146 by atom slices
+        rmsf, mean_s, m2_s, (a0, a1) = parallel.global_chan_scatter(
+            eng, acc.result0, acc.result1, acc.n, n_total, shift, off3, None if acc.packed else shift_work,
+            packed=t if acc.packed else None, slice_coords=sc, root=root)
+        return PipelineResult(rmsf=rmsf, mean=None, m2=None, n_frames=n_total, n_local=n_local, block=(b0, b1),
+                              average=None if average is None else average.view(n_sel, 3), rmsd=rmsd,
+                              transforms=xf_last, transforms_sweep1=xf_first,
+                              extras={"merge_root": root, "merge": "scatter", "atom_slice": (a0, a1),
+                                      "slice_mean": mean_s.view(-1, 3), "slice_m2": m2_s.view(-1, 3)})
     if size > 1:                                             # RMSF.py:141-143 + 146: one all-reduce
         mean, m2, rmsf = parallel.global_chan_shifted(eng, acc.result0, acc.result1, acc.n, n_total,
                                                       shift, off3, None if acc.packed else shift_work,

@@ -42,6 +42,28 @@ class OracleOps:
         out.copy_(torch.from_numpy(np.concatenate([n_k * d, m2_k.numpy() + n_k * (d * d)])))
 
     @staticmethod
+    def chan_shift_pack_sliced(mean_k, m2_k, shift, off3, n_k, sc, out):
+        """the atom-sliced layout: slice r = [T1 | T2] of coordinates
+        [r sc, (r+1) sc) at out[2 r sc:]"""
+        nn = mean_k.numel()
+        d = mean_k.numpy() - OracleOps._c(shift, off3, nn)
+        t1, t2 = n_k * d, m2_k.numpy() + n_k * (d * d)
+        o = out.numpy()
+        for r in range(-(-nn // sc)):
+            a, b = r * sc, min(nn, (r + 1) * sc)
+            o[2 * r * sc:2 * r * sc + b - a] = t1[a:b]
+            o[2 * r * sc + sc:2 * r * sc + sc + b - a] = t2[a:b]
+
+    @staticmethod
+    def chan_shift_finish_slice(t, sc, shift, off3, n_sel, n, mean, m2, rmsf):
+        c = OracleOps._c(shift, off3, 3 * n_sel)
+        t1, t2 = t.numpy()[:3 * n_sel], t.numpy()[sc:sc + 3 * n_sel]
+        q = np.maximum(t2 - t1 * (t1 / n), 0.0)
+        mean.copy_(torch.from_numpy(c + t1 / n))
+        m2.copy_(torch.from_numpy(q))
+        rmsf[:n_sel].copy_(torch.from_numpy(np.sqrt(q.reshape(-1, 3).sum(axis=1) / n)))
+
+    @staticmethod
     def chan_shift_finish(t, shift, off3, n_sel, n, mean, m2, rmsf):
         c = OracleOps._c(shift, off3, 3 * n_sel)
         t1, t2 = t.numpy()[:3 * n_sel], t.numpy()[3 * n_sel:6 * n_sel]
@@ -83,7 +105,7 @@ def _worker(rank, size, port, n_frames, q, merge="two"):
             # reference (f64 centred + COM: align="frame0"'s form), by the
             # sweep-1 average (f64: align="average"), or by frame 0 (f32,
             # broadcast by the owner of block 0: no alignment)
-            if merge in ("ref", "root"):
+            if merge in ("ref", "root", "scatter"):
                 shift, off3, work = torch.from_numpy(ref_c2.reshape(-1).copy()), torch.from_numpy(ref_com2), None
             elif merge == "average":
                 shift, off3, work = torch.from_numpy(avg.reshape(-1).copy()), None, None
@@ -93,21 +115,32 @@ def _worker(rank, size, port, n_frames, q, merge="two"):
                 if rank == owner:
                     shift.copy_(torch.from_numpy(traj[0][sel].reshape(-1)))
                 off3, work = None, parallel.broadcast_async(shift, owner)
-            mean, m2, rmsf_t = parallel.global_chan_shifted(OracleOps, mean_k, m2_k, n_k, n_frames, shift, off3,
-                                                            work, root=0 if merge == "root" else None)
+            if merge == "scatter":  # reduce-scatter by atom slices, RMSF gathered to rank 0
+                rmsf_t, mean_s, m2_s, (a0, a1) = parallel.global_chan_scatter(OracleOps, mean_k, m2_k, n_k, n_frames,
+                                                                             shift, off3, work, root=0)
+                mean_r, m2_r, _ = parallel.global_chan_shifted(OracleOps, mean_k, m2_k, n_k, n_frames, shift, off3)
+                # this rank's slice of the merged statistics: those of the all-reduce form
+                np.testing.assert_allclose(mean_s.numpy(), mean_r.numpy()[3 * a0:3 * a1], rtol=1e-14, atol=1e-14)
+                np.testing.assert_allclose(m2_s.numpy(), m2_r.numpy()[3 * a0:3 * a1], rtol=1e-12, atol=1e-14)
+            else:
+                mean, m2, rmsf_t = parallel.global_chan_shifted(OracleOps, mean_k, m2_k, n_k, n_frames, shift, off3,
+                                                                work, root=0 if merge == "root" else None)
             rmsf = None if rmsf_t is None else rmsf_t.numpy()
         q.put((rank, rmsf, avg))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("merge", ["two", "ref", "average", "frame0", "root"])
+@pytest.mark.parametrize("merge", ["two", "ref", "average", "frame0", "root", "scatter"])
 @pytest.mark.parametrize("size,n_frames", [(2, 40), (3, 40), (2, 1), (3, 2)])
 def test_gloo_two_sweep_merge(size, n_frames, merge):
     """world_size 2/3, including ranks with empty blocks (n_frames < size);
     the two-all-reduce Chan merge and the one-all-reduce shifted form with
     each of the pipeline's shifts; "root": the reduce to rank 0 of
-    RMSF.py:143 (the other ranks get no result)."""
+    RMSF.py:143 (the other ranks get no result); "scatter": the
+    reduce-scatter by atom slices (20 atoms over 3 ranks: a padded last
+    slice), each rank's slice of mean/M2 equal to the all-reduce form's and
+    the RMSF gathered to rank 0."""
     from oracle import rmsf_oracle as O
     from oracle import synth as SY
     from rmsf_amd.synth import motion_table
@@ -117,7 +150,7 @@ def test_gloo_two_sweep_merge(size, n_frames, merge):
     traj = SY.frames(8, 60, 0, n_frames, motion_table(9, n_frames))
     ref = O.rmsf_script(traj, np.arange(0, 60, 3), None, size=1, align="average")
     for rank, rmsf, avg in out:
-        if merge == "root" and rank != 0:
+        if merge in ("root", "scatter") and rank != 0:
             assert rmsf is None
         else:
             np.testing.assert_allclose(rmsf, ref["rmsf"], atol=1e-9)

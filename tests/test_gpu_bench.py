@@ -173,3 +173,21 @@ def test_torchrun_merge_all_same_checksum():
         lines[m] = json.loads(r.stdout.strip().splitlines()[-1])
     assert lines["root"]["config"]["merge"].startswith("reduce") and lines["all"]["config"]["merge"] == "all-reduce"
     assert lines["root"]["rmsf_checksum"] == lines["all"]["rmsf_checksum"]
+
+
+def test_torchrun_merge_scatter_same_checksum():
+    """bench --merge scatter (reduce-scatter by atom slices, RMSF gathered to
+    rank 0) under the driver's torchrun form, 2 gloo ranks on the GPU: the
+    checksum of --merge root, bit for bit (2 ranks: a + b either way)."""
+    common = ["--steps", "2", "--warmup", "1", "--n-atoms", "20001", "--frames", "301", "--no-cpu-baseline",
+              "--no-modes", "--gpus", "2", "--backend", "gloo"]
+    res = {}
+    for merge in ("root", "scatter"):
+        r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                            "bench.py", "--merge", merge] + common, cwd=ROOT, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res[merge] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["scatter"]["config"]["merge"].startswith("reduce-scatter")
+    assert res["scatter"]["rmsf_checksum"] == res["root"]["rmsf_checksum"]

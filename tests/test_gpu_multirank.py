@@ -373,3 +373,75 @@ def test_merge_to_root(size, n_atoms, align, slabs):
                 np.testing.assert_array_equal(a, b)
             else:
                 np.testing.assert_allclose(a, b, rtol=1e-13, atol=1e-13)
+
+
+def _scatter_worker(rank, size, init, q, n_atoms, n_frames, align):
+    sys.path[:0] = [ROOT, PKG]
+    import torch
+    import torch.distributed as dist
+
+    from conftest import init_gloo
+    init_gloo(init, rank, size)
+    try:
+        from rmsf_amd import parallel
+        from rmsf_amd.engine import Engine
+        from rmsf_amd.pipeline import run_pipeline
+        from rmsf_amd.sources import DeviceSource, FrameList
+        from rmsf_amd.synth import generate, motion_table
+        eng = Engine(torch.device("cuda", 0))
+        b0, b1 = parallel.blocks(n_frames, size)[rank]
+        mt = motion_table(7, n_frames) if align else None
+        shard = generate(eng, n_atoms, b0, b1 - b0, seed=15, motion=mt)
+        src = DeviceSource(shard, offset=b0, n_traj=n_frames)
+        fl = FrameList(n_frames)
+        every = run_pipeline(eng, src, fl, align=align, ref_owner=0)
+        sc = run_pipeline(eng, src, fl, align=align, ref_owner=0, merge_root=0, merge_scatter=True)
+        torch.cuda.synchronize()
+        a0, a1 = sc.extras["atom_slice"]
+        q.put((rank, [t.cpu().numpy() for t in (every.rmsf, every.mean, every.m2)],
+               None if sc.rmsf is None else sc.rmsf.cpu().numpy(),
+               (a0, a1, sc.extras["slice_mean"].cpu().numpy(), sc.extras["slice_m2"].cpu().numpy())))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("size,n_atoms,align", [(2, 3000, None), (3, 3001, None), (2, 3000, "frame0"),
+                                                (3, 2999, "average"), (4, 10, None)])
+def test_merge_reduce_scatter(size, n_atoms, align):
+    """The merge as a reduce-scatter by atom slices (bench --merge scatter):
+    each rank finishes its slice (the last one padded when size does not
+    divide the atoms) and only the RMSF is gathered to rank 0.  Rank r's
+    slice of mean and M2 and rank 0's RMSF equal the all-reduce merge's: bit
+    for bit with 2 ranks, within the collective's summation order with 3-4;
+    against the oracle's P-rank RMSF.py within 1e-6 A."""
+    from conftest import spawn_ranks
+    from oracle import rmsf_oracle as O
+    from oracle import synth as SY
+    from rmsf_amd.synth import motion_table
+    n_frames = 30 * size + 2
+    out = spawn_ranks(_scatter_worker, size, lambda r, init, q: (r, size, init, q, n_atoms, n_frames, align),
+                      timeout=200)
+    covered = 0
+    errors = [o for o in out if not isinstance(o[1], list)]
+    assert not errors, errors
+    for rank, every, rmsf, sl in sorted(out, key=lambda o: o[0]):
+        a0, a1, mean_s, m2_s = sl
+        covered += a1 - a0
+        pairs = [(mean_s, every[1][a0:a1]), (m2_s, every[2][a0:a1])]
+        if rank == 0:
+            pairs.append((rmsf, every[0]))
+        else:
+            assert rmsf is None
+        for got, exp in pairs:
+            if size == 2:
+                np.testing.assert_array_equal(got, exp)
+            else:
+                np.testing.assert_allclose(got, exp, rtol=1e-13, atol=1e-13)
+    assert covered == n_atoms
+    mt = motion_table(7, n_frames) if align else None
+    traj = SY.frames(15, n_atoms, 0, n_frames, mt)
+    exp = O.rmsf_script(traj, None, None, size=size, align=align)["rmsf"]
+    r0 = next(o for o in out if o[0] == 0)
+    np.testing.assert_allclose(r0[2], exp, rtol=0, atol=1e-6)

@@ -19,7 +19,11 @@ process, 10 back-to-back steps (wall clock, synchronised at the end) of:
                        (host_enqueue_ms), which must stay below one share's
                        device time for N real devices to run device-bound
                        ("host_in_loop" also counts the merge's wait for the
-                       shift frame's digest, i.e. for the previous step)
+                       shift frame's digest, i.e. for the previous step;
+                       on one GPU the 2N streams share 4 hardware queues, so
+                       a digest can queue behind another context's sweep)
+  context_step_N_tiny  the same over 8-frame blocks: the device work is
+                       negligible, so the call time is the host cost alone
 
 and checks that context_step_1 and the pipeline rank step give the same
 RMSF bit for bit (same kernels, same shift, same order).
@@ -150,10 +154,24 @@ def main():
         row[name + "_host_enqueue_ms"] = i      # the call alone, device idle
         print(f"  {name}: {w:.4f} ms/step wall; host {h:.4f} ms/step in the loop, {i:.4f} ms with the device idle",
               file=sys.stderr, flush=True)
+    # the host cost alone: N contexts over TINY blocks (8 frames each), so the
+    # device work (and the queues 2N streams share on one GPU) cannot hold the
+    # host up; with N real devices this is what the host adds per step
+    tiny = shard[:8]
+    w, h = wall(lambda: ctx_step(many, [tiny] * a.contexts), sync_ctxs(many), a.reps)
+    row[f"context_step_{a.contexts}_tiny_ms"] = w
+    row[f"context_step_{a.contexts}_tiny_host_enqueue_ms"] = idle_host(lambda: ctx_step(many, [tiny] * a.contexts),
+                                                                       sync_ctxs(many), a.reps)
+    w1, _ = wall(lambda: ctx_step(one, [tiny]), sync_ctxs(one), a.reps)
+    row["context_step_1_tiny_ms"] = w1
+    row["context_step_1_tiny_host_enqueue_ms"] = idle_host(lambda: ctx_step(one, [tiny]), sync_ctxs(one), a.reps)
+    print(f"  tiny blocks: {a.contexts} contexts {w:.4f} ms/step wall, "
+          f"{row[f'context_step_{a.contexts}_tiny_host_enqueue_ms']:.4f} ms host; 1 context {w1:.4f} ms wall, "
+          f"{row['context_step_1_tiny_host_enqueue_ms']:.4f} ms host", file=sys.stderr, flush=True)
     p = min(row["pipeline_rank_step_ms"], row["pipeline_rank_step_again_ms"])
     c1 = min(row["context_step_1_ms"], row["context_step_1_again_ms"])
     row["context_1_over_pipeline"] = c1 / p
-    row[f"context_{a.contexts}_host_enqueue_over_share_device_ms"] = row[f"context_step_{a.contexts}_host_enqueue_ms"] / p
+    row[f"context_{a.contexts}_tiny_host_over_share_step"] = row[f"context_step_{a.contexts}_tiny_host_enqueue_ms"] / p
     print(json.dumps(row), flush=True)
     for c in one + many:
         c.close()
