@@ -490,6 +490,21 @@ int digest_reference(rmsf_ctx *c) {
   return digest_into(c, 0, c->ref.p, false, c->n_coord, c->refinfo.p, 3);
 }
 
+// the merge shift frame's gather (selected rows of device frame d, f32) and
+// digest on the side stream, whose ordering the caller set up (side_begin)
+int shift_frame_on_side(rmsf_ctx *c, const float *d) {
+  if (!c->shift.p) CX_OK(c->shift.ensure(sizeof(float) * c->n_coord, c->side));
+  if (!c->zidx_set) {
+    CX_OK(c->zidx.ensure(sizeof(int64_t), c->side));
+    CX_HIP(hipMemsetAsync(c->zidx.p, 0, sizeof(int64_t), c->side));
+    c->zidx_set = true;
+  }
+  CX_OK(rmsf_gather_frames(d, 3 * c->n_atoms, static_cast<const int64_t *>(c->zidx.p), 1, c->n_sel, c->d_sel(),
+                           static_cast<float *>(c->shift.p), c->side));
+  c->shift_set = true;
+  return digest_into(c, 1, c->shift.p, true, c->n_coord, nullptr, 0);
+}
+
 // true when every context holds a reference (shift = false) or a merge shift
 // frame (shift = true) with the same digest; waits for the digests only
 int same_digests(rmsf_ctx **cs, int n, bool shift, bool *same) {
@@ -1554,19 +1569,10 @@ RMSF_EXPORT int rmsf_set_merge_shift_frame(rmsf_ctx *c, const float *xyz, int is
     CX_HIP(hipStreamSynchronize(c->stream));
     d = static_cast<const float *>(c->frame.p);
   }
-  CX_OK(c->shift.ensure(sizeof(float) * c->n_coord, c->stream));
-  if (!c->zidx_set) {
-    CX_OK(c->zidx.ensure(sizeof(int64_t), c->stream));
-    CX_HIP(hipMemsetAsync(c->zidx.p, 0, sizeof(int64_t), c->stream));
-    c->zidx_set = true;
-  }
   // on the side stream, after the work queued so far (a previous merge still
   // reading the old shift); the merge waits for ev_dig[1]
   CX_OK(side_begin(c));
-  CX_OK(rmsf_gather_frames(d, 3 * c->n_atoms, static_cast<const int64_t *>(c->zidx.p), 1, c->n_sel, c->d_sel(),
-                           static_cast<float *>(c->shift.p), c->side));
-  c->shift_set = true;
-  return digest_into(c, 1, c->shift.p, true, c->n_coord, nullptr, 0);
+  return shift_frame_on_side(c, d);
 }
 
 RMSF_EXPORT int rmsf_multi_push_frames(rmsf_ctx **cs, int n, const float *const *d_frames, const int64_t *n_frames,
@@ -1587,15 +1593,20 @@ RMSF_EXPORT int rmsf_multi_push_frames(rmsf_ctx **cs, int n, const float *const 
     if (flags & RMSF_MULTI_RESET)
       CX_OK(rmsf_ctx_reset(c, (mode == RMSF_PUSH_WELFORD || mode == RMSF_PUSH_ALIGN_WELFORD) ? 1 : 2));
     if (d_ref_frames && d_ref_frames[i]) CX_OK(rmsf_set_reference_frame(c, d_ref_frames[i], 1));
-    if (d_shift_frames && d_shift_frames[i]) CX_OK(rmsf_set_merge_shift_frame(c, d_shift_frames[i], 1));
+    // the shift frame is needed only by the merge: its gather is queued on
+    // the side stream AFTER this push's launches (so they leave the host
+    // first) but ordered after the work queued BEFORE them (a previous merge
+    // still reading the old shift), not after the sweep
+    const bool shift_after = d_shift_frames && d_shift_frames[i];
+    if (shift_after) CX_OK(side_begin(c));
     const int64_t nf = n_frames[i];
-    if (nf == 0) return RMSF_OK;
+    if (nf == 0) return shift_after ? shift_frame_on_side(c, d_shift_frames[i]) : RMSF_OK;
     const int64_t stride = frame_stride ? frame_stride : 3 * c->n_atoms;
     // the atom-slab merge (C4's size): a single unaligned launch group over
     // all atoms whose flat plan is chunk-aligned, recorded here and streamed
     // slab by slab by the next rmsf_multi_chan_merge_root
     const int k = merge_slabs == 0 ? (c->n_sel >= kSlabMinAtoms ? kSlabsAuto : 1) : merge_slabs;
-    if (k >= 2 && mode == RMSF_PUSH_WELFORD && !c->d_sel() && c->shift_set && nf <= kChunkFrames &&
+    if (k >= 2 && mode == RMSF_PUSH_WELFORD && !c->d_sel() && (c->shift_set || shift_after) && nf <= kChunkFrames &&
         c->wel.n == 0 && !c->slab.on && stride >= 3 * c->n_atoms) {
       int64_t chunks = 0;
       DeviceScope ds(c->dev);
@@ -1605,10 +1616,11 @@ RMSF_EXPORT int rmsf_multi_push_frames(rmsf_ctx **cs, int n, const float *const 
         c->slab = {true, d_frames[i], stride, nf, chunks, k};
         c->rmsf_valid = false;
         c->merged_away = false;
-        return RMSF_OK;
+        return shift_after ? shift_frame_on_side(c, d_shift_frames[i]) : RMSF_OK;
       }
     }
-    return rmsf_push_frames(c, d_frames[i], nf, stride, mode, 1);
+    CX_OK(rmsf_push_frames(c, d_frames[i], nf, stride, mode, 1));
+    return shift_after ? shift_frame_on_side(c, d_shift_frames[i]) : RMSF_OK;
   });
 }
 

@@ -254,8 +254,13 @@ class Context:
         coordinate planes, [F, 3, n_atoms] (SoA: x, y, z planes per frame),
         through the stager, which interleaves the selection on the host."""
         a = frames
-        if a.dtype != np.float32 or a.ndim != 3 or a.shape[1] != 3 or a.shape[2] != self.n_atoms or a.strides[2] != 4:
-            raise ValueError("push_planes: a float32 [F, 3, n_atoms] host array with contiguous planes is required")
+        if a.dtype != np.float32 or a.ndim != 3 or a.shape[1] != 3 or a.shape[2] != self.n_atoms:
+            raise ValueError("push_planes: a float32 [F, 3, n_atoms] host array is required")
+        s0, s1, s2 = a.strides
+        # the stager reads plane p of frame f at ptr[f] + p * plane_stride
+        # floats, n_atoms contiguous floats each: any other view is copied
+        if s2 != 4 or s1 < 0 or s0 < 0 or s1 % 4 or s0 % 4 or s1 < 4 * self.n_atoms or s0 < 3 * s1:
+            a = np.ascontiguousarray(a)
         r = np.asarray(rows, dtype=np.int64)
         if r.size and (r.min() < 0 or r.max() >= a.shape[0]):
             raise IndexError("push_planes: row out of range")

@@ -88,22 +88,30 @@ def test_soa_multi_device_path(c1, align):
 
 
 def test_soa_context_push(c1):
+    """push_planes of contiguous planes, of a transposed VIEW of the rows
+    (strides the stager cannot walk: copied first) and of padded
+    planes (a wider plane stride, walked in place) all equal push_rows."""
     from rmsf_amd.context import PUSH_WELFORD, Context
     d, traj = c1
     soa = _soa(traj)
+    wide = np.zeros((traj.shape[0], 3, traj.shape[1] + 5), dtype=np.float32)
+    wide[:, :, :traj.shape[1]] = soa
+    views = [("rows", traj), ("planes", soa), ("transposed view", traj.transpose(0, 2, 1)),
+             ("padded planes", wide[:, :, :traj.shape[1]])]
     out = []
-    for planes in (False, True):
+    for name, arr in views:
         c = Context(traj.shape[1], d["sel"])
         rows = np.array([0, 3, 4, 5, 50, 97])
-        if planes:
-            c.push_planes(soa, rows, PUSH_WELFORD)
+        if name == "rows":
+            c.push_rows(arr, rows, PUSH_WELFORD)
         else:
-            c.push_rows(traj, rows, PUSH_WELFORD)
+            c.push_planes(arr, rows, PUSH_WELFORD)
         out.append(c.partial())
         c.close()
-    assert out[0][0] == out[1][0] == 6
-    np.testing.assert_array_equal(out[0][1], out[1][1])
-    np.testing.assert_array_equal(out[0][2], out[1][2])
+    for o in out[1:]:
+        assert o[0] == 6
+        np.testing.assert_array_equal(out[0][1], o[1])
+        np.testing.assert_array_equal(out[0][2], o[2])
 
 
 @pytest.mark.parametrize("box", [None, (60.0, 90.0, 60.0, 90.0, 90.0, 60.0)])

@@ -7,9 +7,10 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=${1:-pmc_flops}
+WL=${2:-c3}    # c2 (flat Welford), c3 (superposition + aligned Welford), average (+ the aligned sum)
 timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 \
     SQ_INSTS_VALU_CVT SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_WAVES --output-format csv -d gpurun_out/$TAG -o run \
-    -- python3 bench.py --workload c3 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/$TAG.log 2>&1
+    -- python3 bench.py --workload $WL --steps 2 --warmup 1 --no-cpu-baseline --no-modes > gpurun_out/$TAG.log 2>&1
 rc=$?; echo rc=$rc; if [ $rc -ne 0 ]; then tail -5 gpurun_out/$TAG.log; exit $rc; fi
 python3 - "$TAG" <<'P'
 import csv, glob, json, sys
@@ -18,8 +19,10 @@ agg = {}
 for f in glob.glob(f"gpurun_out/{tag}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
-        for key in ("k_frame_stats", "k_accum_split_sk", "k_qcp_frames"):
-            if key in k:
+        for base in ("k_frame_stats", "k_accum_split_sk", "k_qcp_frames", "k_welford_flat_sk", "k_fold_sk"):
+            if base in k:
+                # the template arguments tell the sweeps apart (<0,...> Welford, <1,...> sum)
+                key = k.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
                 d = agg.setdefault(key, {})
                 d.setdefault(r["Counter_Name"], {}).setdefault(r.get("Dispatch_Id", r.get("Correlation_Id")), 0.0)
                 d[r["Counter_Name"]][r.get("Dispatch_Id", r.get("Correlation_Id"))] += float(r["Counter_Value"])
