@@ -204,7 +204,9 @@ def test_context_errors(c1):
 
 def test_plain_c_host_program(c1, tmp_path):
     """mdanalysis-mpi_amd/lib/rmsf_demo: RMSF.py's script written against the
-    C ABI alone, P contexts, host pushes in halves."""
+    C ABI alone, P contexts, host pushes in halves; --device: the blocks in
+    HBM and the one-process step (rmsf_multi_push_frames +
+    rmsf_multi_chan_merge_root)."""
     d, traj = c1
     exe = os.path.join(PKG, "lib", "rmsf_demo")
     f = tmp_path / "traj.f32"
@@ -213,7 +215,11 @@ def test_plain_c_host_program(c1, tmp_path):
     d["sel"].astype(np.int64).tofile(s)
     for P, mode, tag, extra in [(1, "average", "rmsf_average_P1", []), (2, "average", "rmsf_average_P2", []),
                                 (8, "frame0", "rmsf_frame0_P8", []), (2, "none", "rmsf_none_P2", []),
-                                (1, "average", "rmsf_average_P1", ["--rccl"])]:
+                                (1, "average", "rmsf_average_P1", ["--rccl"]),
+                                # the one-process step on HBM blocks: multi push + reduce to context 0
+                                (2, "none", "rmsf_none_P2", ["--device"]), (8, "frame0", "rmsf_frame0_P8", ["--device"]),
+                                (2, "average", "rmsf_average_P2", ["--device"]),
+                                (1, "none", "rmsf_none_P1", ["--device", "--rccl"])]:
         out = tmp_path / f"rmsf_{P}_{mode}.f64"
         r = subprocess.run([exe, str(f), "98", str(traj.shape[1]), str(s), "214", str(P), mode, str(out)] + extra,
                            capture_output=True, text=True, timeout=120)

@@ -5,7 +5,9 @@ frames / alignment / batch size, and merge slabs forced on where the flat
 plan allows them -- each rank's RMSF against the oracle's mpirun -n P
 emulation of RMSF.py.  ``--root``: half the cases merge with a reduce to a
 random rank (merge_root); ``--planes``: half the shards are HBM coordinate
-planes.  python tools/fuzz_multirank.py [n_cases [--root] [--planes]]"""
+planes; ``--scatter``: a third of the other cases merge as a reduce-scatter
+by atom slices with the RMSF gathered to a random root (merge_scatter).
+python tools/fuzz_multirank.py [n_cases [--root] [--planes] [--scatter]]"""
 import os
 import sys
 import tempfile
@@ -40,7 +42,7 @@ def _worker(rank, size, init, q, case):
         else:
             src = DeviceSource(shard, sel, offset=b0, n_traj=nf)
         res = run_pipeline(eng, src, FrameList(nf), align=align, max_batch=batch, merge_slabs=slabs,
-                           merge_root=case.get("root"))
+                           merge_root=case.get("root"), merge_scatter=bool(case.get("scatter")))
         torch.cuda.synchronize()
         q.put((rank, None if res.rmsf is None else res.rmsf.cpu().numpy(), res.extras.get("merge_slabs", 0)))
     except Exception as e:  # noqa: BLE001
@@ -93,6 +95,9 @@ def main():
             case["root"] = int(rng.integers(0, P))  # the merge as a reduce to this rank (RMSF.py:143)
         if "--planes" in sys.argv[2:] and rng.random() < 0.5:
             case["planes"] = True
+        if "--scatter" in sys.argv[2:] and not case.get("planes") and rng.random() < 0.34:
+            case["scatter"] = True  # reduce-scatter by atom slices, RMSF gathered to the root
+            case["root"] = int(rng.integers(0, P))
         out = run_case(case)
         if any(o[2] == -1 for o in out):
             print(f"case {k}: FAILED {[o[1] for o in out if o[2] == -1][:1]}", flush=True)
@@ -108,7 +113,8 @@ def main():
         d = max(float(np.abs(o[1] - exp).max()) for o in out if o[1] is not None)
         worst = max(worst, d)
         print(f"case {k:2d}: P={P} {na:7d} atoms {len(cols):7d} sel {nf:4d} frames align={align} "
-              f"batch={batch} slabs={out[0][2]} root={root} planes={bool(case.get('planes'))} max|d|={d:.2e}",
+              f"batch={batch} slabs={out[0][2]} root={root} planes={bool(case.get('planes'))} "
+              f"scatter={bool(case.get('scatter'))} max|d|={d:.2e}",
               flush=True)
         if d > 1e-6:
             print("EXCEEDS 1e-6", flush=True)
