@@ -88,3 +88,9 @@ def test_merge_defaults_to_reduce_to_root():
     assert bench.parse([]).merge == "root"
     assert bench.parse(["--merge", "all"]).merge == "all"
     assert bench.parse(["--merge", "all", "--merge-root"]).merge == "root"
+
+
+def test_merge_scatter_and_rehearsal_transport_flags():
+    a = bench.parse(["--merge", "scatter", "--gpus", "8", "--rehearse", "--rehearse-transport", "noop"])
+    assert a.merge == "scatter" and a.rehearse and a.rehearse_transport == "noop"
+    assert bench.parse([]).rehearse_transport == "fold"

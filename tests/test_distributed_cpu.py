@@ -155,3 +155,26 @@ def test_gloo_two_sweep_merge(size, n_frames, merge):
         else:
             np.testing.assert_allclose(rmsf, ref["rmsf"], atol=1e-9)
         np.testing.assert_allclose(avg, ref["average"], atol=1e-9)
+
+
+def test_scatter_layout_single_process():
+    """The atom-sliced layout of the reduce-scatter merge, one process: the
+    pad coordinates of the last slices are zeroed, and the merge equals the
+    one-all-reduce form (the oracle's ops; size 1 = no collective)."""
+    from rmsf_amd import parallel
+    t = torch.full((2 * 9 * 3,), 7.0, dtype=torch.float64)
+    parallel.zero_slice_padding(t, n=20, sc=9, size=3)   # slices of 9 coordinates, 20 real
+    t = t.numpy()
+    assert (t[:36] == 7).all()                             # slices 0 and 1 full
+    assert (t[36:38] == 7).all() and (t[38:45] == 0).all()  # slice 2: T1 has 2 real coordinates
+    assert (t[45:47] == 7).all() and (t[47:] == 0).all()    # ... and so has T2
+    rng = np.random.default_rng(5)
+    mean_k = torch.from_numpy(rng.normal(50, 3, 3 * 7))
+    m2_k = torch.from_numpy(rng.uniform(0, 2, 3 * 7))
+    shift = torch.from_numpy(rng.normal(50, 3, 3 * 7).astype(np.float32))
+    rmsf, mean_s, m2_s, sl = parallel.global_chan_scatter(OracleOps, mean_k, m2_k, 11, 11, shift)
+    mean, m2, rmsf2 = parallel.global_chan_shifted(OracleOps, mean_k, m2_k, 11, 11, shift)
+    assert sl == (0, 7)
+    np.testing.assert_array_equal(rmsf.numpy(), rmsf2.numpy())
+    np.testing.assert_array_equal(mean_s.numpy(), mean.numpy())
+    np.testing.assert_array_equal(m2_s.numpy(), m2.numpy())
