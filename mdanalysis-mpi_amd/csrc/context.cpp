@@ -320,6 +320,15 @@ int check_ctx(const rmsf_ctx *c, const char *fn) {
   return RMSF_OK;
 }
 
+// the context stream and its side stream (a shift frame's gather reads a
+// caller's frame there): what a getter waits for before the caller may free
+// what it pushed
+int sync_streams(rmsf_ctx *c) {
+  CX_HIP(hipStreamSynchronize(c->stream));
+  if (c->side) CX_HIP(hipStreamSynchronize(c->side));
+  return RMSF_OK;
+}
+
 int zero_running(rmsf_ctx *c, Running &r, bool two) {
   const size_t row = sizeof(double) * c->n_coord;
   CX_OK(r.parts0.ensure(row, c->stream, true));
@@ -550,11 +559,13 @@ int ensure_stager(rmsf_ctx *c) {
 // calling thread); the first failure is reported on the calling thread.
 int for_each_ctx(rmsf_ctx **cs, int n, const std::function<int(int)> &fn) {
   if (n == 1) return fn(0);
+  // every worker exists before any job is posted: a job must never outlive
+  // this frame (it refers to fn)
   for (int i = 1; i < n; ++i) {
     if (!cs[i]->worker) cs[i]->worker = new (std::nothrow) Worker;
     if (!cs[i]->worker) return fail(RMSF_ENOMEM, "rmsf_multi: cannot start a worker thread");
-    cs[i]->worker->post([&fn, i] { return fn(i); });
   }
+  for (int i = 1; i < n; ++i) cs[i]->worker->post([&fn, i] { return fn(i); });
   int rc = fn(0);
   std::string msg = rc ? std::string(rmsf_last_error()) : std::string();
   for (int i = 1; i < n; ++i) {
@@ -1089,7 +1100,7 @@ RMSF_EXPORT int rmsf_ctx_kernel_time(rmsf_ctx *c, int which, int64_t *launches, 
   if (which != RMSF_TIME_ACCUMULATE && which != RMSF_TIME_SUPERPOSE)
     return fail(RMSF_EINVAL, "rmsf_ctx_kernel_time: bad kernel");
   DeviceScope ds(c->dev);
-  CX_HIP(hipStreamSynchronize(c->stream));
+  CX_OK(sync_streams(c));
   int64_t k = 0;
   double t = 0.0, af = 0.0;
   for (auto &sp : c->spans) {
@@ -1373,7 +1384,7 @@ RMSF_EXPORT int rmsf_get_partial(rmsf_ctx *c, int64_t *n, double *h_mean, double
   const size_t row = sizeof(double) * c->n_coord;
   if (h_mean) CX_HIP(hipMemcpyAsync(h_mean, c->wel.parts0.p, row, hipMemcpyDeviceToHost, c->stream));
   if (h_m2) CX_HIP(hipMemcpyAsync(h_m2, c->wel.parts1.p, row, hipMemcpyDeviceToHost, c->stream));
-  CX_HIP(hipStreamSynchronize(c->stream));
+  CX_OK(sync_streams(c));
   if (n) *n = c->wel.n;
   return RMSF_OK;
 }
@@ -1385,7 +1396,7 @@ RMSF_EXPORT int rmsf_get_sum(rmsf_ctx *c, int64_t *n, double *h_sum) {
   CX_OK(ensure_zeroed(c, c->sum, false));
   if (h_sum)
     CX_HIP(hipMemcpyAsync(h_sum, c->sum.parts0.p, sizeof(double) * c->n_coord, hipMemcpyDeviceToHost, c->stream));
-  CX_HIP(hipStreamSynchronize(c->stream));
+  CX_OK(sync_streams(c));
   if (n) *n = c->sum.n;
   return RMSF_OK;
 }
@@ -1399,7 +1410,7 @@ RMSF_EXPORT int rmsf_get_average(rmsf_ctx *c, double *h_avg) {
   CX_OK(c->avg.ensure(sizeof(double) * c->n_coord, c->stream));
   CX_OK(rmsf_divide(c->sum.parts0.d(), (double)c->sum.n, c->n_coord, c->avg.d(), c->stream));
   CX_HIP(hipMemcpyAsync(h_avg, c->avg.p, sizeof(double) * c->n_coord, hipMemcpyDeviceToHost, c->stream));
-  CX_HIP(hipStreamSynchronize(c->stream));
+  CX_OK(sync_streams(c));
   return RMSF_OK;
 }
 
@@ -1417,7 +1428,7 @@ RMSF_EXPORT int rmsf_get_rmsf(rmsf_ctx *c, double *h_rmsf) {
     c->rmsf_valid = true;
   }
   CX_HIP(hipMemcpyAsync(h_rmsf, c->rmsf.p, sizeof(double) * c->n_sel, hipMemcpyDeviceToHost, c->stream));
-  CX_HIP(hipStreamSynchronize(c->stream));
+  CX_OK(sync_streams(c));
   return RMSF_OK;
 }
 
@@ -1572,7 +1583,11 @@ RMSF_EXPORT int rmsf_set_merge_shift_frame(rmsf_ctx *c, const float *xyz, int is
   // on the side stream, after the work queued so far (a previous merge still
   // reading the old shift); the merge waits for ev_dig[1]
   CX_OK(side_begin(c));
-  return shift_frame_on_side(c, d);
+  CX_OK(shift_frame_on_side(c, d));
+  // a host frame was staged in c->frame, which the next host setter reuses:
+  // the gather from it finishes here
+  if (!is_device_ptr) CX_HIP(hipStreamSynchronize(c->side));
+  return RMSF_OK;
 }
 
 RMSF_EXPORT int rmsf_multi_push_frames(rmsf_ctx **cs, int n, const float *const *d_frames, const int64_t *n_frames,

@@ -88,7 +88,7 @@ class Context:
         self.n_sel = len(self._sel) if self._sel is not None else int(n_sel if n_sel is not None else n_atoms)
         m = None if masses is None else _f64(masses, self.n_sel, "masses")
         self.device = device
-        self._alive = []     # device tensors read by queued work (released at the next synchronisation)
+        self._alive = {}     # device tensors read by queued work, by id (released at the next synchronisation)
         self._ext = None     # torch's view of the context stream (cached)
         self._h = ctypes.c_void_p()
         call("rmsf_ctx_create", device, self.n_atoms, self.n_sel,
@@ -172,7 +172,7 @@ class Context:
             # the setup kernels read the frame asynchronously on the context
             # stream: a temporary (e.g. a copy from another device) must
             # outlive them
-            self._alive.append(keep)
+            self._alive[id(keep)] = keep
 
     def set_merge_shift_frame(self, frame) -> None:
         """The merge's shift for unaligned Welford state: frame 0 of the frame
@@ -181,7 +181,7 @@ class Context:
         ptr, dev, keep = self._frames_ptr(frame, 1)
         call("rmsf_set_merge_shift_frame", self._h, ptr, dev)
         if dev:
-            self._alive.append(keep)
+            self._alive[id(keep)] = keep
 
     def set_reference_average(self) -> None:
         call("rmsf_set_reference_average", self._h)
@@ -224,7 +224,7 @@ class Context:
         if dev:
             # device frames are read asynchronously: the tensor is kept alive
             # until the context is next synchronised (no host sync here)
-            self._alive.append(keep)
+            self._alive[id(keep)] = keep
 
     def push_xtc(self, xtc, start: int = 0, stop: int | None = None, step: int = 1, mode: int = PUSH_WELFORD):
         stop = xtc.n_frames if stop is None else min(stop, xtc.n_frames)
@@ -406,7 +406,7 @@ class Context:
                     keep.append(f)
             if after_torch:
                 c._after_torch(t)
-            c._alive.extend(keep)
+            c._alive.update((id(k), k) for k in keep)
         h, _ = Context._handles(ctxs)
         call("rmsf_multi_push_frames", h, n, ptrs, counts, 0, int(mode), RMSF_MULTI_RESET if reset else 0,
              refs, shifts, int(merge_slabs))
