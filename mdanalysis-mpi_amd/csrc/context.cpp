@@ -270,6 +270,7 @@ struct rmsf_ctx {
   };
   bool timing = false;
   std::vector<Span> spans;
+  std::vector<hipEvent_t> event_pool;  // events of read spans, reused by the next ones
   // per-frame QCP rmsd of the aligned Welford pushes (rmsf_ctx_collect_rmsd)
   bool collect_rmsd = false;
   DevBuf rmsd;
@@ -354,9 +355,15 @@ template <class F>
 int timed(rmsf_ctx *c, int which, int64_t atom_frames, F &&launch) {
   if (!c->timing) return launch();
   rmsf_ctx::Span sp{nullptr, nullptr, which, atom_frames};
-  CX_HIP(hipEventCreate(&sp.a));
-  if (hipEventCreate(&sp.b) != hipSuccess) {
-    (void)hipEventDestroy(sp.a);
+  auto take = [c](hipEvent_t *e) -> hipError_t {
+    if (c->event_pool.empty()) return hipEventCreate(e);
+    *e = c->event_pool.back();
+    c->event_pool.pop_back();
+    return hipSuccess;
+  };
+  CX_HIP(take(&sp.a));
+  if (take(&sp.b) != hipSuccess) {
+    c->event_pool.push_back(sp.a);
     return fail(RMSF_EHIP, "hipEventCreate failed");
   }
   c->spans.push_back(sp);  // owned by the context from here on
@@ -366,17 +373,26 @@ int timed(rmsf_ctx *c, int which, int64_t atom_frames, F &&launch) {
   return RMSF_OK;
 }
 
+// which >= 0: the spans of that family are read -- their events go back to
+// the pool; which < 0: the context is destroyed -- every event is released
 void drop_spans(rmsf_ctx *c, int which) {
   std::vector<rmsf_ctx::Span> keep;
   for (auto &sp : c->spans) {
-    if (which < 0 || sp.which == which) {
+    if (which < 0) {
       (void)hipEventDestroy(sp.a);
       (void)hipEventDestroy(sp.b);
+    } else if (sp.which == which) {
+      c->event_pool.push_back(sp.a);
+      c->event_pool.push_back(sp.b);
     } else {
       keep.push_back(sp);
     }
   }
   c->spans.swap(keep);
+  if (which < 0) {
+    for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
+    c->event_pool.clear();
+  }
 }
 
 // the deferred fold of the last accumulate (plain: into the running state)
