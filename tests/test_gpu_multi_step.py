@@ -199,3 +199,26 @@ def test_noop_transport_and_lazy_reset(traj):
     np.testing.assert_allclose(ctxs[1].rmsf(), O.rmsf_two_pass(traj), rtol=0, atol=1e-9)
     for ctx in ctxs:
         ctx.close()
+
+
+@pytest.mark.parametrize("align", [None, "frame0"])
+def test_multi_push_selection_and_masses(traj, align):
+    """The one-process step over contexts with an atom selection (gathered in
+    the kernels; the shift frame is gathered to the selection too) and, when
+    aligned, heterogeneous masses (RMSF.py:84's mass-weighted COM): against
+    the oracle's 3-rank RMSF.py."""
+    from rmsf_amd.context import PUSH_ALIGN_WELFORD, PUSH_WELFORD, Context
+    P = 3
+    sel = np.sort(np.random.default_rng(7).choice(traj.shape[1], 321, replace=False))
+    masses = np.random.default_rng(8).uniform(1, 16, len(sel)) if align else None
+    x = torch.tensor(traj, device="cuda")
+    ctxs = [Context(traj.shape[1], sel=sel, masses=masses) for _ in range(P)]
+    if align:
+        Context.multi_push_frames(ctxs, _blocks(x, P), PUSH_ALIGN_WELFORD, ref_frames=[x[0]] * P)
+    else:
+        Context.multi_push_frames(ctxs, _blocks(x, P), PUSH_WELFORD, shift_frames=[x[0]] * P)
+    Context.multi_chan_merge(ctxs, root=1)
+    exp = O.rmsf_script(traj, sel, masses, size=P, align=align)["rmsf"]
+    np.testing.assert_allclose(ctxs[1].rmsf(), exp, rtol=0, atol=TOL)
+    for c in ctxs:
+        c.close()
