@@ -222,3 +222,27 @@ def test_multi_push_selection_and_masses(traj, align):
     np.testing.assert_allclose(ctxs[1].rmsf(), exp, rtol=0, atol=TOL)
     for c in ctxs:
         c.close()
+
+
+def test_long_device_push_launch_groups():
+    """A device push longer than one launch group (16,384 frames): each
+    group's fold is deferred to the next group's launch and the last one to
+    the merge (fused with the pack); the result equals the pipeline's one
+    batch and the CPU two-pass variance."""
+    from rmsf_amd import RMSF
+    from rmsf_amd.context import PUSH_WELFORD, Context
+    from rmsf_amd.engine import Engine
+    from rmsf_amd.synth import generate
+    n_atoms, nf = 96, 40_001
+    x = generate(Engine(), n_atoms, 0, nf, seed=33)
+    torch.cuda.synchronize()
+    ctxs = _ctxs(n_atoms, 2)
+    Context.multi_push_frames(ctxs, [x[:20_000].contiguous(), x[20_000:].contiguous()], PUSH_WELFORD,
+                              shift_frames=[x[0], x[0]])
+    Context.multi_chan_merge(ctxs, root=0)
+    got = ctxs[0].rmsf()
+    for c in ctxs:
+        c.close()
+    np.testing.assert_allclose(got, RMSF(x).run().results.rmsf, rtol=1e-12, atol=1e-13)
+    host = SY.frames(33, n_atoms, 0, nf)
+    np.testing.assert_allclose(got, O.rmsf_two_pass(host), rtol=0, atol=1e-9)
