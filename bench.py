@@ -571,6 +571,15 @@ def main():
     coll_dev = eng.device if a.backend == "nccl" else None
     rows = gather_rank_rows([launches, acc_ms, acc_af], coll_dev)
     out["roofline"] = rank_roofline(kname, rows, traffic, f"profiles/pmc_{a.workload}.json" if traffic else None)
+    if world > 1:
+        # the cross-rank merge as each rank's launching stream saw it: HIP events
+        # around the collective + unpack/finalise (waits for the slowest rank
+        # included; with atom slabs, only the exposed part after the last slab)
+        mrows = gather_rank_rows(list(timer.totals("merge")), coll_dev)
+        out["merge_timing"] = {"per_rank_ms_per_step": [r[1] / max(1.0, r[0]) for r in mrows],
+                               "max_ms_per_step": max(r[1] / max(1.0, r[0]) for r in mrows),
+                               "rule": "HIP events on the launching stream around the merge collective and the "
+                                       "unpack/finalise, per timed step"}
     out["cpu_baseline"] = cpu
     # the merged result (on rank 0 only with the default reduce-to-root merge)
     out["rmsf_checksum"] = float(res.rmsf.sum()) if res.rmsf is not None else None

@@ -471,35 +471,42 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                         (rmsf_fin, n_total) if rmsf_fin is not None else None)
     if slabbed is not None:                                  # RMSF.py:141-143 + 146, slab by slab
         if root is not None and rank != root:
-            for *_, work in slabbed:
-                if work is not None:
-                    work.wait()
+            with _span(timer, "merge"):                      # the exposed part: waits for the slabs' reduces
+                for *_, work in slabbed:
+                    if work is not None:
+                        work.wait()
             return PipelineResult(rmsf=None, mean=None, m2=None, n_frames=n_total, n_local=n_local, block=(b0, b1),
                                   average=None, rmsd=rmsd, extras={"merge_slabs": len(slabbed), "merge_root": root})
         mean, m2, rmsf = eng.empty(3 * n_sel), eng.empty(3 * n_sel), eng.empty(n_sel)
-        for t_k, j0, j1, work in slabbed:
-            if work is not None:
-                work.wait()
-            eng.chan_shift_finish(t_k, shift[j0:j1], off3, (j1 - j0) // 3, n_total, mean[j0:j1], m2[j0:j1],
-                                  rmsf[j0 // 3:j1 // 3])
+        with _span(timer, "merge"):
+            for t_k, j0, j1, work in slabbed:
+                if work is not None:
+                    work.wait()
+                eng.chan_shift_finish(t_k, shift[j0:j1], off3, (j1 - j0) // 3, n_total, mean[j0:j1], m2[j0:j1],
+                                      rmsf[j0 // 3:j1 // 3])
         if planes:
             mean, m2, rmsf = _rows_from_planes(eng, mean, m2, n_sel, n_total)
         return PipelineResult(rmsf=rmsf, mean=mean.view(n_sel, 3), m2=m2.view(n_sel, 3), n_frames=n_total,
                               n_local=n_local, block=(b0, b1), average=None, rmsd=rmsd,
                               extras={"merge_slabs": len(slabbed), "merge_root": root})
     if scatter:                                              # RMSF.py:141-143 + 146 by atom slices
-        rmsf, mean_s, m2_s, (a0, a1) = parallel.global_chan_scatter(
-            eng, acc.result0, acc.result1, acc.n, n_total, shift, off3, None if acc.packed else shift_work,
-            packed=t if acc.packed else None, slice_coords=sc, root=root)
+        with _span(timer, "merge"):
+            rmsf, mean_s, m2_s, (a0, a1) = parallel.global_chan_scatter(
+                eng, acc.result0, acc.result1, acc.n, n_total, shift, off3, None if acc.packed else shift_work,
+                packed=t if acc.packed else None, slice_coords=sc, root=root)
         return PipelineResult(rmsf=rmsf, mean=None, m2=None, n_frames=n_total, n_local=n_local, block=(b0, b1),
                               average=None if average is None else average.view(n_sel, 3), rmsd=rmsd,
                               transforms=xf_last, transforms_sweep1=xf_first,
                               extras={"merge_root": root, "merge": "scatter", "atom_slice": (a0, a1),
                                       "slice_mean": mean_s.view(-1, 3), "slice_m2": m2_s.view(-1, 3)})
     if size > 1:                                             # RMSF.py:141-143 + 146: one all-reduce
-        mean, m2, rmsf = parallel.global_chan_shifted(eng, acc.result0, acc.result1, acc.n, n_total,
-                                                      shift, off3, None if acc.packed else shift_work,
-                                                      packed=t if acc.packed else None, root=root)
+        # "merge" span: from the packed moments to the finished result on the
+        # launching stream -- the collective (incl. waiting for the slowest
+        # rank) and the unpack/finalise
+        with _span(timer, "merge"):
+            mean, m2, rmsf = parallel.global_chan_shifted(eng, acc.result0, acc.result1, acc.n, n_total,
+                                                          shift, off3, None if acc.packed else shift_work,
+                                                          packed=t if acc.packed else None, root=root)
         if planes and rmsf is not None:
             mean, m2, rmsf = _rows_from_planes(eng, mean, m2, n_sel, n_total)
         if rmsf is None:                                     # a non-root rank of the reduce

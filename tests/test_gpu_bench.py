@@ -191,3 +191,6 @@ def test_torchrun_merge_scatter_same_checksum():
         res[merge] = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["scatter"]["config"]["merge"].startswith("reduce-scatter")
     assert res["scatter"]["rmsf_checksum"] == res["root"]["rmsf_checksum"]
+    for r in res.values():  # the merge's time on every rank's stream, per step
+        mt = r["merge_timing"]
+        assert len(mt["per_rank_ms_per_step"]) == 2 and 0 < mt["max_ms_per_step"] < r["ms_per_step"]
