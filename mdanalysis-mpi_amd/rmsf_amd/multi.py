@@ -447,8 +447,29 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
                 for r in blocks[i]:
                     src.push(c, r, mode)
 
+        # HBM shards whose device blocks are single unit-step runs: one
+        # rmsf_multi_push_frames call (every context's launches from its own
+        # host thread; from 1M atoms the unaligned sweep runs in atom slabs
+        # beside the merge's collectives)
+        whole = (isinstance(src, _DeviceShards) and not staged
+                 and all(len(runs) <= 1 and all(r.step == 1 for r in runs) for runs in blocks))
+
+        def multi_push(mode):
+            parts = []
+            for i, runs in enumerate(blocks):
+                t = src.parts[i]
+                if runs:
+                    off = int(src.offsets[i])
+                    parts.append(t[runs[0].start - off:runs[0].stop - off])
+                else:
+                    parts.append(t[:0])
+            Context.multi_push_frames(ctxs, parts, mode, reset=False)
+
         if align == "average":
-            each(lambda i: push(i, PUSH_ALIGN_SUM))
+            if whole:
+                multi_push(PUSH_ALIGN_SUM)
+            else:
+                each(lambda i: push(i, PUSH_ALIGN_SUM))
             Context.multi_allreduce_sum(ctxs)
             for c in ctxs:
                 c.set_reference_average()
@@ -456,7 +477,10 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
         if collect_rmsd:
             for c in ctxs:  # the last sweep's rmsd only, as the pipeline reports it
                 c.collect_rmsd(True)
-        each(lambda i: push(i, PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD))
+        if whole:
+            multi_push(PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD)
+        else:
+            each(lambda i: push(i, PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD))
         Context.multi_chan_merge(ctxs, root=merge_root)
         home = ctxs[merge_root or 0]
         n, mean, m2 = home.partial()
