@@ -162,6 +162,24 @@ def main():
     row[f"context_step_{a.contexts}_tiny_ms"] = w
     row[f"context_step_{a.contexts}_tiny_host_enqueue_ms"] = idle_host(lambda: ctx_step(many, [tiny] * a.contexts),
                                                                        sync_ctxs(many), a.reps)
+    # the same host cost split into the push call and the merge call
+    sync_many = sync_ctxs(many)
+    push_ms, merge_ms = [], []
+    for _ in range(a.reps * 10):
+        sync_many()
+        h0 = time.perf_counter()
+        Context.multi_push_frames(many, [tiny] * a.contexts, PUSH_WELFORD, shift_frames=[frame0] * a.contexts,
+                                  after_torch=False)
+        h1 = time.perf_counter()
+        Context.multi_chan_merge(many, root=0)
+        h2 = time.perf_counter()
+        push_ms.append((h1 - h0) * 1e3)
+        merge_ms.append((h2 - h1) * 1e3)
+    sync_many()
+    push_ms.sort()
+    merge_ms.sort()
+    row[f"context_step_{a.contexts}_tiny_push_call_ms"] = push_ms[len(push_ms) // 2]
+    row[f"context_step_{a.contexts}_tiny_merge_call_ms"] = merge_ms[len(merge_ms) // 2]
     w1, _ = wall(lambda: ctx_step(one, [tiny]), sync_ctxs(one), a.reps)
     row["context_step_1_tiny_ms"] = w1
     row["context_step_1_tiny_host_enqueue_ms"] = idle_host(lambda: ctx_step(one, [tiny]), sync_ctxs(one), a.reps)
