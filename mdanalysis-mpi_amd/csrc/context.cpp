@@ -745,7 +745,9 @@ int exchange_chan_shifted(rmsf_ctx **cs, int n, const Reduce &red, bool host_cou
   if (total == 0) return fail(RMSF_EEMPTY, "rmsf chan merge: no frames on any rank (RMSF.py:39 ZeroDivisionError)");
   const int64_t nc = cs[0]->n_coord;
   std::vector<double *> t(n);
-  for (int i = 0; i < n; ++i) {
+  // each context's pack (and below its finish) from its own worker thread:
+  // with one device per context the launches leave in parallel
+  CX_OK(for_each_ctx(cs, n, [&](int i) -> int {
     rmsf_ctx *c = cs[i];
     DeviceScope ds(c->dev);
     const ShiftArgs sh = shift_of(c, kind);
@@ -760,14 +762,15 @@ int exchange_chan_shifted(rmsf_ctx **cs, int n, const Reduce &red, bool host_cou
                                  c->xa.d(), c->stream));
     }
     t[i] = c->xa.d();
-  }
+    return RMSF_OK;
+  }));
   CX_OK(red(2 * nc, t.data(), root));
-  for (int i = 0; i < n; ++i) {
+  return for_each_ctx(cs, n, [&](int i) -> int {
     rmsf_ctx *c = cs[i];
     if (root >= 0 && i != root) {
       c->merged_away = true;
       c->rmsf_valid = false;
-      continue;
+      return RMSF_OK;
     }
     DeviceScope ds(c->dev);
     const ShiftArgs sh = shift_of(c, kind);
@@ -777,8 +780,8 @@ int exchange_chan_shifted(rmsf_ctx **cs, int n, const Reduce &red, bool host_cou
     c->wel.n = total;
     c->rmsf_valid = true;
     c->merged_away = false;
-  }
-  return RMSF_OK;
+    return RMSF_OK;
+  });
 }
 
 Reduce callback_reduce(rmsf_ctx *c, rmsf_allreduce_fn fn, void *user) {
