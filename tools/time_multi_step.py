@@ -164,7 +164,11 @@ def main():
                                                                        sync_ctxs(many), a.reps)
     # the same host cost split into the push call and the merge call
     sync_many = sync_ctxs(many)
-    push_ms, merge_ms = [], []
+    # (the merge call first waits for the shift frames' digests: on ONE device
+    # the 2N streams share 4 hardware queues, so that wait is device time;
+    # "merge_call_ready" times the merge with the pushes already finished --
+    # its host cost alone)
+    push_ms, merge_ms, ready_ms = [], [], []
     for _ in range(a.reps * 10):
         sync_many()
         h0 = time.perf_counter()
@@ -175,11 +179,19 @@ def main():
         h2 = time.perf_counter()
         push_ms.append((h1 - h0) * 1e3)
         merge_ms.append((h2 - h1) * 1e3)
+        sync_many()
+        Context.multi_push_frames(many, [tiny] * a.contexts, PUSH_WELFORD, shift_frames=[frame0] * a.contexts,
+                                  after_torch=False)
+        sync_many()
+        h3 = time.perf_counter()
+        Context.multi_chan_merge(many, root=0)
+        ready_ms.append((time.perf_counter() - h3) * 1e3)
     sync_many()
-    push_ms.sort()
-    merge_ms.sort()
+    for v in (push_ms, merge_ms, ready_ms):
+        v.sort()
     row[f"context_step_{a.contexts}_tiny_push_call_ms"] = push_ms[len(push_ms) // 2]
     row[f"context_step_{a.contexts}_tiny_merge_call_ms"] = merge_ms[len(merge_ms) // 2]
+    row[f"context_step_{a.contexts}_tiny_merge_call_ready_ms"] = ready_ms[len(ready_ms) // 2]
     w1, _ = wall(lambda: ctx_step(one, [tiny]), sync_ctxs(one), a.reps)
     row["context_step_1_tiny_ms"] = w1
     row["context_step_1_tiny_host_enqueue_ms"] = idle_host(lambda: ctx_step(one, [tiny]), sync_ctxs(one), a.reps)
