@@ -17,9 +17,11 @@ subset of the selection language (BASELINE C1: adk PSF/DCD).
 Defaults mirror RMSF.py: selection "protein and name CA" (RMSF.py:77),
 ref_frame 0 (RMSF.py:63), the two-sweep average alignment (RMSF.py:89-140),
 frame blocks per rank (RMSF.py:65-69) with the per-rank range printed as at
-RMSF.py:74, and the RMSF computed on rank 0 (RMSF.py:145-146) -- which this
-script also writes out (``--out``), where RMSF.py only says "#Do something
-with RMSF" (RMSF.py:147).
+RMSF.py:74, the ranks' statistics merged by a reduce to rank 0
+(RMSF.py:143's ``comm.reduce(root=0)``; ``--merge all`` / ``scatter`` for the
+all-reduce / the reduce-scatter by atom slices) and the RMSF computed on
+rank 0 (RMSF.py:145-146) -- which this script also writes out (``--out``),
+where RMSF.py only says "#Do something with RMSF" (RMSF.py:147).
 """
 from __future__ import annotations
 
@@ -41,6 +43,8 @@ def main(argv=None) -> int:
     ap.add_argument("--align", choices=["average", "frame0", "none"], default="average")
     ap.add_argument("--ref-frame", type=int, default=0)
     ap.add_argument("--out", default=None, help="write rank 0's RMSF (.npy)")
+    ap.add_argument("--merge", choices=["root", "all", "scatter"], default="root",
+                    help="N>1: reduce to rank 0 (RMSF.py:143, default), all-reduce, or reduce-scatter by atom slices")
     a = ap.parse_args(argv)
 
     import torch
@@ -59,6 +63,7 @@ def main(argv=None) -> int:
 
     align = None if a.align == "none" else a.align
     rank, size = parallel.world()
+    root = None if a.merge == "all" else 0
     if a.synthetic:
         n_atoms, n_frames = a.synthetic
         eng = Engine()
@@ -67,8 +72,8 @@ def main(argv=None) -> int:
         motion = motion_table(a.seed + 1, n_frames) if align else None
         shard = generate(eng, n_atoms, b0, max(b1 - b0, 1), seed=a.seed, motion=motion)[: b1 - b0]
         res = run_pipeline(eng, DeviceSource(shard, offset=b0, n_traj=n_frames), FrameList(n_frames),
-                           align=align, ref_frame=a.ref_frame)
-        rmsf = res.rmsf.cpu().numpy()
+                           align=align, ref_frame=a.ref_frame, merge_root=root, merge_scatter=a.merge == "scatter")
+        rmsf = None if res.rmsf is None else res.rmsf.cpu().numpy()   # None on the non-root ranks
     else:
         if not (a.topology and a.trajectory):
             ap.error("--topology/--trajectory (MDAnalysis) or --synthetic is required")
@@ -79,7 +84,7 @@ def main(argv=None) -> int:
         if mda is not None:
             u = mda.Universe(a.topology, a.trajectory)
             ag = u.select_atoms(a.select)
-            rmsf = RMSF(ag, align=align, ref_frame=a.ref_frame, verbose=True).run().results.rmsf
+            rmsf = RMSF(ag, align=align, ref_frame=a.ref_frame, verbose=True, merge_root=root).run().results.rmsf
         else:
             # native fallback: GRO or PSF topology + selection subset; XTC, DCD (or
             # multi-frame GRO) trajectory.  PSF masses (GRO: masses guessed from
@@ -96,7 +101,7 @@ def main(argv=None) -> int:
             traj = (a.trajectory if a.trajectory.lower().endswith((".xtc", ".dcd"))
                     else GroTopology(a.trajectory).frames)
             rmsf = RMSF(traj, select=sel, align=align, masses=masses, ref_frame=a.ref_frame,
-                        verbose=True).run().results.rmsf
+                        verbose=True, merge_root=root).run().results.rmsf
     if rank == 0:
         print(f"RMSF over {len(rmsf)} atoms: mean {rmsf.mean():.6f} A, max {rmsf.max():.6f} A", flush=True)
         if a.out:
