@@ -155,3 +155,39 @@ def test_full_size_rmsf_py_two_sweeps():
     np.testing.assert_allclose(r.mean[atoms], mean, rtol=0, atol=TOL)
     np.testing.assert_allclose(r.rmsf[atoms], rmsf, rtol=0, atol=TOL)
     _release(traj)
+
+
+def test_full_size_c3_strided_selection():
+    """C3 at full size with a "CA-like" strided selection (every 10th atom,
+    10k of 100k; SURVEY 8, "an optional strided fit subset"): the gathered
+    superposition sums and the gathered aligned accumulate over 100k x 20k.
+    Device R/COM of sampled frames against the CPU QCP on the whole
+    selection (1e-9), then 48 selected atoms rebuilt through RMSF.py:133-138
+    with the device's per-frame records (1e-6 A)."""
+    import torch as _t
+    from rmsf_amd import RMSF
+    from rmsf_amd.engine import Engine
+    from rmsf_amd.synth import generate, motion_table
+    n_atoms, nf = N_FULL, NF_FULL
+    sel = np.arange(0, n_atoms, 10)
+    traj = generate(Engine(), n_atoms, 0, nf, seed=0, motion=motion_table(1, nf))
+    r = RMSF(traj, select=sel, align="frame0", collect_transforms=True).run().results
+    T = r.transforms
+    assert T.shape == (nf, 16) and r.rmsf.shape == (len(sel),)
+    sel_dev = _t.as_tensor(sel, device=traj.device)
+    ref_full = traj[0][sel_dev].cpu().numpy().astype(np.float64)
+    ref_com, ref_c = O.centred_reference(ref_full)
+    for f in SAMPLE_FRAMES[::2]:
+        mob = traj[f][sel_dev].cpu().numpy()
+        com = O.center_of_mass(mob).astype(np.float64)
+        R = O.get_rotation_matrix(ref_c, mob.astype(np.float64) - com, len(mob))
+        np.testing.assert_allclose(T[f, 9:12], com, rtol=0, atol=1e-9, err_msg=f"COM of frame {f}")
+        np.testing.assert_allclose(T[f, :9], R.reshape(-1), rtol=0, atol=1e-9, err_msg=f"R of frame {f}")
+    pick = np.sort(np.random.default_rng(11).choice(len(sel), 48, replace=False))
+    rows = traj[:, _t.as_tensor(sel[pick], device=traj.device)].cpu().numpy()
+    mean, rmsf = _welford_rmsf(_aligned_rows(rows, T, ref_com))
+    print(f"\n  C3 strided selection, 48 atoms: max|dmean| {np.abs(r.mean[pick] - mean).max():.2e}, "
+          f"max|dRMSF| {np.abs(r.rmsf[pick] - rmsf).max():.2e} A")
+    np.testing.assert_allclose(r.mean[pick], mean, rtol=0, atol=TOL)
+    np.testing.assert_allclose(r.rmsf[pick], rmsf, rtol=0, atol=TOL)
+    _release(traj)
