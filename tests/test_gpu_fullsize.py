@@ -191,3 +191,47 @@ def test_full_size_c3_strided_selection():
     np.testing.assert_allclose(r.mean[pick], mean, rtol=0, atol=TOL)
     np.testing.assert_allclose(r.rmsf[pick], rmsf, rtol=0, atol=TOL)
     _release(traj)
+
+
+def test_full_size_rmsf_py_selection_masses():
+    """RMSF.py's two sweeps at full size over a strided selection with
+    heterogeneous masses (RMSF.py:84,94,117,127's mass-weighted centres of
+    mass; the QCP stays unweighted, as RMSF.py:48 passes weights=None).
+    Sweep 1's records are pinned on sampled frames and its average rebuilt on
+    48 atoms (RMSF.py:94-111); sweep 2's records are pinned against the CPU
+    QCP to the device average (RMSF.py:113-118) and the 48 atoms' RMSF is
+    rebuilt through RMSF.py:133-138 + 146 (1e-6 A)."""
+    import torch as _t
+    from rmsf_amd import RMSF
+    from rmsf_amd.engine import Engine
+    from rmsf_amd.synth import generate, motion_table
+    n_atoms, nf = N_FULL, NF_FULL
+    sel = np.arange(3, n_atoms, 10)
+    m = np.random.default_rng(5).uniform(1.0, 16.0, len(sel))
+    traj = generate(Engine(), n_atoms, 0, nf, seed=0, motion=motion_table(1, nf))
+    r = RMSF(traj, select=sel, masses=m, align="average", collect_transforms=True).run().results
+    T1, T2 = r.transforms_sweep1, r.transforms
+    sel_dev = _t.as_tensor(sel, device=traj.device)
+
+    def check(T, ref_sel_f64, frames):
+        ref_com, ref_c = O.centred_reference(ref_sel_f64, m)
+        for f in frames:
+            mob = traj[f][sel_dev].cpu().numpy()
+            com = O.center_of_mass(mob, m).astype(np.float64)
+            R = O.get_rotation_matrix(ref_c, mob.astype(np.float64) - com, len(mob))
+            np.testing.assert_allclose(T[f, 9:12], com, rtol=0, atol=1e-9, err_msg=f"COM of frame {f}")
+            np.testing.assert_allclose(T[f, :9], R.reshape(-1), rtol=0, atol=1e-9, err_msg=f"R of frame {f}")
+        return ref_com
+
+    ref_com1 = check(T1, traj[0][sel_dev].cpu().numpy().astype(np.float64), SAMPLE_FRAMES[::2])
+    pick = np.sort(np.random.default_rng(12).choice(len(sel), 48, replace=False))
+    rows = traj[:, _t.as_tensor(sel[pick], device=traj.device)].cpu().numpy()
+    avg = _aligned_rows(rows, T1, ref_com1).astype(np.float64).sum(axis=0) / nf
+    np.testing.assert_allclose(r.average[pick], avg, rtol=0, atol=TOL)
+    ref_com2 = check(T2, np.asarray(r.average, dtype=np.float64), SAMPLE_FRAMES[1::2])
+    mean, rmsf = _welford_rmsf(_aligned_rows(rows, T2, ref_com2))
+    print(f"\n  RMSF.py sweeps, strided selection + masses, 48 atoms: max|daverage| "
+          f"{np.abs(r.average[pick] - avg).max():.2e}, max|dRMSF| {np.abs(r.rmsf[pick] - rmsf).max():.2e} A")
+    np.testing.assert_allclose(r.mean[pick], mean, rtol=0, atol=TOL)
+    np.testing.assert_allclose(r.rmsf[pick], rmsf, rtol=0, atol=TOL)
+    _release(traj)
