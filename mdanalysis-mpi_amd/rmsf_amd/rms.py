@@ -83,6 +83,13 @@ class RMSF:
         are None.  Default: every rank receives the merged result.  With
         ``gpus=``: the merge is a reduce to that device index and the
         results (which this one process returns either way) come from it.
+    merge_scatter : bool
+        Under ``torch.distributed``: merge by a reduce-scatter of atom slices
+        instead -- each rank finishes its slice and only the RMSF is gathered
+        to ``merge_root`` (default 0).  ``results.rmsf`` on that rank; every
+        rank's ``results.atom_slice``, ``slice_mean`` and
+        ``slice_sumsquares`` hold its slice (``mean``/``sumsquares`` are
+        None).
     gpus : int | list of int, optional
         Drive this many devices (or these device ids) from one process: each
         takes the RMSF.py:65-69 block of its index and the blocks merge over
@@ -96,7 +103,8 @@ class RMSF:
     def __init__(self, atomgroup, *, select=None, align=None, masses=None, ref_frame: int = 0,
                  device=None, batch_frames: int | None = None, n_splits: int | None = None,
                  collect_rmsd: bool = False, verbose: bool = False, gpus=None,
-                 collect_transforms: bool = False, layout: str = "fac", merge_root: int | None = None, **kwargs):
+                 collect_transforms: bool = False, layout: str = "fac", merge_root: int | None = None,
+                 merge_scatter: bool = False, **kwargs):
         if layout not in ("fac", "soa"):
             raise ValueError(f"layout must be 'fac' or 'soa', got {layout!r}")
         if layout == "soa" and not (isinstance(atomgroup, np.ndarray) or isinstance(atomgroup, torch.Tensor)):
@@ -104,6 +112,7 @@ class RMSF:
                              "AtomGroups have their own layout")
         self.layout = layout
         self.merge_root = merge_root
+        self.merge_scatter = bool(merge_scatter)
         self._input = atomgroup
         self.select = select
         self.align = align
@@ -124,6 +133,9 @@ class RMSF:
         if self.gpus is not None or isinstance(self._input, (list, tuple)):
             if self.collect_transforms:
                 raise NotImplementedError("collect_transforms is for one device per process")
+            if self.merge_scatter:
+                raise NotImplementedError("merge_scatter is for one process per GPU (torch.distributed); with "
+                                          "gpus= the one process receives the merged result")
             return self._run_multi(start, stop, step, frames)  # several devices, or HBM shards per device
         eng = Engine(self.device)
         # torch's current device = the engine's, so the buffers sources and
@@ -138,7 +150,8 @@ class RMSF:
                 print("Process:%3d --> Frames: %10d -- %10d" % (rank, b0, b1))  # RMSF.py:74
             res = run_pipeline(eng, src, fl, align=self.align, masses=masses, ref_frame=self.ref_frame,
                                max_batch=self.batch_frames, n_splits=self.n_splits, collect_rmsd=self.collect_rmsd,
-                               collect_transforms=self.collect_transforms, merge_root=self.merge_root)
+                               collect_transforms=self.collect_transforms, merge_root=self.merge_root,
+                               merge_scatter=self.merge_scatter)
             torch.cuda.current_stream(eng.device).synchronize()
             r = self.results
             host = lambda t: None if t is None else t.cpu().numpy()  # noqa: E731  (None: a non-root rank)
@@ -157,6 +170,10 @@ class RMSF:
                 r.transforms = res.transforms.cpu().numpy()
             if res.transforms_sweep1 is not None:
                 r.transforms_sweep1 = res.transforms_sweep1.cpu().numpy()
+            if "atom_slice" in res.extras:  # merge_scatter: this rank's slice of the statistics
+                r.atom_slice = res.extras["atom_slice"]
+                r.slice_mean = res.extras["slice_mean"].cpu().numpy()
+                r.slice_sumsquares = res.extras["slice_m2"].cpu().numpy()
         self.n_frames = res.n_frames
         return self
 

@@ -398,6 +398,15 @@ def _scatter_worker(rank, size, init, q, n_atoms, n_frames, align):
         sc = run_pipeline(eng, src, fl, align=align, ref_owner=0, merge_root=0, merge_scatter=True)
         torch.cuda.synchronize()
         a0, a1 = sc.extras["atom_slice"]
+        # the same through the MDAnalysis-style surface
+        from rmsf_amd import RMSF
+        R = RMSF(src, align=align, merge_root=0, merge_scatter=True).run().results
+        assert R.atom_slice == (a0, a1) and R.mean is None
+        np.testing.assert_array_equal(R.slice_mean, sc.extras["slice_mean"].cpu().numpy())
+        if rank == 0:
+            np.testing.assert_array_equal(R.rmsf, sc.rmsf.cpu().numpy())
+        else:
+            assert R.rmsf is None
         q.put((rank, [t.cpu().numpy() for t in (every.rmsf, every.mean, every.m2)],
                None if sc.rmsf is None else sc.rmsf.cpu().numpy(),
                (a0, a1, sc.extras["slice_mean"].cpu().numpy(), sc.extras["slice_m2"].cpu().numpy())))
