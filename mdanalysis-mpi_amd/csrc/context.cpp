@@ -13,6 +13,16 @@
 //        current chunk's split partials), n               (RMSF.py:120-138)
 //   sum: parts [1+S][3 n_sel] (slot 0 = running sum), n   (RMSF.py:89-105)
 //   xform[chunk][16] + superpose workspace, exchange buffers, rmsf[n_sel]
+//   shift[3 n_sel] f32: the unaligned merge's shift frame (selected rows)
+//
+// Laziness (round 4), invisible to every entry point: a push's fold is
+// deferred until the running state is next used (the shifted merge then
+// folds and packs in one launch); a reset only marks the state, which is
+// zeroed if it is read before a fold overwrites it; rmsf_multi_push_frames
+// may record a push for the atom-slab merge, which any other call runs whole.
+// Host side: one worker thread per context for the rmsf_multi_* calls, a side
+// stream for digests and the shift frame's gather, a communicator stream for
+// the slab merge's collectives.
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
 #include <rccl/rccl.h>
