@@ -8,6 +8,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r4_validate
 mkdir -p $O
 set -o pipefail
+timeout -k 10 300 python -u -m pytest tests/test_gpu_multi_step.py tests/test_gpu_context_fuzz.py -x -q --timeout 200 --timeout-method thread > $O/tests.txt 2>&1 || { tail -20 $O/tests.txt; exit 1; }
+tail -1 $O/tests.txt
 timeout -k 10 400 python -u tools/fuzz_parity.py 150 > $O/fuzz_parity_150.txt 2>&1 || { tail -5 $O/fuzz_parity_150.txt; exit 1; }
 tail -1 $O/fuzz_parity_150.txt
 timeout -k 10 500 python -u tools/fuzz_multirank.py 30 --root --planes --scatter > $O/fuzz_multirank_30.txt 2>&1 || { tail -5 $O/fuzz_multirank_30.txt; exit 1; }
