@@ -4,7 +4,8 @@ one process (tools/_ab/librmsf_old.so vs the current one): the fold
 (rmsf_fold_balanced / _shift, k_fold_sk), the accumulate and the
 superposition (k_frame_stats + k_qcp_frames) at the strong-scaling shares,
 each launch timed alone with HIP events, A/B/A; outputs compared byte for
-byte.  python tools/ab_fold.py"""
+byte, per buffer.  python tools/ab_fold.py [--old LIB] [--new LIB]"""
+import argparse
 import ctypes
 import os
 import sys
@@ -29,6 +30,58 @@ def lib(path):
     return L
 
 
+def refold(wk, j):
+    """k_fold_sk's walk and Chan fold for coordinate j, in Python floats."""
+    h = wk[:16].view(np.int64)
+    lanes, C, nf, T, G, P, cpl, mode, S, cw = (int(v) for v in h[:10])
+    p0 = wk[16:]
+    slot_d = cw * cpl
+    p1 = G * P * slot_d
+    c = (j // cpl) // cw
+    off = j - c * slot_d
+    clo, chi = c * nf, c * nf + nf
+
+    def sk_lo(b):
+        return T * b // G
+
+    def seg_len(lo, hi):
+        f0 = lo - (lo // nf) * nf
+        return min(hi - lo, nf - f0, 4096)
+
+    b = clo * G // T
+    while b > 0 and sk_lo(b) > clo:
+        b -= 1
+    while sk_lo(b + 1) <= clo:
+        b += 1
+    lo, hi, slot = sk_lo(b), sk_lo(b + 1), b * P
+    while lo < clo:
+        lo += seg_len(lo, hi)
+        slot += 1
+    n1, mu, M = 0.0, 0.0, 0.0
+    while True:
+        if lo >= hi:
+            b += 1
+            if b >= G:
+                break
+            lo, hi, slot = sk_lo(b), sk_lo(b + 1), b * P
+        if lo >= chi:
+            break
+        ln = float(seg_len(lo, hi))
+        pm, pq = float(p0[slot * slot_d + off]), float(p0[p1 + slot * slot_d + off])
+        if n1 <= 0:
+            mu, M = pm, pq
+        else:
+            t = n1 + ln
+            d = pm - mu
+            mun = (n1 * mu + ln * pm) / t
+            M = M + pq + (n1 * ln / t) * (d * d)
+            mu = mun
+        n1 = ln if n1 <= 0 else n1 + ln
+        lo += int(ln)
+        slot += 1
+    return mu, M
+
+
 def med_time(fn, reps):
     for _ in range(3):
         fn()
@@ -43,7 +96,12 @@ def med_time(fn, reps):
 
 
 def main():
-    libs = {"old": lib(os.path.join(ROOT, "tools", "_ab", "librmsf_old.so")), "new": lib(LIB_PATH)}
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--old", default=os.path.join(ROOT, "tools", "_ab", "librmsf_old.so"))
+    ap.add_argument("--new", default=LIB_PATH)
+    a = ap.parse_args()
+    print("old", a.old, "new", a.new, flush=True)
+    libs = {"old": lib(a.old), "new": lib(a.new)}
     eng = Engine()
     s = lambda: eng.stream  # noqa: E731
     for n, nf, aligned in ((100_000, 2_500, False), (100_000, 20_000, False), (1_000_000, 2_500, False),
@@ -51,12 +109,13 @@ def main():
         traj = generate(eng, n, 0, nf, seed=0, motion=motion_table(1, nf) if aligned else None)
         nc = 3 * n
         ref, info = eng.reference_setup(n, frame_ptr=traj.data_ptr())
-        xf = {k: eng.empty(nf, 16) for k in libs}
+        xf = {k: eng.zeros(nf, 16) for k in libs}
         sw = eng.empty(eng.workspace_bytes(n, nf) // 8 + 2)
         work = eng.empty(eng.balanced_workspace_bytes(n, nf) // 8 + 2)
         shift = traj[0].reshape(-1).clone()
-        out = {k: [eng.empty(nc), eng.empty(nc), eng.empty(2 * nc)] for k in libs}
+        out = {k: [eng.zeros(nc), eng.zeros(nc), eng.zeros(2 * nc)] for k in libs}
         t = {k: {"superpose": [], "accumulate": [], "fold": []} for k in libs}
+        parts = {}
         for order in ("old", "new", "old", "new"):
             L = libs[order]
 
@@ -88,8 +147,23 @@ def main():
             acc()
             fold()
             torch.cuda.synchronize()
-        same = all(np.array_equal(a.cpu().numpy().view(np.uint64), b.cpu().numpy().view(np.uint64))
-                   for a, b in zip(out["old"] + [xf["old"]], out["new"] + [xf["new"]]))
+            parts[order] = work.cpu().numpy()
+        eq = [np.array_equal(a.cpu().numpy().view(np.uint64), b.cpu().numpy().view(np.uint64))
+              for a, b in zip(out["old"] + [xf["old"]], out["new"] + [xf["new"]])]
+        same = all(eq)
+        if not same:
+            diffs = [float((a - b).abs().max()) for a, b in zip(out["old"] + [xf["old"]], out["new"] + [xf["new"]])]
+            same = f"False (mean, M2, T, xform equal: {eq}; max |diff| {diffs})"
+            if not eq[0]:
+                # which build is IEEE-exact: refold the differing coordinates
+                # from each build's own partials in Python f64 (same walk, same order)
+                po, pn = parts["old"], parts["new"]
+                print(f"    partials equal {np.array_equal(po.view(np.uint64), pn.view(np.uint64))}", flush=True)
+                mo, mn = out["old"][0].cpu().numpy(), out["new"][0].cpu().numpy()
+                for j in np.flatnonzero(mo != mn)[:3]:
+                    ro, rn = refold(po, int(j))[0], refold(pn, int(j))[0]
+                    print(f"    coord {j}: old {mo[j]!r} (python on its partials {ro!r}) new {mn[j]!r} "
+                          f"(python {rn!r})", flush=True)
         line = f"{n:8d} x {nf:6d} aligned {aligned!s:5s}:"
         for kname in ("superpose", "accumulate", "fold"):
             if not t["old"][kname]:
