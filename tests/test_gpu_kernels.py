@@ -443,6 +443,105 @@ def test_chan_shift_merge_kernels(eng, shift_kind):
     np.testing.assert_array_equal(mean.cpu().numpy(), f0.astype(np.float64))
 
 
+def _segment_walks(work):
+    """For every lane chunk of the balanced plan in ``work``: its segments'
+    (partial slot, frame count) in frame order -- the walk k_fold_sk replays
+    (sk_lo / sk_seg_len, segments cut at RMSF_MAX_SPLIT_FRAMES = 4096)."""
+    h = work[:16].view(np.int64)
+    lanes, C, nf, T, G, P, cpl, mode, S, cw = (int(v) for v in h[:10])
+
+    def seg_len(lo, hi):
+        return min(hi - lo, nf - lo % nf, 4096)
+
+    walks = []
+    for c in range(C):
+        clo, chi = c * nf, c * nf + nf
+        b = clo * G // T
+        while b > 0 and T * b // G > clo:
+            b -= 1
+        while T * (b + 1) // G <= clo:
+            b += 1
+        lo, hi, slot = T * b // G, T * (b + 1) // G, b * P
+        while lo < clo:
+            lo += seg_len(lo, hi)
+            slot += 1
+        segs = []
+        while True:
+            if lo >= hi:
+                b += 1
+                if b >= G:
+                    break
+                lo, hi, slot = T * b // G, T * (b + 1) // G, b * P
+            if lo >= chi:
+                break
+            n = seg_len(lo, hi)
+            segs.append((slot, n))
+            lo += n
+            slot += 1
+        walks.append(segs)
+    return dict(G=G, P=P, cpl=cpl, cw=cw, slot_d=cw * cpl), walks
+
+
+@pytest.mark.parametrize("n_sel,nf,groups,gather", [
+    (4096, 9000, 0, False), (4096, 1000, 3, False), (1001, 333, 7, True), (257, 4097, 2, False),
+    (300_000, 64, 0, False), (3, 5, 2, True)])
+def test_fold_is_reference_chan_merge(eng, n_sel, nf, groups, gather):
+    """k_fold_sk bit for bit against RMSF.py:36-41's own second_order_moments
+    (the oracle's verbatim restatement, numpy) applied to the accumulate's
+    segment partials in frame order, after a running state (acc_n > 0) too;
+    the SUM fold against numpy's sequential sum.  Holds because the library
+    is built without FP contraction (csrc/Makefile): the device evaluates the
+    merge's expressions exactly as numpy does.  Flat and atom plans, segments
+    cut at 4096 frames, forced workgroup counts, chunk-aligned ranges."""
+    from rmsf_amd.synth import generate
+    from rmsf_amd._lib import RMSF_MODE_SUM, RMSF_MODE_WELFORD
+    n_atoms = n_sel + 5 if gather else n_sel
+    traj = generate(eng, n_atoms, 0, nf, seed=41)
+    sel = np.sort(np.random.default_rng(8).choice(n_atoms, n_sel, replace=False)) if gather else None
+    sdev = torch.tensor(sel.astype(np.int32), device=eng.device) if gather else None
+    nc = 3 * n_sel
+    rng = np.random.default_rng(n_sel)
+    acc_n = 7
+    run_mean, run_m2 = rng.normal(40, 3, nc), rng.uniform(0, 5, nc)
+    for mode in (RMSF_MODE_WELFORD, RMSF_MODE_SUM):
+        work = eng.empty(eng.balanced_workspace_bytes(n_sel, nf, groups) // 8 + 2)
+        eng.accumulate_balanced(traj.data_ptr(), 3 * n_atoms, nf, n_sel, sdev, None, None, mode, work, groups)
+        outs = []
+        for a_n in (0, acc_n):
+            m0 = torch.tensor(run_mean, device=eng.device)
+            m1 = torch.tensor(run_m2, device=eng.device) if mode == RMSF_MODE_WELFORD else None
+            eng.fold_balanced(work, nc, mode, a_n, m0, m1)
+            outs.append((m0, m1))
+        _sync()
+        wk = work.cpu().numpy()
+        pl, walks = _segment_walks(wk)
+        p0 = wk[16:]
+        p1 = p0[pl["G"] * pl["P"] * pl["slot_d"]:]
+        for (m0, m1), a_n in zip(outs, (0, acc_n)):
+            got0 = m0.cpu().numpy()
+            got1 = m1.cpu().numpy() if m1 is not None else None
+            for c, segs in enumerate(walks):
+                j0 = c * pl["slot_d"]
+                j1 = min(j0 + pl["slot_d"], nc)
+                if j0 >= nc:
+                    break
+                rows = [(n, p0[s * pl["slot_d"]:s * pl["slot_d"] + j1 - j0], p1[s * pl["slot_d"]:s * pl["slot_d"] + j1 - j0])
+                        for s, n in segs]
+                if mode == RMSF_MODE_WELFORD:
+                    S = (a_n, run_mean[j0:j1], run_m2[j0:j1]) if a_n else (rows[0][0], rows[0][1], rows[0][2])
+                    for n, mu, m2 in rows[0 if a_n else 1:]:
+                        S = O.second_order_moments(S, (n, mu, m2))
+                    want0, want1 = S[1], S[2]
+                    np.testing.assert_array_equal(got1[j0:j1].view(np.uint64), np.asarray(want1).view(np.uint64),
+                                                  err_msg=f"M2 chunk {c} acc_n {a_n}")
+                else:
+                    want0 = run_mean[j0:j1].copy() if a_n else np.zeros(j1 - j0)
+                    for _, part, _ in rows:
+                        want0 = want0 + part
+                np.testing.assert_array_equal(got0[j0:j1].view(np.uint64), np.asarray(want0).view(np.uint64),
+                                              err_msg=f"mode {mode} chunk {c} acc_n {a_n}")
+
+
 @pytest.mark.parametrize("shift_kind", ["f64", "f64+off3", "f32"])
 @pytest.mark.parametrize("n_sel,nf,groups", [(4096, 1000, 0), (1001, 333, 7), (3, 5, 2), (100_000, 64, 0),
                                             (300_000, 33, 0)])

@@ -57,7 +57,7 @@ def refold(wk, j):
     while lo < clo:
         lo += seg_len(lo, hi)
         slot += 1
-    n1, mu, M = 0.0, 0.0, 0.0
+    segs = []
     while True:
         if lo >= hi:
             b += 1
@@ -67,19 +67,35 @@ def refold(wk, j):
         if lo >= chi:
             break
         ln = float(seg_len(lo, hi))
-        pm, pq = float(p0[slot * slot_d + off]), float(p0[p1 + slot * slot_d + off])
+        segs.append((slot, ln, float(p0[slot * slot_d + off]), float(p0[p1 + slot * slot_d + off])))
+        lo += int(ln)
+        slot += 1
+    mu, M = chan(segs)
+    return mu, M, segs
+
+
+def chan(segs, ops=None):
+    """Chan's merge of (slot, n, mean, M2) in list order; ops = (mul, add, sub, div) to evaluate elsewhere."""
+    mul, add, sub, div = ops or ((lambda a, b: a * b), (lambda a, b: a + b), (lambda a, b: a - b), (lambda a, b: a / b))
+    n1, mu, M = 0.0, 0.0, 0.0
+    for _, ln, pm, pq in segs:
         if n1 <= 0:
             mu, M = pm, pq
         else:
             t = n1 + ln
-            d = pm - mu
-            mun = (n1 * mu + ln * pm) / t
-            M = M + pq + (n1 * ln / t) * (d * d)
+            d = sub(pm, mu)
+            mun = div(add(mul(n1, mu), mul(ln, pm)), t)
+            M = add(add(M, pq), mul(div(n1 * ln, t), mul(d, d)))
             mu = mun
         n1 = ln if n1 <= 0 else n1 + ln
-        lo += int(ln)
-        slot += 1
-    return mu, M
+    return float(mu), float(M)
+
+
+def gpu_ops():
+    """The same f64 operations as single-element torch kernels on the GPU."""
+    T = lambda v: v if torch.is_tensor(v) else torch.tensor(v, dtype=torch.float64, device="cuda")  # noqa: E731
+    return ((lambda a, b: T(a) * T(b)), (lambda a, b: T(a) + T(b)), (lambda a, b: T(a) - T(b)),
+            (lambda a, b: T(a) / T(b)))
 
 
 def med_time(fn, reps):
@@ -99,9 +115,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--old", default=os.path.join(ROOT, "tools", "_ab", "librmsf_old.so"))
     ap.add_argument("--new", default=LIB_PATH)
+    ap.add_argument("--dump", help="write the differing coordinates' segments (n, mean, M2) as JSON")
     a = ap.parse_args()
     print("old", a.old, "new", a.new, flush=True)
     libs = {"old": lib(a.old), "new": lib(a.new)}
+    dump = []
     eng = Engine()
     s = lambda: eng.stream  # noqa: E731
     for n, nf, aligned in ((100_000, 2_500, False), (100_000, 20_000, False), (1_000_000, 2_500, False),
@@ -161,9 +179,21 @@ def main():
                 print(f"    partials equal {np.array_equal(po.view(np.uint64), pn.view(np.uint64))}", flush=True)
                 mo, mn = out["old"][0].cpu().numpy(), out["new"][0].cpu().numpy()
                 for j in np.flatnonzero(mo != mn)[:3]:
-                    ro, rn = refold(po, int(j))[0], refold(pn, int(j))[0]
+                    ro, _, segs = refold(po, int(j))
+                    rn = refold(pn, int(j))[0]
                     print(f"    coord {j}: old {mo[j]!r} (python on its partials {ro!r}) new {mn[j]!r} "
                           f"(python {rn!r})", flush=True)
+                    print(f"      segments (slot, n): {[(s_[0], s_[1]) for s_ in segs]}; "
+                          f"torch-on-GPU ops {chan(segs, gpu_ops())[0]!r}; "
+                          f"reversed order {chan(segs[::-1])[0]!r}", flush=True)
+                    dump.append({"case": [n, nf, aligned], "coord": int(j), "old": float(mo[j]), "new": float(mn[j]),
+                                 "old_m2": float(out["old"][1][j]), "new_m2": float(out["new"][1][j]),
+                                 "segs": [[int(a), b, c, d] for a, b, c, d in segs]})
+                    import itertools
+                    hits = [p for p in itertools.permutations(range(len(segs)))
+                            if len(segs) <= 7 and chan([segs[i] for i in p])[0] in (mo[j], mn[j])]
+                    print(f"      orders giving old/new: {[(p, chan([segs[i] for i in p])[0] == mo[j]) for p in hits[:6]]}",
+                          flush=True)
         line = f"{n:8d} x {nf:6d} aligned {aligned!s:5s}:"
         for kname in ("superpose", "accumulate", "fold"):
             if not t["old"][kname]:
@@ -173,6 +203,10 @@ def main():
         print(line + f"  bitwise equal {same}", flush=True)
         del traj, work, sw
         torch.cuda.empty_cache()
+    if a.dump and dump:
+        import json
+        with open(a.dump, "w") as f:
+            json.dump(dump, f)
 
 
 if __name__ == "__main__":

@@ -9,5 +9,5 @@ mkdir -p $O
 set -o pipefail
 
 
-timeout -k 10 300 python -u tools/ab_fold.py --new tools/_ab/librmsf_percoord.so > $O/ab_percoord.txt 2>&1 || { tail -20 $O/ab_percoord.txt; exit 1; }
+timeout -k 10 300 python -u tools/ab_fold.py --new tools/_ab/librmsf_percoord.so --dump $O/diff_segments.json > $O/ab_percoord.txt 2>&1 || { tail -20 $O/ab_percoord.txt; exit 1; }
 cat $O/ab_percoord.txt
