@@ -305,6 +305,27 @@ int rmsf_fold_balanced_shift_slab(const void *d_work, int64_t n_coord,
                                   double *d_t, int64_t c0, int64_t c1,
                                   void *stream);
 
+/* ---- RMSF.py:137-138 as written: the sequential Welford ---------------------
+ * For every selected coordinate (atom d_sel[a], or a, when d_sel is NULL;
+ * f32 rows d_xyz[f * frame_stride + 3 atom + c], no transform), the frames
+ * f = 0 .. n_frames-1 in order with k = k0 + f:
+ *   sumsquares += (k / (k + 1.0)) * (x - mean)**2 ;  mean = (k*mean + x)/(k+1)
+ * in numpy's operations and roundings, so d_mean / d_sumsquares (f64
+ * [3 n_sel], the running state after k0 frames; k0 = 0: start from zeros,
+ * inputs ignored) end as the reference recurrence's own values bit for bit
+ * -- a rank's S of RMSF.py:140, which rmsf_chan_merge then combines as
+ * RMSF.py:143 does, also bit for bit.  Parallel over coordinates only (one
+ * lane per coordinate through every frame); rmsf_accumulate_balanced is the
+ * reassociated, frame-parallel form (faster, equal to ~1e-13).
+ * d_work: rmsf_welford_sequential_workspace_bytes(n_frames) bytes (the
+ * per-frame coefficients).  Replaces RMSF.py:120-138's loop for one rank.   */
+size_t rmsf_welford_sequential_workspace_bytes(int64_t n_frames);
+int rmsf_welford_sequential(const float *d_xyz, int64_t frame_stride,
+                            int64_t n_frames, int64_t n_sel,
+                            const int32_t *d_sel, int64_t k0, double *d_mean,
+                            double *d_sumsquares, void *d_work,
+                            size_t work_bytes, void *stream);
+
 /* ---- finalise: RMSF.py:146  rmsf = sqrt(M2.sum(axis=1) / n) ---------------*/
 int rmsf_finalize(const double *d_m2, int64_t n_sel, int64_t n_frames,
                   double *d_rmsf, void *stream);

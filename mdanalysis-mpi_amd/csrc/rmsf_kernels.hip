@@ -413,6 +413,112 @@ __global__ __launch_bounds__(kBlock) void k_welford_flat_sk(const float *__restr
   }
 }
 
+// ---------------------------------------------------------------------------
+// RMSF.py:137-138 as written (round 4, the sequential Welford): for every
+// coordinate, the batch's frames in order, k = k0 + f,
+//   sumsquares += (k / (k + 1.0)) * (x - mean)**2
+//   mean = (k * mean + x) / (k + 1)
+// with numpy's operations and roundings (no contraction, csrc/Makefile), so
+// the running (mean, sumsquares) are the reference recurrence's own values
+// bit for bit.  Parallel over coordinates only: a lane carries CPT
+// consecutive coordinates through every frame, with the next U frames' loads
+// in flight while it folds the current U.  The per-frame constants come
+// from a table (k_seq_coef) read by scalar loads: c_k = k / (k + 1.0), and
+// r_k, 1 / (k + 1) refined as the hardware division refines it, so the
+// division costs a mul and two FMAs per coordinate -- q0 = num r_k,
+// q = fma(fma(-(k+1), q0, num), r_k, q0), the closing steps of the IEEE
+// division sequence (v_div_scale / v_div_fmas / v_div_fixup change nothing
+// for a finite numerator in normal range; any other numerator takes the
+// full division).
+struct SeqCoef {
+  double c, r;
+};
+
+__global__ __launch_bounds__(kBlock) void k_seq_coef(int64_t k0, int64_t nf, SeqCoef *__restrict__ out) {
+  const int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (f >= nf) return;
+  const double k = (double)(k0 + f), k1 = k + 1.0;
+  double r = __builtin_amdgcn_rcp(k1);
+  double e = __builtin_fma(-k1, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-k1, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  out[f] = SeqCoef{k / k1, r};
+}
+
+// num / k1 for k1 = k + 1 >= 1 and r = k_seq_coef's refined 1/k1.  The
+// fast form is the hardware division's own closing steps; it is exact
+// whenever v_div_scale would not rescale, i.e. for every finite nonzero
+// numerator that f32 coordinates can produce (|num| between ~2^-201 and
+// 2^181, far inside the 2^-968 .. 2^1023 band).  Zero and infinity divide
+// to themselves, and a NaN stays NaN, so one select covers the rest.
+__device__ __forceinline__ double seq_div(double num, double k1, double r) {
+  const double q0 = num * r;
+  const double q = __builtin_fma(__builtin_fma(-k1, q0, num), r, q0);
+  return (num == 0.0 || __builtin_isinf(num)) ? num : q;
+}
+
+template <int U, bool GATHER>
+__global__ __launch_bounds__(kBlock) void k_welford_seq(const float *__restrict__ xyz, int64_t fstride, int64_t nf,
+                                                        int64_t n_coord, const int32_t *__restrict__ sel,
+                                                        int64_t k0, const SeqCoef *__restrict__ coef,
+                                                        double *__restrict__ mean, double *__restrict__ ss) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n_coord) return;
+  // RMSF.py:119-120: np.zeros; later batches continue the running state
+  double m = k0 > 0 ? mean[j] : 0.0, q = k0 > 0 ? ss[j] : 0.0;
+  const float *__restrict__ p = xyz + (GATHER ? 3 * (int64_t)sel[j / 3] + j % 3 : j);
+  // k = k0 + f exactly (integers below 2^53)
+  auto step = [&](float v, const SeqCoef cf, double k) {
+    const double x = (double)v;
+    const double d = x - m;
+    q = q + cf.c * (d * d);
+    m = seq_div(k * m + x, k + 1.0, cf.r);
+  };
+  auto load = [&](float (&v)[U], SeqCoef (&c)[U], int64_t f) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      v[u] = __builtin_nontemporal_load(p + (f + u) * fstride);
+      c[u] = coef[f + u];
+    }
+  };
+  auto run = [&](const float (&v)[U], const SeqCoef (&c)[U], int64_t f) {
+    const double kb = (double)(k0 + f);
+#pragma unroll
+    for (int u = 0; u < U; ++u) step(v[u], c[u], kb + (double)u);
+  };
+  // two register blocks in turn, one always loading while the other folds
+  // (no copies between them: a copy makes the compiler wait on the
+  // coefficients' scalar loads where it is made)
+  int64_t f = 0;
+  if (nf >= U) {
+    float a[U], b[U];
+    SeqCoef ca[U], cb[U];
+    load(a, ca, 0);
+    for (;;) {
+      if (f + 2 * U > nf) {
+        run(a, ca, f);
+        f += U;
+        break;
+      }
+      load(b, cb, f + U);
+      run(a, ca, f);
+      f += U;
+      if (f + 2 * U > nf) {
+        run(b, cb, f);
+        f += U;
+        break;
+      }
+      load(a, ca, f + U);
+      run(b, cb, f);
+      f += U;
+    }
+  }
+  for (; f < nf; ++f) step(__builtin_nontemporal_load(p + f * fstride), coef[f], (double)(k0 + f));
+  mean[j] = m;
+  ss[j] = q;
+}
+
 template <int MODE, bool ALIGN, bool GATHER, int U, bool PLANES = false>
 __global__ __launch_bounds__(kBlock) void k_accum_atoms_sk(const float *__restrict__ xyz, int64_t fstride,
                                                            const int32_t *__restrict__ sel,
@@ -1872,6 +1978,9 @@ constexpr int kSkPerCuFlat = 2, kSkPerCuAtoms = 2, kSkPerCuAligned = 32;
 // Q = 4 at 4/CU -- against the one-sub-block kernel at 32/CU, 17-20 % less
 // time at 2,500 frames, 11-12 % at 5,000, 2-3 % at 20,000.
 constexpr int kQWel = 2, kSkPerCuSplitWel = 8, kQSum = 4, kSkPerCuSplitSum = 4;
+// Sequential Welford (k_welford_seq): frames per register block (two blocks
+// in turn: 8 frames folding while the next 8 load; 4, 6 and 12 are slower).
+constexpr int kSeqU = 8;
 
 
 // Balanced-grid plan for `lanes` lanes (cpl coordinates each) over nf frames.
@@ -2290,6 +2399,37 @@ RMSF_EXPORT int rmsf_chan_shift_finish_slice(const double *d_t, int64_t slice_co
                                              double *d_mean, double *d_m2, double *d_rmsf, void *stream) {
   return shift_finish(d_t, slice_coords, d_shift, shift_is_f32, d_off3, n_sel, n_frames, d_mean, d_m2, d_rmsf,
                       stream);
+}
+
+RMSF_EXPORT size_t rmsf_welford_sequential_workspace_bytes(int64_t n_frames) {
+  return n_frames < 1 ? 0 : (size_t)n_frames * sizeof(SeqCoef);
+}
+
+RMSF_EXPORT int rmsf_welford_sequential(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
+                                        const int32_t *d_sel, int64_t k0, double *d_mean, double *d_sumsquares,
+                                        void *d_work, size_t work_bytes, void *stream) {
+  if (!d_xyz || !d_mean || !d_sumsquares || !d_work || n_sel < 1 || (!d_sel && fstride < 3 * n_sel) ||
+      n_frames < 0 || k0 < 0 || k0 + n_frames > (int64_t(1) << 53))
+    return fail(RMSF_EINVAL, "rmsf_welford_sequential: bad arguments");
+  if (n_frames == 0) return RMSF_OK;
+  if (work_bytes < rmsf_welford_sequential_workspace_bytes(n_frames))
+    return fail(RMSF_EINVAL, "rmsf_welford_sequential: workspace too small");
+  hipStream_t s = S(stream);
+  SeqCoef *coef = static_cast<SeqCoef *>(d_work);
+  hipLaunchKernelGGL(k_seq_coef, dim3(grid1(n_frames)), dim3(kBlock), 0, s, k0, n_frames, coef);
+  if (int rc = after_launch("k_seq_coef")) return rc;
+  // one coordinate per lane: the recurrence is serial in frames, so the
+  // coordinates are the only parallelism, and more waves beat wider loads
+  // (100k x 20k: 4.25 ms at 1 coordinate per lane, 4.74 at 2, 5.45 at 4;
+  // DESIGN section 4)
+  const int64_t n_coord = 3 * n_sel;
+  if (d_sel)
+    hipLaunchKernelGGL((k_welford_seq<kSeqU, true>), dim3(grid1(n_coord)), dim3(kBlock), 0, s, d_xyz, fstride,
+                       n_frames, n_coord, d_sel, k0, coef, d_mean, d_sumsquares);
+  else
+    hipLaunchKernelGGL((k_welford_seq<kSeqU, false>), dim3(grid1(n_coord)), dim3(kBlock), 0, s, d_xyz, fstride,
+                       n_frames, n_coord, nullptr, k0, coef, d_mean, d_sumsquares);
+  return after_launch("k_welford_seq");
 }
 
 RMSF_EXPORT int rmsf_finalize(const double *d_m2, int64_t n_sel, int64_t n_frames, double *d_rmsf, void *stream) {

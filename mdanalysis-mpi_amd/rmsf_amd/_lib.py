@@ -73,6 +73,8 @@ SIGNATURES = {
     "rmsf_chan_weight": (c_int, [P, c_double, c_int64, P, P]),
     "rmsf_chan_deviation": (c_int, [P, P, P, c_double, c_int64, P, P]),
     "rmsf_finalize": (c_int, [P, c_int64, c_int64, P, P]),
+    "rmsf_welford_sequential_workspace_bytes": (c_size_t, [c_int64]),
+    "rmsf_welford_sequential": (c_int, [P, c_int64, c_int64, c_int64, P, c_int64, P, P, P, c_size_t, P]),
     "rmsf_chan_shift_pack": (c_int, [P, P, P, c_int, P, c_double, c_int64, P, P]),
     "rmsf_fold_balanced_shift": (c_int, [P, c_int64, c_int64, P, P, P, c_int, P, P, P]),
     "rmsf_fold_balanced_shift_sliced": (c_int, [P, c_int64, c_int64, P, P, P, c_int, P, c_int64, P, P]),

@@ -260,6 +260,21 @@ class Engine:
         call("rmsf_planes_to_rows", x.data_ptr(), n, out.data_ptr(), self.stream)
         return out
 
+    def welford_sequential(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, sel, k0: int,
+                           mean: torch.Tensor, sumsquares: torch.Tensor,
+                           work: torch.Tensor | None = None) -> torch.Tensor:
+        """RMSF.py:137-138 as written, frame by frame from k = k0 (k0 = 0:
+        the state starts at np.zeros): the reference recurrence's own
+        (mean, sumsquares), bit for bit.  Unaligned rows; ``sel`` an int32
+        device index tensor or None.  Returns the coefficient workspace
+        (pass it back to reuse it)."""
+        need = int(self.lib.rmsf_welford_sequential_workspace_bytes(n_frames))
+        if work is None or work.numel() * work.element_size() < need:
+            work = self.empty(max(need, 16) // 8)
+        call("rmsf_welford_sequential", xyz_ptr, fstride, n_frames, n_sel, _ptr(sel), k0, mean.data_ptr(),
+             sumsquares.data_ptr(), work.data_ptr(), work.numel() * work.element_size(), self.stream)
+        return work
+
     def finalize(self, m2: torch.Tensor, n_sel: int, n_frames: int, out: torch.Tensor) -> None:
         """RMSF.py:146: sqrt(M2.sum(axis=1)/n)."""
         call("rmsf_finalize", m2.data_ptr(), n_sel, n_frames, out.data_ptr(), self.stream)

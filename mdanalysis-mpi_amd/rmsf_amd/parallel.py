@@ -185,6 +185,43 @@ def gather_(t: torch.Tensor, root: int):
     return out.to(t.device) if staged else out
 
 
+def all_gather_(t: torch.Tensor) -> torch.Tensor:
+    """Every rank's ``t`` (equal sizes) concatenated in rank order, on every
+    rank."""
+    _, size = world()
+    if size == 1:
+        return t
+    staged = _staged(t)
+    src = t.cpu() if staged else t
+    parts = [torch.empty_like(src) for _ in range(size)]
+    dist.all_gather(parts, src)
+    out = torch.cat(parts)
+    return out.to(t.device) if staged else out
+
+
+def global_chan_exact(ops, mean_k: torch.Tensor, m2_k: torch.Tensor, counts: list[int], root: int | None = None):
+    """RMSF.py:141-143 with second_order_moments' own arithmetic: every
+    rank's (mean_k, M2_k) gathered, then folded in rank order by
+    k_chan_merge (RMSF.py:36-41 bit for bit; ``counts`` = the ranks' frame
+    counts, RMSF.py:65-69's blocks).  MPI may combine a commutative
+    user-defined reduce in any order; rank order is the canonical one (the
+    oracle's chan_fold).  ``root``: the result on that rank only (None
+    elsewhere), as comm.reduce(root=0); None: on every rank (all-gather).
+    Returns (mean, M2) or (None, None)."""
+    rank, size = world()
+    if size == 1:
+        return mean_k, m2_k
+    n = mean_k.numel()
+    both = torch.cat([mean_k.reshape(-1), m2_k.reshape(-1)])
+    g = all_gather_(both) if root is None else gather_(both, root)
+    if g is None:
+        return None, None
+    g = g.view(size, 2, n)
+    mean, m2 = torch.empty_like(mean_k), torch.empty_like(m2_k)
+    ops.chan_merge(g[:, 0].contiguous(), g[:, 1].contiguous(), [int(c) for c in counts], n, mean, m2)
+    return mean, m2
+
+
 def global_chan_scatter(ops, mean_k: torch.Tensor, m2_k: torch.Tensor, n_k: int, n_total: int, shift: torch.Tensor,
                         off3: torch.Tensor | None = None, shift_work=None, packed: torch.Tensor | None = None,
                         slice_coords: int | None = None, root: int = 0):

@@ -346,7 +346,7 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                  ref_owner: int | None = None, block: tuple[int, int] | None = None,
                  timer: KernelTimer | None = None, collect_transforms: bool = False,
                  merge_slabs: int | None = None, merge_root: int | None = None,
-                 merge_scatter: bool = False) -> PipelineResult:
+                 merge_scatter: bool = False, exact: bool = False) -> PipelineResult:
     """``merge_slabs`` (N > 1, no alignment, HBM-resident block in one batch,
     flat chunk-aligned plan): cut the final sweep into that many atom slabs
     so each slab's cross-rank all-reduce overlaps the next slab's stream;
@@ -358,9 +358,21 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     (parallel.global_chan_scatter): each rank finishes its slice and only
     the RMSF is gathered to ``merge_root`` (default 0); ``mean``/``m2`` are
     None and each rank's slice of them is in ``extras`` ("atom_slice",
-    "slice_mean", "slice_m2")."""
+    "slice_mean", "slice_m2").
+    ``exact`` (no alignment): RMSF.py:120-146 with the reference's own
+    arithmetic -- each rank's block through the sequential Welford
+    (rmsf_welford_sequential), the ranks folded in rank order by
+    second_order_moments (parallel.global_chan_exact), RMSF.py:146: results
+    bit-identical to RMSF.py's recurrence, ~1.2x the balanced path's time."""
     if align not in ALIGN_MODES:
         raise ValueError(f"align must be one of {ALIGN_MODES}, got {align!r}")
+    if exact:
+        if align is not None:
+            raise NotImplementedError("exact=True covers align=None (RMSF.py:120-146 on an aligned trajectory)")
+        if n_splits or merge_scatter or merge_slabs not in (None, 0, 1) or collect_rmsd or collect_transforms:
+            raise ValueError("exact=True runs the sequential Welford: no n_splits, merge_scatter, merge_slabs, "
+                             "collect_rmsd or collect_transforms")
+        return _run_exact(eng, source, frames, max_batch, block, timer, merge_root)
     rank, size = parallel.world()
     n_total = len(frames)
     if n_total == 0:
@@ -527,6 +539,41 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                           n_local=n_local, block=(b0, b1),
                           average=None if average is None else average.view(n_sel, 3), rmsd=rmsd,
                           transforms=xf_last, transforms_sweep1=xf_first)
+
+
+def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, merge_root) -> PipelineResult:
+    """run_pipeline(exact=True): RMSF.py:120-146 bit for bit (see there)."""
+    rank, size = parallel.world()
+    n_total = len(frames)
+    if n_total == 0:
+        raise RmsfEmptyError(-4, "RMSF.run", "no frames selected")
+    if merge_root is not None and not 0 <= merge_root < size:
+        raise ValueError(f"merge_root {merge_root} is not a rank of this {size}-rank group")
+    root = merge_root if size > 1 else None
+    blocks = parallel.blocks(n_total, size)
+    if block is not None and size > 1 and tuple(block) != blocks[rank]:
+        raise ValueError(f"rank {rank}: block {tuple(block)} is not the RMSF.py:65-69 block {blocks[rank]}")
+    b0, b1 = block if block is not None else blocks[rank]
+    n_local = b1 - b0
+    n_sel = source.n_sel
+    max_batch = max(1, min(max_batch or max(1, n_local), max(1, n_local)))
+    mean, ss = eng.zeros(3 * n_sel), eng.zeros(3 * n_sel)   # RMSF.py:119-120
+    work, k = None, 0
+    for b in source.batches(frames, b0, b1, max_batch, eng.stream):  # rows: (frame, atom, xyz)
+        with _span(timer, "accumulate", b.n_frames * n_sel):
+            work = eng.welford_sequential(b.ptr, b.fstride, b.n_frames, n_sel, b.sel, k, mean, ss, work)
+        k += b.n_frames
+        b.done()
+    if size > 1:                                             # RMSF.py:141-143, rank order
+        with _span(timer, "merge"):
+            mean, ss = parallel.global_chan_exact(eng, mean, ss, [e - s for s, e in blocks], root)
+    rmsf = None
+    if mean is not None:
+        rmsf = eng.empty(n_sel)
+        eng.finalize(ss, n_sel, n_total, rmsf)               # RMSF.py:146
+    return PipelineResult(rmsf=rmsf, mean=None if mean is None else mean.view(n_sel, 3),
+                          m2=None if ss is None else ss.view(n_sel, 3), n_frames=n_total, n_local=n_local,
+                          block=(b0, b1), extras={"exact": True, "merge_root": root})
 
 
 class CapturedPipeline:

@@ -90,6 +90,15 @@ class RMSF:
         rank's ``results.atom_slice``, ``slice_mean`` and
         ``slice_sumsquares`` hold its slice (``mean``/``sumsquares`` are
         None).
+    exact : bool
+        ``align=None`` only: compute RMSF.py:120-146 with the reference's own
+        arithmetic -- each rank's frames through the per-frame Welford of
+        RMSF.py:137-138 in order (rmsf_welford_sequential), the ranks folded
+        in rank order by second_order_moments, RMSF.py:146 -- so
+        ``results`` are bit-identical to the script's recurrence on the same
+        float32 coordinates (``mean``, ``sumsquares`` and ``rmsf``).  About
+        1.2x the time of the default frame-parallel path, which agrees with
+        it to ~1e-13.
     gpus : int | list of int, optional
         Drive this many devices (or these device ids) from one process: each
         takes the RMSF.py:65-69 block of its index and the blocks merge over
@@ -104,7 +113,7 @@ class RMSF:
                  device=None, batch_frames: int | None = None, n_splits: int | None = None,
                  collect_rmsd: bool = False, verbose: bool = False, gpus=None,
                  collect_transforms: bool = False, layout: str = "fac", merge_root: int | None = None,
-                 merge_scatter: bool = False, **kwargs):
+                 merge_scatter: bool = False, exact: bool = False, **kwargs):
         if layout not in ("fac", "soa"):
             raise ValueError(f"layout must be 'fac' or 'soa', got {layout!r}")
         if layout == "soa" and not (isinstance(atomgroup, np.ndarray) or isinstance(atomgroup, torch.Tensor)):
@@ -113,6 +122,7 @@ class RMSF:
         self.layout = layout
         self.merge_root = merge_root
         self.merge_scatter = bool(merge_scatter)
+        self.exact = bool(exact)
         self._input = atomgroup
         self.select = select
         self.align = align
@@ -136,6 +146,8 @@ class RMSF:
             if self.merge_scatter:
                 raise NotImplementedError("merge_scatter is for one process per GPU (torch.distributed); with "
                                           "gpus= the one process receives the merged result")
+            if self.exact:
+                raise NotImplementedError("exact=True is for one device per process")
             return self._run_multi(start, stop, step, frames)  # several devices, or HBM shards per device
         eng = Engine(self.device)
         # torch's current device = the engine's, so the buffers sources and
@@ -151,7 +163,7 @@ class RMSF:
             res = run_pipeline(eng, src, fl, align=self.align, masses=masses, ref_frame=self.ref_frame,
                                max_batch=self.batch_frames, n_splits=self.n_splits, collect_rmsd=self.collect_rmsd,
                                collect_transforms=self.collect_transforms, merge_root=self.merge_root,
-                               merge_scatter=self.merge_scatter)
+                               merge_scatter=self.merge_scatter, exact=self.exact)
             torch.cuda.current_stream(eng.device).synchronize()
             r = self.results
             host = lambda t: None if t is None else t.cpu().numpy()  # noqa: E731  (None: a non-root rank)

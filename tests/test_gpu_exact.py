@@ -1,0 +1,126 @@
+"""GPU tier: ``exact=True`` -- RMSF.py:120-146 with the reference's own
+arithmetic, bit for bit.
+
+rmsf_welford_sequential runs RMSF.py:137-138's per-frame update in frame
+order with numpy's operations and roundings (the library is built without FP
+contraction), rmsf_chan_merge folds the ranks with second_order_moments
+(RMSF.py:36-41) in rank order, and k_finalize is RMSF.py:146.  The oracle's
+rank_sweep2 / rmsf_script(align=None) are those lines restated in numpy, so
+every comparison here is ``assert_array_equal`` on the float64 bit patterns
+-- mean, sumsquares and RMSF -- not a tolerance.  Sizes: one and two
+batches (the recurrence's k continued across them), a gathered selection,
+frame subsets, host and HBM inputs, 2-3 ranks sharing the GPU over gloo."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import rmsf_oracle as O
+from oracle import synth as SY
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64)).view(np.uint64)
+
+
+def _same(got, want, what):
+    np.testing.assert_array_equal(_bits(got), _bits(want), err_msg=what)
+
+
+@pytest.mark.parametrize("n_atoms,nf,gather", [(4096, 700, False), (1001, 333, True), (5, 40, False),
+                                               (3, 1, False), (257, 4097, True)])
+def test_sequential_kernel_is_rmsf_py_recurrence(n_atoms, nf, gather):
+    from rmsf_amd.engine import Engine
+    from rmsf_amd.synth import generate
+    eng = Engine()
+    traj = generate(eng, n_atoms, 0, nf, seed=5)
+    host = traj.cpu().numpy()
+    sel = np.sort(np.random.default_rng(2).choice(n_atoms, max(1, n_atoms // 3), replace=False)) if gather \
+        else np.arange(n_atoms)
+    sdev = eng.sel_tensor(sel) if gather else None
+    n_sel = len(sel)
+    S = O.rank_sweep2(host, sel, None, 0, nf)
+    m, q = eng.empty(3 * n_sel), eng.empty(3 * n_sel)
+    eng.welford_sequential(traj.data_ptr(), 3 * n_atoms, nf, n_sel, sdev, 0, m, q)
+    # the same frames in three batches: k continues at k0
+    m3, q3 = eng.empty(3 * n_sel), eng.empty(3 * n_sel)
+    cuts = [0, nf // 3, (2 * nf) // 3, nf]
+    for f0, f1 in zip(cuts, cuts[1:]):
+        eng.welford_sequential(traj.data_ptr() + f0 * 3 * n_atoms * 4, 3 * n_atoms, f1 - f0, n_sel, sdev, f0,
+                               m3, q3)
+    torch.cuda.synchronize()
+    for got_m, got_q, how in ((m, q, "one batch"), (m3, q3, "three batches")):
+        _same(got_m.cpu().numpy(), S[1].reshape(-1), f"mean, {how}")
+        _same(got_q.cpu().numpy(), S[2].reshape(-1), f"sumsquares, {how}")
+
+
+@pytest.mark.parametrize("kind", ["host", "hbm"])
+@pytest.mark.parametrize("run_kw,batch", [({}, None), ({}, 37), ({"start": 3, "stop": 290, "step": 4}, None),
+                                          ({"frames": [0, 5, 6, 9, 100, 250]}, 2)])
+def test_rmsf_exact_single_rank(kind, run_kw, batch):
+    from rmsf_amd import RMSF
+    n_atoms, nf = 600, 300
+    traj = SY.frames(11, n_atoms, 0, nf)
+    sel = np.arange(2, n_atoms, 5)
+    inp = traj if kind == "host" else torch.tensor(traj, device="cuda")
+    r = RMSF(inp, select=sel, exact=True, batch_frames=batch).run(**run_kw).results
+    fl = O._frame_list(nf, run_kw.get("start"), run_kw.get("stop"), run_kw.get("step"))
+    if "frames" in run_kw:
+        fl = run_kw["frames"]
+    want = O.rmsf_script(traj[fl], sel=sel, size=1, align=None)
+    _same(r.mean, want["mean"], "mean")
+    _same(r.sumsquares, want["m2"], "sumsquares")
+    _same(r.rmsf, want["rmsf"], "rmsf")
+    # the default (frame-parallel, reassociated) path agrees to rounding
+    d = RMSF(inp, select=sel, batch_frames=batch).run(**run_kw).results
+    np.testing.assert_allclose(d.rmsf, r.rmsf, rtol=0, atol=1e-12)
+
+
+def test_rmsf_exact_rejects_alignment_and_splits():
+    from rmsf_amd import RMSF
+    traj = SY.frames(1, 10, 0, 5)
+    with pytest.raises(NotImplementedError):
+        RMSF(traj, align="frame0", exact=True).run()
+    with pytest.raises(ValueError):
+        RMSF(traj, exact=True, n_splits=2).run()
+
+
+def _exact_worker(rank, size, init, n_frames, root, q):
+    import sys
+
+    from conftest import PKG, ROOT
+    sys.path[:0] = [ROOT, PKG]
+    import torch.distributed as dist
+
+    from conftest import init_gloo
+    init_gloo(init, rank, size)
+    try:
+        from rmsf_amd import RMSF
+        traj = SY.frames(4, 500, 0, n_frames)
+        r = RMSF(traj, select=np.arange(0, 500, 2), exact=True, merge_root=root).run().results
+        q.put((rank, r.rmsf, r.mean, r.sumsquares, r.block))
+    except Exception as e:  # surface the failure to the parent
+        q.put((rank, repr(e), None, None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("size,n_frames,root", [(2, 61, 0), (3, 100, None), (3, 2, 1)])
+def test_rmsf_exact_ranks(size, n_frames, root):
+    """RMSF.py under mpirun -n size: each rank's block (RMSF.py:65-69)
+    through the recurrence, the ranks folded in rank order (RMSF.py:143's
+    reduce with second_order_moments), bit for bit with the oracle's
+    rmsf_script(size=...); 2 frames on 3 ranks leaves rank 0 empty."""
+    from conftest import spawn_ranks
+    out = spawn_ranks(_exact_worker, size, lambda r, init, q: (r, size, init, n_frames, root, q), timeout=100)
+    traj = SY.frames(4, 500, 0, n_frames)
+    want = O.rmsf_script(traj, sel=np.arange(0, 500, 2), size=size, align=None)
+    for rank, rmsf, mean, m2, block in sorted(out, key=lambda o: o[0]):
+        assert not isinstance(rmsf, str), rmsf
+        if root is not None and rank != root:
+            assert rmsf is None and mean is None
+            continue
+        _same(rmsf, want["rmsf"], f"rank {rank} rmsf")
+        _same(mean, want["mean"], f"rank {rank} mean")
+        _same(m2, want["m2"], f"rank {rank} sumsquares")

@@ -47,6 +47,14 @@ def test_full_size_unaligned(n_atoms, nf):
     # the frame-tile split is an internal choice: 3 tiles vs the default
     s = RMSF(traj, n_splits=3).run().results
     np.testing.assert_allclose(s.rmsf, r.rmsf, rtol=0, atol=1e-12)
+    # exact=True: RMSF.py:137-138's recurrence over all nf frames, bit for
+    # bit on the sampled atoms (the oracle's rank_sweep2 on their columns)
+    e = RMSF(traj, exact=True).run().results
+    S = O.rank_sweep2(host, np.arange(48), None, 0, nf)
+    for got, want in ((e.mean[atoms], S[1]), (e.sumsquares[atoms], S[2]),
+                      (e.rmsf[atoms], np.sqrt(S[2].sum(axis=1) / nf))):
+        np.testing.assert_array_equal(got.view(np.uint64), np.ascontiguousarray(want).view(np.uint64))
+    np.testing.assert_allclose(e.rmsf, r.rmsf, rtol=0, atol=1e-11)
     _release(traj)
 
 
