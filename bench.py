@@ -622,13 +622,35 @@ def main():
 
     # -- aligned modes at N=1 (reported beside the headline) ------------------
     if world == 1 and not a.no_modes and wl["align"] is None and not wl.get("host"):
+        # exact=True on the headline's frames: RMSF.py:137-138 as written
+        # (k_welford_seq), bit-identical to the reference recurrence
+        def run_exact(timer=None):
+            return run_pipeline(eng, src, fl, block=(b0, b1), max_batch=a.batch_frames, timer=timer, exact=True)
+
+        run_exact()
+        torch.cuda.synchronize()
+        xt = KernelTimer()
+        t0 = time.perf_counter()
+        for _ in range(a.mode_steps):
+            res_x = run_exact(xt)
+        torch.cuda.synchronize()
+        xdt = time.perf_counter() - t0
+        k_x, x_ms, x_af = xt.totals("accumulate")
+        exact_mode = {
+            "atom_frames_per_s": n_total * n_atoms * a.mode_steps / xdt,
+            "ms_per_step": xdt / a.mode_steps * 1e3,
+            "kernel": "k_welford_seq",
+            "avg_launch_ms": x_ms / max(1, k_x),
+            "hbm_frac": B_PER_ATOM_FRAME * x_af / (x_ms / 1e3) / 1e9 / HBM_PEAK_GBS if x_ms > 0 else None,
+            "max_abs_rmsf_diff_vs_headline": float((res_x.rmsf - res.rmsf).abs().max()),
+            "note": "RMSF.py:120-146 with the reference's own arithmetic, bit for bit (tests/test_gpu_exact.py)"}
         del traj, src
         torch.cuda.empty_cache()
         motion = motion_table(1, n_total)
         traj = generate(eng, n_atoms, b0, n_local, seed=0, motion=motion)
         torch.cuda.synchronize()
         src = DeviceSource(traj, offset=b0, n_traj=n_total)
-        modes = {}
+        modes = {"c2_exact": exact_mode}
         for name, align in (("c3_frame0", "frame0"), ("rmsf_py_average", "average")):
             mdt, mt, _ = timed(align, a.mode_steps, 1)
             sweeps = 2 if align == "average" else 1

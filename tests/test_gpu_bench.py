@@ -54,6 +54,9 @@ def test_bench_cli_small_json_line():
     m = line["modes"]
     for name in ("c3_frame0", "rmsf_py_average"):
         assert 0 < m[name]["accumulate_hbm_gbs"] < 8000 and 0 < m[name]["superpose_hbm_gbs"] < 8000
+    x = m["c2_exact"]
+    assert x["kernel"] == "k_welford_seq" and 0 < x["hbm_frac"] < 1.0
+    assert x["max_abs_rmsf_diff_vs_headline"] < 1e-12
 
 
 def test_bench_batched_launches_roofline_below_peak():
