@@ -64,6 +64,15 @@ class OracleOps:
         rmsf[:n_sel].copy_(torch.from_numpy(np.sqrt(q.reshape(-1, 3).sum(axis=1) / n)))
 
     @staticmethod
+    def chan_merge(means, m2s, counts, n, mean_out, m2_out):
+        """k_chan_merge: second_order_moments (RMSF.py:36-41) folded over the
+        parts in order, empty parts skipped (the oracle's chan_fold)."""
+        from oracle import rmsf_oracle as O
+        S = O.chan_fold([(c, means[i].numpy(), m2s[i].numpy()) for i, c in enumerate(counts)])
+        mean_out.copy_(torch.from_numpy(np.asarray(S[1])))
+        m2_out.copy_(torch.from_numpy(np.asarray(S[2])))
+
+    @staticmethod
     def chan_shift_finish(t, shift, off3, n_sel, n, mean, m2, rmsf):
         c = OracleOps._c(shift, off3, 3 * n_sel)
         t1, t2 = t.numpy()[:3 * n_sel], t.numpy()[3 * n_sel:6 * n_sel]
@@ -100,6 +109,12 @@ def _worker(rank, size, port, n_frames, q, merge="two"):
         if merge == "two":
             mean, m2 = parallel.global_chan(OracleOps, mean_k, m2_k, n_k, n_frames)
             rmsf = np.sqrt(m2.numpy().reshape(-1, 3).sum(axis=1) / n_frames)
+        elif merge in ("exact", "exact_root"):
+            # exact=True's merge: every rank's S gathered, folded in rank order
+            counts = [b - a for a, b in parallel.blocks(n_frames, size)]
+            mean, m2 = parallel.global_chan_exact(OracleOps, mean_k, m2_k, counts,
+                                                  root=1 % size if merge == "exact_root" else None)
+            rmsf = None if m2 is None else np.sqrt(m2.numpy().reshape(-1, 3).sum(axis=1) / n_frames)
         else:
             # the pipeline's one-all-reduce merge, shifted by the sweep-2
             # reference (f64 centred + COM: align="frame0"'s form), by the
@@ -131,7 +146,7 @@ def _worker(rank, size, port, n_frames, q, merge="two"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("merge", ["two", "ref", "average", "frame0", "root", "scatter"])
+@pytest.mark.parametrize("merge", ["two", "ref", "average", "frame0", "root", "scatter", "exact", "exact_root"])
 @pytest.mark.parametrize("size,n_frames", [(2, 40), (3, 40), (2, 1), (3, 2)])
 def test_gloo_two_sweep_merge(size, n_frames, merge):
     """world_size 2/3, including ranks with empty blocks (n_frames < size);
@@ -149,9 +164,13 @@ def test_gloo_two_sweep_merge(size, n_frames, merge):
     out = spawn_ranks(_worker, size, lambda r, init, q: (r, size, init, n_frames, q, merge))
     traj = SY.frames(8, 60, 0, n_frames, motion_table(9, n_frames))
     ref = O.rmsf_script(traj, np.arange(0, 60, 3), None, size=1, align="average")
+    # the exact merge: RMSF.py under mpirun -n size reduced in rank order, bit for bit
+    ref_p = O.rmsf_script(traj, np.arange(0, 60, 3), None, size=size, align="average")
     for rank, rmsf, avg in out:
-        if merge in ("root", "scatter") and rank != 0:
+        if (merge in ("root", "scatter") and rank != 0) or (merge == "exact_root" and rank != 1 % size):
             assert rmsf is None
+        elif merge.startswith("exact"):
+            np.testing.assert_array_equal(rmsf.view(np.uint64), ref_p["rmsf"].view(np.uint64))
         else:
             np.testing.assert_allclose(rmsf, ref["rmsf"], atol=1e-9)
         np.testing.assert_allclose(avg, ref["average"], atol=1e-9)
