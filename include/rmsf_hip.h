@@ -532,6 +532,13 @@ typedef struct rmsf_ctx rmsf_ctx;
 #define RMSF_PUSH_ALIGN_SUM 1     /* superpose, f64 sum      (RMSF.py:91-105) */
 #define RMSF_PUSH_ALIGN_WELFORD 2 /* superpose, Welford      (RMSF.py:123-138)*/
 #define RMSF_PUSH_SUM 3           /* f64 sum of the raw frames                */
+/* RMSF.py:137-138 as written on the raw frames (rmsf_welford_sequential):
+ * the running Welford state continued frame by frame with the reference's
+ * own arithmetic, so rmsf_get_partial returns a rank's S of RMSF.py:140 bit
+ * for bit -- reduce those with RMSF.py:143's own second_order_moments (or
+ * rmsf_chan_merge in rank order) for the script's result.  The multi-context
+ * merges combine such states too (to rounding, not bit for bit).          */
+#define RMSF_PUSH_EXACT 4
 
 /* h_sel: n_sel int64 atom indices (MDAnalysis AtomGroup.indices; copied),
  * NULL = atoms 0..n_sel-1.  h_masses: n_sel f64 (copied) or NULL = uniform

@@ -261,6 +261,7 @@ struct rmsf_ctx {
   std::vector<double> h_masses;
   hipStream_t stream = nullptr;
   DevBuf sel, masses, ref, refinfo, xform, work, accwork, frame, avg, rmsf, xa, xb, cnt, refdig;
+  DevBuf seqwork;  // the sequential Welford's per-frame coefficients (RMSF_PUSH_EXACT)
   bool ref_set = false;
   Running wel, sum;
   rmsf_stager *stager = nullptr;
@@ -420,6 +421,27 @@ int process(rmsf_ctx *c, const float *d_xyz, int64_t stride, int64_t n_frames, c
   const bool aligned = mode == RMSF_PUSH_ALIGN_SUM || mode == RMSF_PUSH_ALIGN_WELFORD;
   const bool welford = mode == RMSF_PUSH_WELFORD || mode == RMSF_PUSH_ALIGN_WELFORD;
   CX_OK(flush_fold(c));  // the workspace is about to be rewritten
+  if (mode == RMSF_PUSH_EXACT) {
+    // RMSF.py:137-138 as written, continuing the running state at k = n (a
+    // reset state has n = 0: the kernel starts from zeros); the recurrence
+    // updates (mean, sumsquares) in place, nothing to fold
+    Running &r = c->wel;
+    const size_t row = sizeof(double) * c->n_coord;
+    CX_OK(r.parts0.ensure(row, c->stream, true));
+    CX_OK(r.parts1.ensure(row, c->stream, true));
+    const size_t wb = rmsf_welford_sequential_workspace_bytes(n_frames);
+    CX_OK(c->seqwork.ensure(std::max<size_t>(wb, 16), c->stream));
+    CX_OK(timed(c, RMSF_TIME_ACCUMULATE, c->n_sel * n_frames, [&] {
+      return rmsf_welford_sequential(d_xyz, stride, n_frames, c->n_sel, d_sel, r.n, r.parts0.d(), r.parts1.d(),
+                                     c->seqwork.p, c->seqwork.bytes, c->stream);
+    }));
+    r.n += n_frames;
+    r.stale = false;
+    c->wel_aligned = false;
+    c->rmsf_valid = false;
+    c->merged_away = false;
+    return RMSF_OK;
+  }
   const double *xf = nullptr;
   if (aligned) {
     if (!c->ref_set) return fail(RMSF_EINVAL, "rmsf_push: aligned mode before a reference was set");
@@ -562,7 +584,7 @@ int same_digests(rmsf_ctx **cs, int n, bool shift, bool *same) {
 }
 
 int check_mode(int mode, const char *fn) {
-  if (mode < RMSF_PUSH_WELFORD || mode > RMSF_PUSH_SUM) return fail(RMSF_EINVAL, std::string(fn) + ": bad mode");
+  if (mode < RMSF_PUSH_WELFORD || mode > RMSF_PUSH_EXACT) return fail(RMSF_EINVAL, std::string(fn) + ": bad mode");
   return RMSF_OK;
 }
 
@@ -1635,7 +1657,8 @@ RMSF_EXPORT int rmsf_multi_push_frames(rmsf_ctx **cs, int n, const float *const 
   return for_each_ctx(cs, n, [&](int i) -> int {
     rmsf_ctx *c = cs[i];
     if (flags & RMSF_MULTI_RESET)
-      CX_OK(rmsf_ctx_reset(c, (mode == RMSF_PUSH_WELFORD || mode == RMSF_PUSH_ALIGN_WELFORD) ? 1 : 2));
+      CX_OK(rmsf_ctx_reset(c, (mode == RMSF_PUSH_WELFORD || mode == RMSF_PUSH_ALIGN_WELFORD ||
+                               mode == RMSF_PUSH_EXACT) ? 1 : 2));
     if (d_ref_frames && d_ref_frames[i]) CX_OK(rmsf_set_reference_frame(c, d_ref_frames[i], 1));
     // the shift frame is needed only by the merge: its gather is queued on
     // the side stream AFTER this push's launches (so they leave the host

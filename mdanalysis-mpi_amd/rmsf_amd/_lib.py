@@ -153,7 +153,7 @@ SIGNATURES = {
 
 # int (*rmsf_allreduce_fn)(double *d_buf, int64_t count, void *stream, void *user)
 ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int64, c_void_p, c_void_p)
-RMSF_PUSH_WELFORD, RMSF_PUSH_ALIGN_SUM, RMSF_PUSH_ALIGN_WELFORD, RMSF_PUSH_SUM = 0, 1, 2, 3
+RMSF_PUSH_WELFORD, RMSF_PUSH_ALIGN_SUM, RMSF_PUSH_ALIGN_WELFORD, RMSF_PUSH_SUM, RMSF_PUSH_EXACT = 0, 1, 2, 3, 4
 RMSF_UNIQUE_ID_BYTES = 128
 RMSF_TIME_ACCUMULATE, RMSF_TIME_SUPERPOSE = 0, 1
 RMSF_MULTI_RESET = 1

@@ -27,14 +27,15 @@ import ctypes
 
 import numpy as np
 
-from ._lib import (ALLREDUCE_FN, RMSF_MULTI_RESET, RMSF_PUSH_ALIGN_SUM, RMSF_PUSH_ALIGN_WELFORD, RMSF_PUSH_SUM,
-                   RMSF_PUSH_WELFORD, RMSF_TIME_ACCUMULATE, RMSF_TIME_SUPERPOSE, RMSF_TRANSPORT_AUTO,
+from ._lib import (ALLREDUCE_FN, RMSF_MULTI_RESET, RMSF_PUSH_ALIGN_SUM, RMSF_PUSH_ALIGN_WELFORD, RMSF_PUSH_EXACT,
+                   RMSF_PUSH_SUM, RMSF_PUSH_WELFORD, RMSF_TIME_ACCUMULATE, RMSF_TIME_SUPERPOSE, RMSF_TRANSPORT_AUTO,
                    RMSF_TRANSPORT_NOOP, RMSF_UNIQUE_ID_BYTES, call, load)
 
 PUSH_WELFORD = RMSF_PUSH_WELFORD
 PUSH_ALIGN_SUM = RMSF_PUSH_ALIGN_SUM
 PUSH_ALIGN_WELFORD = RMSF_PUSH_ALIGN_WELFORD
 PUSH_SUM = RMSF_PUSH_SUM
+PUSH_EXACT = RMSF_PUSH_EXACT  # RMSF.py:137-138 as written (rmsf_welford_sequential)
 TRANSPORT_AUTO = RMSF_TRANSPORT_AUTO
 TRANSPORT_NOOP = RMSF_TRANSPORT_NOOP
 

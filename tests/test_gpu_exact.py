@@ -124,3 +124,40 @@ def test_rmsf_exact_ranks(size, n_frames, root):
         _same(rmsf, want["rmsf"], f"rank {rank} rmsf")
         _same(mean, want["mean"], f"rank {rank} mean")
         _same(m2, want["m2"], f"rank {rank} sumsquares")
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_context_exact_push_is_rmsf_py_rank(device):
+    """RMSF_PUSH_EXACT through the context ABI (the torch-free boundary an
+    mpi4py / C host binds): a rank's S of RMSF.py:140 bit for bit over
+    several pushes (host frames through the stager in 7-frame batches, or
+    HBM frames), with a gathered selection; reduced by RMSF.py's own
+    second_order_moments in rank order (the oracle's chan_fold, what
+    RMSF.py:143 runs on the host) they give rmsf_script(size=3)'s result.
+    A checkpoint (get / set_partial) continues the recurrence exactly."""
+    from rmsf_amd import parallel
+    from rmsf_amd.context import PUSH_EXACT, Context
+    n_atoms, nf = 400, 90
+    traj = SY.frames(21, n_atoms, 0, nf)
+    sel = np.arange(3, n_atoms, 4)
+    x = torch.tensor(traj, device="cuda") if device else traj
+    parts = []
+    for b0, b1 in parallel.blocks(nf, 3):
+        S = O.rank_sweep2(traj, sel, None, b0, b1)
+        mid = (b0 + b1) // 2
+        with Context(n_atoms, sel=sel) as c, Context(n_atoms, sel=sel) as d:
+            c.set_staging(batch_frames=7, n_slots=2, n_threads=2)
+            c.push(x[b0:mid], PUSH_EXACT)
+            d.set_partial(*c.partial())          # checkpoint -> restore, then continue
+            c.push(x[mid:b1], PUSH_EXACT)
+            d.push(x[mid:b1], PUSH_EXACT)
+            for ctx in (c, d):
+                n, mean, m2 = ctx.partial()
+                assert n == b1 - b0
+                _same(mean.reshape(-1), S[1].reshape(-1), f"block {b0}-{b1} mean")
+                _same(m2.reshape(-1), S[2].reshape(-1), f"block {b0}-{b1} sumsquares")
+            parts.append((n, mean.reshape(-1, 3), m2.reshape(-1, 3)))
+            _same(c.rmsf(), np.sqrt(S[2].sum(axis=1) / (b1 - b0)), "the context's own RMSF.py:146")
+    Data = O.chan_fold(parts)
+    want = O.rmsf_script(traj, sel, size=3, align=None)
+    _same(np.sqrt(Data[2].sum(axis=1) / Data[0]), want["rmsf"], "rmsf, 3 ranks reduced in rank order")
