@@ -45,7 +45,12 @@ def main(argv=None) -> int:
     ap.add_argument("--out", default=None, help="write rank 0's RMSF (.npy)")
     ap.add_argument("--merge", choices=["root", "all", "scatter"], default="root",
                     help="N>1: reduce to rank 0 (RMSF.py:143, default), all-reduce, or reduce-scatter by atom slices")
+    ap.add_argument("--exact", action="store_true",
+                    help="with --align none: RMSF.py:120-146 with the script's own arithmetic, bit for bit "
+                         "(per-frame Welford, ranks reduced in rank order by second_order_moments)")
     a = ap.parse_args(argv)
+    if a.exact and (a.align != "none" or a.merge == "scatter"):
+        ap.error("--exact needs --align none and --merge root or all")
 
     import torch
     import torch.distributed as dist
@@ -72,7 +77,8 @@ def main(argv=None) -> int:
         motion = motion_table(a.seed + 1, n_frames) if align else None
         shard = generate(eng, n_atoms, b0, max(b1 - b0, 1), seed=a.seed, motion=motion)[: b1 - b0]
         res = run_pipeline(eng, DeviceSource(shard, offset=b0, n_traj=n_frames), FrameList(n_frames),
-                           align=align, ref_frame=a.ref_frame, merge_root=root, merge_scatter=a.merge == "scatter")
+                           align=align, ref_frame=a.ref_frame, merge_root=root, merge_scatter=a.merge == "scatter",
+                           exact=a.exact)
         rmsf = None if res.rmsf is None else res.rmsf.cpu().numpy()   # None on the non-root ranks
     else:
         if not (a.topology and a.trajectory):
@@ -84,7 +90,8 @@ def main(argv=None) -> int:
         if mda is not None:
             u = mda.Universe(a.topology, a.trajectory)
             ag = u.select_atoms(a.select)
-            rmsf = RMSF(ag, align=align, ref_frame=a.ref_frame, verbose=True, merge_root=root).run().results.rmsf
+            rmsf = RMSF(ag, align=align, ref_frame=a.ref_frame, verbose=True, merge_root=root,
+                        exact=a.exact).run().results.rmsf
         else:
             # native fallback: GRO or PSF topology + selection subset; XTC, DCD (or
             # multi-frame GRO) trajectory.  PSF masses (GRO: masses guessed from
@@ -101,7 +108,7 @@ def main(argv=None) -> int:
             traj = (a.trajectory if a.trajectory.lower().endswith((".xtc", ".dcd"))
                     else GroTopology(a.trajectory).frames)
             rmsf = RMSF(traj, select=sel, align=align, masses=masses, ref_frame=a.ref_frame,
-                        verbose=True, merge_root=root).run().results.rmsf
+                        verbose=True, merge_root=root, exact=a.exact).run().results.rmsf
     if rank == 0:
         print(f"RMSF over {len(rmsf)} atoms: mean {rmsf.mean():.6f} A, max {rmsf.max():.6f} A", flush=True)
         if a.out:

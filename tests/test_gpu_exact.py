@@ -161,3 +161,34 @@ def test_context_exact_push_is_rmsf_py_rank(device):
     Data = O.chan_fold(parts)
     want = O.rmsf_script(traj, sel, size=3, align=None)
     _same(np.sqrt(Data[2].sum(axis=1) / Data[0]), want["rmsf"], "rmsf, 3 ranks reduced in rank order")
+
+
+def test_script_mode_exact(tmp_path):
+    """rmsf_mi355x.py --align none --exact on RMSF.py's input pair (GRO +
+    XTC, read natively): the script's own arithmetic on the decoded frames,
+    bit for bit; --exact with alignment is refused."""
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+    from rmsf_amd.topology import GroTopology, write_gro
+    from rmsf_amd.xtc import XTCFile, write_xtc
+    n_res = 40
+    resids = np.repeat(np.arange(1, n_res + 1), 3)
+    resnames = np.array(["ALA"] * (3 * n_res))
+    names = np.tile(["N", "CA", "C"], n_res)
+    x = SY.frames(31, len(names), 0, 33)
+    gro, xtc, out = str(tmp_path / "s.gro"), str(tmp_path / "s.xtc"), str(tmp_path / "rmsf.npy")
+    write_gro(gro, resids, resnames, names, x[0])
+    write_xtc(xtc, x)
+    script = f"{ROOT}/mdanalysis-mpi_amd/rmsf_mi355x.py"
+    r = subprocess.run([sys.executable, script, "--topology", gro, "--trajectory", xtc, "--out", out,
+                        "--align", "none", "--exact"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    sel = GroTopology(gro).select("protein and name CA")
+    with XTCFile(xtc) as f:
+        dec = f.read()
+    _same(np.load(out), O.rmsf_script(dec, sel, None, size=1, align=None)["rmsf"], "script --exact")
+    bad = subprocess.run([sys.executable, script, "--synthetic", "10", "5", "--exact"], capture_output=True,
+                         text=True, timeout=120)
+    assert bad.returncode != 0 and "--exact needs --align none" in bad.stderr
