@@ -3,7 +3,8 @@ selections, align modes, frame selections and inputs (HBM tensor / host
 array in rows or coordinate planes / HBM planes / DCD or XTC file / one-process
 gpus=1)
 through RMSF(...).run() vs the oracle's RMSF.py
-restatement on the selected frames.  python tools/fuzz_parity.py [n_cases [--big]]"""
+restatement on the selected frames; the unaligned cases also through
+RMSF(..., exact=True), which must match the restatement bit for bit.  python tools/fuzz_parity.py [n_cases [--big]]"""
 import os
 import sys
 import tempfile
@@ -25,7 +26,7 @@ from rmsf_amd.synth import motion_table  # noqa: E402
 def main():
     n_cases = int(sys.argv[1]) if len(sys.argv) > 1 else 40
     rng = np.random.default_rng(2026)
-    worst = 0.0
+    worst, n_exact = 0.0, 0
     tmp = tempfile.mkdtemp(prefix="fuzz_")
     big = "--big" in sys.argv[2:]  # larger shapes: up to 200k atoms / 4,000 frames, <= 2e7 atom-frames
     for k in range(n_cases):
@@ -74,7 +75,13 @@ def main():
         print(f"case {k:2d}: {na:5d} atoms {len(sel):5d} sel {len(frames):4d}/{nf:3d} frames align={align} "
               f"{where:6s} batch={bf} max|d|={err:.2e}", flush=True)
         assert err < 1e-6, f"case {k}: {err}"
-    print(f"all {n_cases} cases within 1e-6 A (worst {worst:.2e})")
+        if align is None and where != "gpus1":
+            # exact=True: RMSF.py:120-146's own arithmetic, bit for bit
+            ex = RMSF(x, select=sel, exact=True, batch_frames=bf, **kw).run(frames=frames).results.rmsf
+            assert np.array_equal(ex.view(np.uint64), exp.view(np.uint64)), f"case {k}: exact=True differs"
+            n_exact += 1
+    print(f"all {n_cases} cases within 1e-6 A (worst {worst:.2e}); exact=True bit for bit in all {n_exact} "
+          f"unaligned cases")
 
 
 if __name__ == "__main__":
