@@ -31,7 +31,7 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 
 from . import parallel
-from .context import PUSH_ALIGN_SUM, PUSH_ALIGN_WELFORD, PUSH_WELFORD, Context
+from .context import PUSH_ALIGN_SUM, PUSH_ALIGN_WELFORD, PUSH_EXACT, PUSH_WELFORD, Context
 from ._lib import RmsfEmptyError
 from .sources import FrameList
 
@@ -345,16 +345,43 @@ def _set_frame(c: Context, fr, setter: str) -> None:
         getattr(c, setter)(fr)
 
 
+def _exact_merge(ctxs, home_dev) -> dict:
+    """RMSF.py:141-146 for exact=True: the contexts' states (each a block's S
+    of RMSF.py:140) folded in device order by k_chan_merge (RMSF.py:36-41
+    bit for bit) on ``home_dev``, then RMSF.py:146."""
+    import torch
+
+    from .engine import Engine
+    parts = [c.partial() for c in ctxs]
+    n_coord = parts[0][1].size
+    eng = Engine(torch.device("cuda", home_dev))
+    with torch.cuda.device(eng.device):
+        means = torch.tensor(np.stack([p[1].reshape(-1) for p in parts]), device=eng.device)
+        m2s = torch.tensor(np.stack([p[2].reshape(-1) for p in parts]), device=eng.device)
+        mean, m2, rmsf = eng.empty(n_coord), eng.empty(n_coord), eng.empty(n_coord // 3)
+        counts = [int(p[0]) for p in parts]
+        eng.chan_merge(means, m2s, counts, n_coord, mean, m2)
+        eng.finalize(m2, n_coord // 3, sum(counts), rmsf)
+        torch.cuda.current_stream(eng.device).synchronize()
+        return dict(rmsf=rmsf.cpu().numpy(), mean=mean.cpu().numpy().reshape(-1, 3),
+                    sumsquares=m2.cpu().numpy().reshape(-1, 3), n_frames=sum(counts))
+
+
 def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int = 0, start=None, stop=None,
               step=None, batch_frames: int | None = None, frames=None, collect_rmsd: bool = False,
-              layout: str = "fac", merge_root: int | None = None) -> dict:
+              layout: str = "fac", merge_root: int | None = None, exact: bool = False) -> dict:
     """RMSF.py's computation over the devices ``gpus`` from one process.
     Returns the ``results`` fields (rmsf, mean, sumsquares, n_frames, ...;
     ``rmsd`` with ``collect_rmsd``: per-frame QCP rmsd of the last sweep in
     frame-list order, the by-product RMSF.py:48 discards).  ``merge_root``:
     the final merge is a reduce to that device index (RMSF.py:143's shape)
     and the results are read from it; None = an all-reduce, read from
-    device index 0 (the same numbers)."""
+    device index 0 (the same numbers).  ``exact`` (align=None): every
+    device runs RMSF.py:137-138's recurrence over its block (RMSF_PUSH_EXACT)
+    and the blocks are folded in device order by second_order_moments
+    (k_chan_merge on the home device): the script's arithmetic bit for bit."""
+    if exact and align is not None:
+        raise NotImplementedError("exact=True covers align=None (RMSF.py:120-146 on an aligned trajectory)")
     if align not in (None, "frame0", "average"):
         raise ValueError(f"align must be one of (None, 'frame0', 'average'), got {align!r}")
     if parallel.world()[1] > 1:
@@ -421,7 +448,7 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
                 ref = ref[src.sel]
             for c in ctxs:  # every rank reads the reference frame (RMSF.py:80-87)
                 _set_frame(c, ref, "set_reference_frame")
-        elif len(ctxs) > 1:
+        elif len(ctxs) > 1 and not exact:
             # the merge's shift: frame 0 of the frame list on every context
             # (the one-collective merge, as the torchrun pipeline's)
             shift = src.reference(fl[0])
@@ -477,10 +504,15 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
         if collect_rmsd:
             for c in ctxs:  # the last sweep's rmsd only, as the pipeline reports it
                 c.collect_rmsd(True)
+        last = PUSH_EXACT if exact else (PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD)
         if whole:
-            multi_push(PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD)
+            multi_push(last)
         else:
-            each(lambda i: push(i, PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD))
+            each(lambda i: push(i, last))
+        if exact:
+            out.update(_exact_merge(ctxs, devs[merge_root or 0]), blocks=[(int(b0), int(b1)) for b0, b1 in spans],
+                       devices=devs)
+            return out
         Context.multi_chan_merge(ctxs, root=merge_root)
         home = ctxs[merge_root or 0]
         n, mean, m2 = home.partial()

@@ -146,8 +146,6 @@ class RMSF:
             if self.merge_scatter:
                 raise NotImplementedError("merge_scatter is for one process per GPU (torch.distributed); with "
                                           "gpus= the one process receives the merged result")
-            if self.exact:
-                raise NotImplementedError("exact=True is for one device per process")
             return self._run_multi(start, stop, step, frames)  # several devices, or HBM shards per device
         eng = Engine(self.device)
         # torch's current device = the engine's, so the buffers sources and
@@ -198,7 +196,7 @@ class RMSF:
         out = run_multi(self._input, self.gpus, select=self.select, align=self.align, masses=self.masses,
                         ref_frame=self.ref_frame, start=start, stop=stop, step=step,
                         batch_frames=self.batch_frames, frames=frames, collect_rmsd=self.collect_rmsd,
-                        layout=self.layout, merge_root=self.merge_root)
+                        layout=self.layout, merge_root=self.merge_root, exact=self.exact)
         r = self.results
         r.update(out)
         r.m2 = r.sumsquares

@@ -192,3 +192,28 @@ def test_script_mode_exact(tmp_path):
     bad = subprocess.run([sys.executable, script, "--synthetic", "10", "5", "--exact"], capture_output=True,
                          text=True, timeout=120)
     assert bad.returncode != 0 and "--exact needs --align none" in bad.stderr
+
+
+@pytest.mark.parametrize("inp", ["host", "shards"])
+@pytest.mark.parametrize("gpus", [1, [0, 0, 0]])
+def test_rmsf_exact_one_process_devices(inp, gpus):
+    """RMSF(gpus=..., exact=True): each device context runs RMSF.py:137-138's
+    recurrence over its RMSF.py:65-69 block (RMSF_PUSH_EXACT), the blocks
+    are folded in device order by second_order_moments: rmsf_script with
+    size = the device count, bit for bit.  Host input (contexts stage their
+    blocks) and HBM shards (each device's frames in place, three shards of
+    a 71-frame trajectory)."""
+    from rmsf_amd import RMSF, parallel
+    n_atoms, nf = 300, 71
+    traj = SY.frames(17, n_atoms, 0, nf)
+    sel = np.arange(1, n_atoms, 3)
+    n_dev = 1 if gpus == 1 else len(gpus)
+    if inp == "host":
+        x = traj
+    else:
+        x = [torch.tensor(traj[b0:b1], device="cuda") for b0, b1 in parallel.blocks(nf, n_dev)]
+    r = RMSF(x, select=sel, exact=True, gpus=gpus, batch_frames=9).run().results
+    want = O.rmsf_script(traj, sel, None, size=n_dev, align=None)
+    _same(r.rmsf, want["rmsf"], "rmsf")
+    _same(r.mean, want["mean"], "mean")
+    _same(r.sumsquares, want["m2"], "sumsquares")
