@@ -560,6 +560,8 @@ def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, 
     mean, ss = eng.zeros(3 * n_sel), eng.zeros(3 * n_sel)   # RMSF.py:119-120
     work, k = None, 0
     for b in source.batches(frames, b0, b1, max_batch, eng.stream):  # rows: (frame, atom, xyz)
+        if b.pstride:
+            raise ValueError("exact=True reads (frame, atom, xyz) rows; this source handed over coordinate planes")
         with _span(timer, "accumulate", b.n_frames * n_sel):
             work = eng.welford_sequential(b.ptr, b.fstride, b.n_frames, n_sel, b.sel, k, mean, ss, work)
         k += b.n_frames
