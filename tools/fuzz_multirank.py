@@ -6,8 +6,10 @@ plan allows them -- each rank's RMSF against the oracle's mpirun -n P
 emulation of RMSF.py.  ``--root``: half the cases merge with a reduce to a
 random rank (merge_root); ``--planes``: half the shards are HBM coordinate
 planes; ``--scatter``: a third of the other cases merge as a reduce-scatter
-by atom slices with the RMSF gathered to a random root (merge_scatter).
-python tools/fuzz_multirank.py [n_cases [--root] [--planes] [--scatter]]"""
+by atom slices with the RMSF gathered to a random root (merge_scatter);
+``--exact``: half the unaligned cases run exact=True and must equal the
+oracle's P-rank script bit for bit.
+python tools/fuzz_multirank.py [n_cases [--root] [--planes] [--scatter] [--exact]]"""
 import os
 import sys
 import tempfile
@@ -42,7 +44,8 @@ def _worker(rank, size, init, q, case):
         else:
             src = DeviceSource(shard, sel, offset=b0, n_traj=nf)
         res = run_pipeline(eng, src, FrameList(nf), align=align, max_batch=batch, merge_slabs=slabs,
-                           merge_root=case.get("root"), merge_scatter=bool(case.get("scatter")))
+                           merge_root=case.get("root"), merge_scatter=bool(case.get("scatter")),
+                           exact=bool(case.get("exact")))
         torch.cuda.synchronize()
         q.put((rank, None if res.rmsf is None else res.rmsf.cpu().numpy(), res.extras.get("merge_slabs", 0)))
     except Exception as e:  # noqa: BLE001
@@ -75,7 +78,7 @@ def main():
     from rmsf_amd.synth import motion_table
     n_cases = int(sys.argv[1]) if len(sys.argv) > 1 else 24
     rng = np.random.default_rng(303)
-    worst = 0.0
+    worst, n_exact = 0.0, 0
     for k in range(n_cases):
         P = int(rng.integers(2, 5))
         big = k % 6 == 5  # every sixth case: 300k atoms, the chunk-aligned plan (merge slabs)
@@ -98,6 +101,8 @@ def main():
         if "--scatter" in sys.argv[2:] and not case.get("planes") and rng.random() < 0.34:
             case["scatter"] = True  # reduce-scatter by atom slices, RMSF gathered to the root
             case["root"] = int(rng.integers(0, P))
+        if "--exact" in sys.argv[2:] and align is None and not big and not case.get("scatter") and rng.random() < 0.5:
+            case["exact"] = True  # RMSF.py's own arithmetic: bit for bit with the oracle's P-rank script
         out = run_case(case)
         if any(o[2] == -1 for o in out):
             print(f"case {k}: FAILED {[o[1] for o in out if o[2] == -1][:1]}", flush=True)
@@ -111,15 +116,19 @@ def main():
         if root is not None:  # only the root has a result
             assert all((o[1] is None) == (o[0] != root) for o in out), "reduce-to-root results on the wrong ranks"
         d = max(float(np.abs(o[1] - exp).max()) for o in out if o[1] is not None)
+        if case.get("exact"):
+            assert all(np.array_equal(o[1].view(np.uint64), exp.view(np.uint64)) for o in out if o[1] is not None), \
+                f"case {k}: exact=True differs from the oracle's bits"
+            n_exact += 1
         worst = max(worst, d)
         print(f"case {k:2d}: P={P} {na:7d} atoms {len(cols):7d} sel {nf:4d} frames align={align} "
               f"batch={batch} slabs={out[0][2]} root={root} planes={bool(case.get('planes'))} "
-              f"scatter={bool(case.get('scatter'))} max|d|={d:.2e}",
+              f"scatter={bool(case.get('scatter'))} exact={bool(case.get('exact'))} max|d|={d:.2e}",
               flush=True)
         if d > 1e-6:
             print("EXCEEDS 1e-6", flush=True)
             sys.exit(1)
-    print(f"all {n_cases} cases within 1e-6 A (worst {worst:.2e})")
+    print(f"all {n_cases} cases within 1e-6 A (worst {worst:.2e}); exact=True bit for bit in {n_exact} cases")
 
 
 if __name__ == "__main__":
