@@ -319,9 +319,10 @@ int rmsf_fold_balanced_shift_slab(const void *d_work, int64_t n_coord,
  * reassociated, frame-parallel form (faster, equal to ~1e-13).
  * d_work: rmsf_welford_sequential_workspace_bytes(n_frames) bytes (the
  * per-frame coefficients).  Replaces RMSF.py:120-138's loop for one rank.
- * Domain of the bit-for-bit claim: any float32 coordinates (zeros, infinities
- * and NaNs included) and any running state they can produce; a caller-made
- * state with |mean| beyond ~1e270 would need the full division sequence.  */
+ * Domain of the bit-for-bit claim: any float32 coordinates (zeros and
+ * infinities included; NaN wherever the reference has NaN, payload bits
+ * aside) and any running state they can produce; a caller-made state with
+ * |mean| beyond ~1e270 would need the full division sequence.              */
 size_t rmsf_welford_sequential_workspace_bytes(int64_t n_frames);
 int rmsf_welford_sequential(const float *d_xyz, int64_t frame_stride,
                             int64_t n_frames, int64_t n_sel,
