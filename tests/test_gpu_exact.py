@@ -217,3 +217,30 @@ def test_rmsf_exact_one_process_devices(inp, gpus):
     _same(r.rmsf, want["rmsf"], "rmsf")
     _same(r.mean, want["mean"], "mean")
     _same(r.sumsquares, want["m2"], "sumsquares")
+
+
+def test_sequential_special_values():
+    """Zeros (both signs), infinities and NaNs in the frames: the fast
+    division's select passes zero and infinity numerators through, NaN
+    propagates -- the reference recurrence's values wherever it has a
+    number, NaN wherever it has NaN."""
+    from rmsf_amd.engine import Engine
+    eng = Engine()
+    n_atoms, nf = 64, 50
+    traj = SY.frames(3, n_atoms, 0, nf)
+    rng = np.random.default_rng(9)
+    for v in (0.0, -0.0, np.inf, -np.inf, np.nan):
+        idx = rng.integers(0, nf, 6), rng.integers(0, n_atoms, 6), rng.integers(0, 3, 6)
+        traj[idx] = np.float32(v)
+    traj[:, 5, 0] = 0.0            # a column that is zero throughout
+    traj[:, 6, 1] = -0.0           # ... and negative zero throughout
+    S = O.rank_sweep2(traj, np.arange(n_atoms), None, 0, nf)
+    x = torch.tensor(traj, device="cuda")
+    m, q = eng.empty(3 * n_atoms), eng.empty(3 * n_atoms)
+    eng.welford_sequential(x.data_ptr(), 3 * n_atoms, nf, n_atoms, None, 0, m, q)
+    torch.cuda.synchronize()
+    for got, want, what in ((m.cpu().numpy(), S[1].reshape(-1), "mean"), (q.cpu().numpy(), S[2].reshape(-1),
+                                                                         "sumsquares")):
+        nan = np.isnan(want)
+        assert np.array_equal(np.isnan(got), nan), f"{what}: NaN pattern"
+        _same(got[~nan], want[~nan], what)
