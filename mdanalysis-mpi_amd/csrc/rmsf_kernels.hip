@@ -420,16 +420,15 @@ __global__ __launch_bounds__(kBlock) void k_welford_flat_sk(const float *__restr
 //   mean = (k * mean + x) / (k + 1)
 // with numpy's operations and roundings (no contraction, csrc/Makefile), so
 // the running (mean, sumsquares) are the reference recurrence's own values
-// bit for bit.  Parallel over coordinates only: a lane carries CPT
-// consecutive coordinates through every frame, with the next U frames' loads
-// in flight while it folds the current U.  The per-frame constants come
-// from a table (k_seq_coef) read by scalar loads: c_k = k / (k + 1.0), and
-// r_k, 1 / (k + 1) refined as the hardware division refines it, so the
-// division costs a mul and two FMAs per coordinate -- q0 = num r_k,
-// q = fma(fma(-(k+1), q0, num), r_k, q0), the closing steps of the IEEE
-// division sequence (v_div_scale / v_div_fmas / v_div_fixup change nothing
-// for a finite numerator in normal range; any other numerator takes the
-// full division).
+// bit for bit.  Parallel over coordinates only: a lane carries one
+// coordinate through every frame, with the next U frames' loads in flight
+// while it folds the current U.  The per-frame constants come from a table
+// (k_seq_coef) read by scalar loads: c_k = k / (k + 1.0), and r_k, 1 / (k + 1)
+// refined as the hardware division refines it, so the division costs a mul
+// and two FMAs per coordinate -- q0 = num r_k, q = fma(fma(-(k+1), q0, num),
+// r_k, q0), the closing steps of the IEEE division sequence (v_div_scale /
+// v_div_fmas / v_div_fixup change nothing for a finite numerator in normal
+// range; seq_div covers the rest).
 struct SeqCoef {
   double c, r;
 };
