@@ -481,8 +481,29 @@ __global__ __launch_bounds__(kBlock) void k_welford_seq(const float *__restrict_
       c[u] = coef[f + u];
     }
   };
+  // A block whose coordinates are all nonzero and finite, entered with a
+  // finite running mean, needs no select: every numerator k*mean + x is then
+  // finite and nonzero, or an exact cancellation to +0 that the closing steps
+  // also return as +0 (-0 needs x = -0).  Checked once per block and wave:
+  // 2 % faster at 100k x 20k, the same bits (tools/ab_seq_hoist.py).
+  auto step_fast = [&](float v, const SeqCoef cf, double k) {
+    const double x = (double)v;
+    const double d = x - m;
+    q = q + cf.c * (d * d);
+    const double num = k * m + x, k1 = k + 1.0;
+    const double q0 = num * cf.r;
+    m = __builtin_fma(__builtin_fma(-k1, q0, num), cf.r, q0);
+  };
   auto run = [&](const float (&v)[U], const SeqCoef (&c)[U], int64_t f) {
     const double kb = (double)(k0 + f);
+    bool special = __builtin_isinf(m);
+#pragma unroll
+    for (int u = 0; u < U; ++u) special |= (v[u] == 0.0f) | __builtin_isinf(v[u]);
+    if (!__any((int)special)) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) step_fast(v[u], c[u], kb + (double)u);
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) step(v[u], c[u], kb + (double)u);
   };
