@@ -94,3 +94,17 @@ def test_merge_scatter_and_rehearsal_transport_flags():
     a = bench.parse(["--merge", "scatter", "--gpus", "8", "--rehearse", "--rehearse-transport", "noop"])
     assert a.merge == "scatter" and a.rehearse and a.rehearse_transport == "noop"
     assert bench.parse([]).rehearse_transport == "fold"
+
+
+def test_script_exact_needs_unaligned_root_or_all():
+    """rmsf_mi355x.py --exact is RMSF.py:120-146's own arithmetic: refused
+    with alignment or the reduce-scatter merge, before any device work."""
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+    script = f"{ROOT}/mdanalysis-mpi_amd/rmsf_mi355x.py"
+    for extra in ([], ["--align", "frame0"], ["--align", "none", "--merge", "scatter"]):
+        r = subprocess.run([sys.executable, script, "--synthetic", "10", "5", "--exact", *extra],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 2 and "--exact needs --align none" in r.stderr, (extra, r.stderr[-500:])
