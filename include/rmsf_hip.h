@@ -172,13 +172,13 @@ int rmsf_fold_balanced(const void *d_work, int64_t n_coord, int mode,
                        int64_t acc_n, double *d_acc0, double *d_acc1,
                        void *stream);
 /* rmsf_fold_balanced (WELFORD) of the last batch + the finalise of
- * RMSF.py:146 (d_rmsf[n_sel] over n_total frames) in one launch, bit-identical
- * to rmsf_fold_balanced + rmsf_finalize.  Needs an atom plan: the aligned
- * sweep, a gathered selection or planes (one atom per lane).  The flat plan
- * of an unaligned contiguous selection cannot finalise in the fold: the call
- * then returns RMSF_EINVAL and launches nothing (the library remembers, on the
- * host, which plan its last accumulate wrote into d_work); rmsf_fold_balanced
- * + rmsf_finalize are the calls to make.                                   */
+ * RMSF.py:146 (d_rmsf[n_sel] over n_total frames), bit-identical to
+ * rmsf_fold_balanced + rmsf_finalize, for every plan the accumulate can
+ * write.  An atom plan (the aligned sweep, a gathered selection, planes: one
+ * atom per lane) finalises inside the fold (one launch); the flat plan of an
+ * unaligned contiguous selection (an atom's coordinates span two lanes) is
+ * finalised by a second launch.  The plan is read from the workspace's own
+ * header on the device (the host keeps no record of workspaces).          */
 int rmsf_fold_balanced_finalize(const void *d_work, int64_t n_coord,
                                 int64_t acc_n, double *d_acc0, double *d_acc1,
                                 int64_t n_total, double *d_rmsf, void *stream);
@@ -197,14 +197,51 @@ int rmsf_accumulate_balanced_planes(const float *d_xyz, int64_t frame_stride,
                                     size_t work_bytes, void *stream);
 
 /* ---- Chan merge: second_order_moments, RMSF.py:36-41 ------------------------
- * Folds n_parts partial (count, mean, M2) sets of n_coord coordinates, in
- * order 0..n_parts-1, with T=n1+n2, mu=(n1 mu1+n2 mu2)/T,
- * M=M1+M2+(n1 n2/T)(mu2-mu1)^2.  Empty partials are skipped (RMSF.py:39
- * raises ZeroDivisionError when both are empty; Appendix B Q5).
- * h_counts is a host array of n_parts counts.                               */
+ * op(S1, S2): T = n1+n2, mu = (n1 mu1 + n2 mu2)/T, M = M1+M2+(n1 n2/T)(mu2-mu1)^2,
+ * with RMSF.py's operations in its order (no FP contraction; n1 n2 / T as
+ * Python's exact int product and one rounded division, exact for
+ * n1 n2 < 2^53), so every value RMSF.py produces is reproduced bit for bit.
+ * An empty partial (count 0) is RMSF.py:119-121's (0, zeros, zeros) -- its
+ * memory is not read -- and enters op like any other (op((0,0,0), S) is not
+ * S bit for bit, as in RMSF.py).  op of two empty partials (T = 0), where
+ * RMSF.py:39 raises ZeroDivisionError, is skipped: the result stays empty.
+ * RMSF_EEMPTY when every partial is empty.
+ *
+ * rmsf_chan_merge folds n_parts partials of n_coord coordinates in order:
+ * res = part 0, res = op(res, part i) for i = 1..n_parts-1 (mpi4py's naive
+ * reduce, RMSF_MERGE_RANK below).  h_counts: host array of n_parts counts. */
 int rmsf_chan_merge(const double *d_mean_parts, const double *d_m2_parts,
                     const int64_t *h_counts, int n_parts, int64_t n_coord,
                     double *d_mean, double *d_m2, void *stream);
+
+/* The order RMSF.py:143's comm.reduce(S, root=0, op=second_order_moments)
+ * applies op in (mpi4py's lowercase object reduce; upstream, not vendored):
+ *   RMSF_MERGE_MPI4PY  mpi4py's default (rc.fast_reduce): a binomial tree,
+ *                      for mask = 1, 2, 4, ...: rank r, r % (2 mask) == 0,
+ *                      computes op(S_r, S_{r+mask}) -- at 4 ranks
+ *                      op(op(S0,S1), op(S2,S3)), at 5 op(op(op(S0,S1),
+ *                      op(S2,S3)), S4).  Equal to RANK up to 3 ranks.
+ *   RMSF_MERGE_RANK    rc.fast_reduce = False: op folded in rank order.   */
+#define RMSF_MERGE_RANK 0
+#define RMSF_MERGE_MPI4PY 1
+/* The schedule as (dst, src) steps S[dst] = op(S[dst], S[src]), S[0] the
+ * result: returns the step count (n_parts - 1) and, when h_dst/h_src are
+ * non-NULL, writes up to `capacity` steps.                                   */
+int rmsf_chan_reduce_steps(int n_parts, int order, int *h_dst, int *h_src,
+                           int capacity);
+/* comm.reduce's result over n_parts partials (the ranks' S of RMSF.py:140,
+ * in rank order) in the given order, written to d_mean / d_m2.  The parts
+ * are the schedule's working storage (each rank's `result`, as in mpi4py)
+ * and are overwritten.                                                      */
+int rmsf_chan_reduce(double *d_mean_parts, double *d_m2_parts,
+                     const int64_t *h_counts, int n_parts, int64_t n_coord,
+                     int order, double *d_mean, double *d_m2, void *stream);
+/* One step S1 = op(S1, S2) in place (S2 in separate buffers: the partial
+ * another rank or device just sent) -- a distributed reduction's building
+ * block.  RMSF_EEMPTY when n1 = n2 = 0.                                    */
+int rmsf_chan_merge_pair(double *d_mean1, double *d_m21, int64_t n1,
+                         const double *d_mean2, const double *d_m22,
+                         int64_t n2, int64_t n_coord, void *stream);
 
 /* sum of split partial sums (sweep 1, RMSF.py:103,105) */
 int rmsf_sum_splits(const double *d_parts, int n_parts, int64_t n_coord,
@@ -389,6 +426,11 @@ int rmsf_planes_to_rows(const double *d_src, int64_t n, double *d_dst,
 int rmsf_synth_frames(float *d_out, int64_t frame_stride, int64_t n_atoms,
                       int64_t f0, int64_t nf, uint64_t seed,
                       const double *d_motion, void *stream);
+/* The generator's noise scale sigma(a) of atoms a0..a0+n-1 (f64, device):
+ * an unaligned synthetic atom's population RMSF is sqrt(3) sigma(a) -- the
+ * reference value of the bench's per-mode sanity figure.                    */
+int rmsf_synth_sigma(double *d_sigma, int64_t a0, int64_t n, uint64_t seed,
+                     void *stream);
 
 /* ---- host -> device frame stager (north star subsystem 1) ---
  * Pinned-host, multi-buffered hipMemcpyAsync stager.  Frames arrive as host
@@ -539,9 +581,10 @@ typedef struct rmsf_ctx rmsf_ctx;
 /* RMSF.py:137-138 as written on the raw frames (rmsf_welford_sequential):
  * the running Welford state continued frame by frame with the reference's
  * own arithmetic, so rmsf_get_partial returns a rank's S of RMSF.py:140 bit
- * for bit -- reduce those with RMSF.py:143's own second_order_moments (or
- * rmsf_chan_merge in rank order) for the script's result.  The multi-context
- * merges combine such states too (to rounding, not bit for bit).          */
+ * for bit.  rmsf_multi_chan_merge_exact reduces such contexts with
+ * second_order_moments in comm.reduce's order (RMSF_MERGE_MPI4PY), device to
+ * device: the script's result bit for bit.  (rmsf_multi_chan_merge combines
+ * them too, to rounding.)                                                   */
 #define RMSF_PUSH_EXACT 4
 
 /* h_sel: n_sel int64 atom indices (MDAnalysis AtomGroup.indices; copied),
@@ -692,6 +735,18 @@ int rmsf_set_merge_shift_frame(rmsf_ctx *ctx, const float *xyz,
  * can reduce to a root; the two-pass form leaves the result everywhere.
  * Replaces RMSF.py:140-143 (comm.Barrier + comm.reduce(root=0)).           */
 int rmsf_multi_chan_merge_root(rmsf_ctx **ctxs, int n, int root);
+/* RMSF.py:141-143 as the script computes it: the contexts' Welford states
+ * (each a rank's S of RMSF.py:140, context i = rank i) reduced with
+ * second_order_moments in `order` (RMSF_MERGE_MPI4PY: comm.reduce's
+ * binomial tree; RMSF_MERGE_RANK: rank order) -- each step copies the
+ * source context's state to the destination's device (peer copy over xGMI,
+ * or a device copy) and merges it there (rmsf_chan_merge_pair), the steps of
+ * one tree level on their own streams at once.  The result is context 0's,
+ * then forwarded to `root` (the others refuse getters with RMSF_EINVAL until
+ * reset) or, root = -1, to every context.  Bit for bit with RMSF.py:143 on
+ * RMSF_PUSH_EXACT states.  Contexts of this process only (a communicator
+ * spanning processes: RMSF_EINVAL).                                        */
+int rmsf_multi_chan_merge_exact(rmsf_ctx **ctxs, int n, int root, int order);
 /* Push each context's HBM frames d_frames[i] (n_frames[i] frames,
  * frame_stride floats apart, 0 = 3*n_atoms) in `mode`, the n contexts'
  * launches enqueued from one host thread per context (asynchronous: the

@@ -319,6 +319,7 @@ struct rmsf_ctx {
   int transport = RMSF_TRANSPORT_AUTO;
   hipStream_t comm_stream = nullptr;  // the slab merge's RCCL calls (beside the next slab)
   std::vector<hipEvent_t> ev_pack, ev_done;
+  hipEvent_t ev_sent = nullptr;  // the exact merge: this context's state is ready to be read by a peer
   Worker *worker = nullptr;
 
   const int32_t *d_sel() const { return h_sel.empty() ? nullptr : static_cast<const int32_t *>(sel.p); }
@@ -1024,6 +1025,91 @@ int slab_merge(rmsf_ctx **cs, int n, int kind, const Reduce &red, int root) {
   return RMSF_OK;
 }
 
+// RMSF.py:141-143 with second_order_moments' own arithmetic over contexts of
+// this process (each holding a rank's S of RMSF.py:140, e.g. from
+// RMSF_PUSH_EXACT), device to device: the reduction schedule of `order`
+// (rmsf_chan_reduce_steps) run as mpi4py runs it -- for each step
+// S[dst] = op(S[dst], S[src]), src's state is copied to dst's device
+// (hipMemcpyPeerAsync on dst's stream, after an event on src's stream; xGMI
+// between devices, a device copy on one) and merged there by
+// rmsf_chan_merge_pair.  The tree's steps at one level run on different
+// streams concurrently.  The result lands in context 0, then goes to `root`
+// (root >= 0, as mpi4py forwards 0's result to root; the others are left
+// merged_away) or to every context (root = -1).
+int ensure_event(hipEvent_t *e) {
+  if (!*e) CX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  return RMSF_OK;
+}
+
+// d's stream copies s's Welford state (mean, M2) into d->xb after s's queued work
+int pull_state(rmsf_ctx *d, rmsf_ctx *s, int64_t nc) {
+  {
+    DeviceScope ds(s->dev);
+    CX_OK(ensure_event(&s->ev_sent));
+    CX_HIP(hipEventRecord(s->ev_sent, s->stream));
+  }
+  DeviceScope dd(d->dev);
+  CX_OK(d->xb.ensure(sizeof(double) * 2 * nc, d->stream));
+  CX_HIP(hipStreamWaitEvent(d->stream, s->ev_sent, 0));
+  const size_t row = sizeof(double) * nc;
+  CX_HIP(hipMemcpyPeerAsync(d->xb.p, d->dev, s->wel.parts0.p, s->dev, row, d->stream));
+  CX_HIP(hipMemcpyPeerAsync(d->xb.d() + nc, d->dev, s->wel.parts1.p, s->dev, row, d->stream));
+  return RMSF_OK;
+}
+
+int exact_merge(rmsf_ctx **cs, int n, int root, int order) {
+  std::vector<int64_t> cnt(n);
+  for (int i = 0; i < n; ++i) {
+    DeviceScope ds(cs[i]->dev);
+    CX_OK(settle(cs[i]));
+    CX_OK(ensure_zeroed(cs[i], cs[i]->wel, true));
+    cnt[i] = cs[i]->wel.n;
+  }
+  int64_t total = 0;
+  for (int64_t v : cnt) total += v;
+  if (total == 0) return fail(RMSF_EEMPTY, "rmsf exact merge: no frames on any rank (RMSF.py:39 ZeroDivisionError)");
+  const int64_t nc = cs[0]->n_coord;
+  const int ns = rmsf_chan_reduce_steps(n, order, nullptr, nullptr, 0);
+  if (ns < 0) return ns;
+  std::vector<int> dst(std::max(ns, 1)), src(std::max(ns, 1));
+  if (ns > 0) CX_OK(rmsf_chan_reduce_steps(n, order, dst.data(), src.data(), ns) < 0 ? RMSF_EINVAL : RMSF_OK);
+  for (int k = 0; k < ns; ++k) {
+    rmsf_ctx *d = cs[dst[k]], *s = cs[src[k]];
+    const int64_t n1 = cnt[dst[k]], n2 = cnt[src[k]];
+    if (n1 + n2 == 0) continue;  // two empty states (where RMSF.py:39 raises): dst stays empty
+    CX_OK(pull_state(d, s, nc));
+    DeviceScope dd(d->dev);
+    CX_OK(rmsf_chan_merge_pair(d->wel.parts0.d(), d->wel.parts1.d(), n1, d->xb.d(), d->xb.d() + nc, n2, nc,
+                               d->stream));
+    cnt[dst[k]] = n1 + n2;
+  }
+  // S[0] is comm.reduce's result; forward it as mpi4py forwards rank 0's
+  for (int i = 0; i < n; ++i) {
+    rmsf_ctx *c = cs[i];
+    if (i != 0 && root >= 0 && i != root) {
+      c->merged_away = true;
+      c->rmsf_valid = false;
+      continue;
+    }
+    if (i != 0) {
+      CX_OK(pull_state(c, cs[0], nc));
+      DeviceScope dc(c->dev);
+      CX_HIP(hipMemcpyAsync(c->wel.parts0.p, c->xb.p, sizeof(double) * nc, hipMemcpyDeviceToDevice, c->stream));
+      CX_HIP(hipMemcpyAsync(c->wel.parts1.p, c->xb.d() + nc, sizeof(double) * nc, hipMemcpyDeviceToDevice,
+                            c->stream));
+    }
+    c->wel.n = total;
+    c->wel_aligned = false;
+    c->rmsf_valid = false;
+    c->merged_away = false;
+  }
+  if (root > 0) {  // rank 0 only sent its result on
+    cs[0]->merged_away = true;
+    cs[0]->rmsf_valid = false;
+  }
+  return RMSF_OK;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -1108,6 +1194,7 @@ RMSF_EXPORT int rmsf_ctx_destroy(rmsf_ctx *c) {
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
+    if (c->ev_sent) (void)hipEventDestroy(c->ev_sent);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;  // DevBufs free on the context's device
   }
@@ -1124,6 +1211,9 @@ RMSF_EXPORT int rmsf_ctx_stream(rmsf_ctx *c, void **stream) {
 RMSF_EXPORT int rmsf_ctx_synchronize(rmsf_ctx *c) {
   CX_OK(check_ctx(c, "rmsf_ctx_synchronize"));
   DeviceScope ds(c->dev);
+  // a push recorded for the slab merge still reads the caller's frames: it
+  // runs (whole) now, so the frames are free once this returns, as promised
+  CX_OK(flush_slab(c));
   CX_HIP(hipStreamSynchronize(c->stream));
   if (c->side) CX_HIP(hipStreamSynchronize(c->side));  // a shift frame's gather reads the caller's frame
   if (c->comm_stream) CX_HIP(hipStreamSynchronize(c->comm_stream));
@@ -1151,6 +1241,7 @@ RMSF_EXPORT int rmsf_ctx_kernel_time(rmsf_ctx *c, int which, int64_t *launches, 
   if (which != RMSF_TIME_ACCUMULATE && which != RMSF_TIME_SUPERPOSE)
     return fail(RMSF_EINVAL, "rmsf_ctx_kernel_time: bad kernel");
   DeviceScope ds(c->dev);
+  CX_OK(flush_slab(c));  // a recorded slab push is part of what was timed
   CX_OK(sync_streams(c));
   int64_t k = 0;
   double t = 0.0, af = 0.0;
@@ -1610,6 +1701,26 @@ RMSF_EXPORT int rmsf_multi_chan_merge_root(rmsf_ctx **cs, int n, int root) {
 
 RMSF_EXPORT int rmsf_multi_chan_merge(rmsf_ctx **cs, int n) { return rmsf_multi_chan_merge_root(cs, n, -1); }
 
+RMSF_EXPORT int rmsf_multi_chan_merge_exact(rmsf_ctx **cs, int n, int root, int order) {
+  if (!cs || n < 1) return fail(RMSF_EINVAL, "rmsf_multi_chan_merge_exact: no contexts");
+  if (root < -1 || root >= n) return fail(RMSF_EINVAL, "rmsf_multi_chan_merge_exact: root outside the contexts");
+  if (order != RMSF_MERGE_RANK && order != RMSF_MERGE_MPI4PY)
+    return fail(RMSF_EINVAL, "rmsf_multi_chan_merge_exact: unknown order");
+  for (int i = 0; i < n; ++i) {
+    CX_OK(check_ctx(cs[i], "rmsf_multi_chan_merge_exact"));
+    if (cs[i]->n_coord != cs[0]->n_coord) return fail(RMSF_EINVAL, "rmsf_multi_chan_merge_exact: contexts differ in n_sel");
+    for (int j = 0; j < i; ++j)
+      if (cs[j] == cs[i]) return fail(RMSF_EINVAL, "rmsf_multi_chan_merge_exact: a context is listed twice");
+    if (cs[i]->merged_away)
+      return fail(RMSF_EINVAL, "rmsf_multi_chan_merge_exact: a context's state was merged away (reset it first)");
+  }
+  if (!whole_group_here(cs, n))
+    return fail(RMSF_EINVAL, "rmsf_multi_chan_merge_exact: the communicator spans other processes; merge their "
+                             "rmsf_get_partial states with rmsf_chan_reduce / rmsf_chan_merge_pair over the host's "
+                             "transport");
+  return exact_merge(cs, n, root, order);
+}
+
 RMSF_EXPORT int rmsf_multi_set_transport(rmsf_ctx **cs, int n, int transport) {
   if (!cs || n < 1) return fail(RMSF_EINVAL, "rmsf_multi_set_transport: no contexts");
   if (transport != RMSF_TRANSPORT_AUTO && transport != RMSF_TRANSPORT_NOOP)
@@ -1656,6 +1767,11 @@ RMSF_EXPORT int rmsf_multi_push_frames(rmsf_ctx **cs, int n, const float *const 
   }
   return for_each_ctx(cs, n, [&](int i) -> int {
     rmsf_ctx *c = cs[i];
+    // the job runs on a worker thread whose current device is not c's: every
+    // stream, event and buffer below (side_begin, the shift frame's gather)
+    // belongs on c's device
+    DeviceScope ds(c->dev);
+    if (ds.err != hipSuccess) return fail(RMSF_EHIP, "rmsf_multi_push_frames: hipSetDevice failed");
     if (flags & RMSF_MULTI_RESET)
       CX_OK(rmsf_ctx_reset(c, (mode == RMSF_PUSH_WELFORD || mode == RMSF_PUSH_ALIGN_WELFORD ||
                                mode == RMSF_PUSH_EXACT) ? 1 : 2));
@@ -1676,7 +1792,6 @@ RMSF_EXPORT int rmsf_multi_push_frames(rmsf_ctx **cs, int n, const float *const 
     if (k >= 2 && mode == RMSF_PUSH_WELFORD && !c->d_sel() && (c->shift_set || shift_after) && nf <= kChunkFrames &&
         c->wel.n == 0 && !c->slab.on && stride >= 3 * c->n_atoms) {
       int64_t chunks = 0;
-      DeviceScope ds(c->dev);
       CX_OK(rmsf_balanced_slab_chunks(d_frames[i], stride, nf, c->n_sel, &chunks));
       if (chunks >= 2 * 3) {
         CX_OK(flush_fold(c));

@@ -724,7 +724,8 @@ __device__ __forceinline__ int64_t slice_t1(int64_t j, int64_t t_slice) {
 // FIN: also the finalise of RMSF.py:146 for an atom plan (cpl = 3: lane l is
 // atom l), rmsf[l] = sqrt((M2x + M2y + M2z) / n_total) -- k_finalize's
 // expression on the values just stored, so bit-identical to it, one launch
-// fewer.  A flat plan (cpl = 4) cannot: it writes NaN to every atom.
+// fewer.  A flat plan (cpl = 4: an atom's coordinates span two lanes) writes
+// no RMSF here; k_finalize_flat, launched after it, finalises that plan.
 template <int PACK, bool FIN = false>
 __global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ hdr,
                                                     const double *__restrict__ parts0, int64_t n_coord,
@@ -855,14 +856,7 @@ __global__ __launch_bounds__(kBlock) void k_fold_sk(const int64_t *__restrict__ 
       if (wel) acc1[j0 + x] = M[x];
     }
   }
-  if (FIN) {
-    if (cpl == 3) {
-      if (nx == 3) rmsf[l] = sqrt((M[0] + M[1] + M[2]) / n_total);
-    } else {
-      const int64_t n_sel = n_coord / 3;
-      for (int64_t a = 4 * l; a < 4 * l + 4 && a < n_sel; ++a) rmsf[a] = __builtin_nan("");
-    }
-  }
+  if (FIN && cpl == 3 && nx == 3) rmsf[l] = sqrt((M[0] + M[1] + M[2]) / n_total);
   if (PACK) {
     const double nk = acc_n + (double)pl.nf;  // frames folded in: this rank's n_k
     if (t_slice > 0) {
@@ -1372,40 +1366,131 @@ __global__ __launch_bounds__(kRefThreads) void k_ref_setup1(const float *__restr
 constexpr int kMergeGroup = 128;
 struct MergeCounts {
   double n[kMergeGroup];
+  double w[kMergeGroup];  // n1 n2 / T of the step that merges part s (RMSF.py:39), exact on the host
 };
 
-// Fold (acc) + parts[0..np) in order: second_order_moments, RMSF.py:36-41.
+// second_order_moments(S1, S2), RMSF.py:36-41, one coordinate, with the
+// script's operations in its order (the library is built without FP
+// contraction): T = n1 + n2; mu = (n1 mu1 + n2 mu2) / T;
+// M = M1 + M2 + (n1 n2 / T) (mu2 - mu1)**2.  n1, n2 are the frame counts
+// (Python ints in RMSF.py: n1 n2 is an exact integer product, then one
+// correctly rounded division -- the same as (double)(n1 n2) / T below 2^53).
+// The caller guarantees T > 0 (RMSF.py:39 raises ZeroDivisionError at T = 0).
+__device__ __forceinline__ void som(double n1, double mu1, double M1, double n1n2_over_T, double n2, double mu2,
+                                    double M2, double T, double &mu, double &M) {
+  const double d = mu2 - mu1;
+  mu = (n1 * mu1 + n2 * mu2) / T;
+  M = M1 + M2 + n1n2_over_T * (d * d);
+}
+
+// Fold (acc) + parts[0..np) in order (mpi4py's _py_reduce shape: res = S0,
+// res = op(res, S_i)): second_order_moments, RMSF.py:36-41.  first_verbatim:
+// the state starts as part 0 itself (no op applied, as the fold's first
+// element); else as (acc_n, acc) -- acc_n = 0: the empty state (0, zeros,
+// zeros) RMSF.py:119-121 gives a rank without frames.  An empty partial is
+// (0, zeros, zeros) too (its memory is not read); a merge of two empty states
+// (T = 0, where RMSF.py:39 raises) is skipped.
 __global__ __launch_bounds__(kBlock) void k_chan_merge(const double *__restrict__ acc_mean,
                                                        const double *__restrict__ acc_m2, double acc_n,
                                                        const double *__restrict__ mp,
                                                        const double *__restrict__ qp, MergeCounts cnt,
-                                                       int np, int64_t n, double *mo, double *qo) {
+                                                       int np, int first_verbatim, int64_t n, double *mo, double *qo) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= n) return;
   double n1 = acc_n, mu = 0.0, M = 0.0;
-  if (acc_n > 0) {
+  int s0 = 0;
+  if (first_verbatim) {
+    n1 = cnt.n[0];
+    if (n1 > 0) {
+      mu = mp[j];
+      M = qp[j];
+    }
+    s0 = 1;
+  } else if (acc_n > 0) {
     mu = acc_mean[j];
     M = acc_m2[j];
   }
-  for (int s = 0; s < np; ++s) {
+  for (int s = s0; s < np; ++s) {
     const double n2 = cnt.n[s];
-    if (n2 <= 0) continue;  // empty partial (Appendix B Q5)
-    const double mu2 = mp[(int64_t)s * n + j], M2 = qp[(int64_t)s * n + j];
-    if (n1 <= 0) {
-      n1 = n2;
-      mu = mu2;
-      M = M2;
-      continue;
-    }
     const double T = n1 + n2;
-    const double d = mu2 - mu;
-    const double mun = (n1 * mu + n2 * mu2) / T;
-    M = M + M2 + (n1 * n2 / T) * (d * d);
-    mu = mun;
+    if (T <= 0) continue;  // two empty states (RMSF.py:39's ZeroDivisionError)
+    double mu2 = 0.0, M2 = 0.0;
+    if (n2 > 0) {
+      mu2 = mp[(int64_t)s * n + j];
+      M2 = qp[(int64_t)s * n + j];
+    }
+    som(n1, mu, M, cnt.w[s], n2, mu2, M2, T, mu, M);
     n1 = T;
   }
   mo[j] = mu;
   qo[j] = M;
+}
+
+// A reduction schedule of second_order_moments steps over the partials, run
+// in place: step i is S[dst] = op(S[dst], S[src]) with the host-known counts
+// (n_dst, n_src) of that moment.  Every thread owns one coordinate of every
+// partial and walks the steps in order (no cross-thread dependence); the
+// partials' memory is the schedule's working storage, as each mpi4py rank's
+// `result` is (parts of empty states are not read).  last: write S[0] to
+// (mo, qo) after the steps.
+constexpr int kMaxSteps = 96;
+struct ChanSteps {
+  int dst[kMaxSteps], src[kMaxSteps];
+  double n1[kMaxSteps], n2[kMaxSteps], w[kMaxSteps];
+};
+
+__global__ __launch_bounds__(kBlock) void k_chan_steps(double *mp, double *qp, ChanSteps st, int n_steps,
+                                                       double n0_final, int64_t n, double *mo, double *qo) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  for (int i = 0; i < n_steps; ++i) {
+    const double n1 = st.n1[i], n2 = st.n2[i], T = n1 + n2;
+    const int64_t a = (int64_t)st.dst[i] * n + j, b = (int64_t)st.src[i] * n + j;
+    double mu1 = 0.0, M1 = 0.0, mu2 = 0.0, M2 = 0.0;
+    if (n1 > 0) {
+      mu1 = mp[a];
+      M1 = qp[a];
+    }
+    if (n2 > 0) {
+      mu2 = mp[b];
+      M2 = qp[b];
+    }
+    double mu, M;
+    som(n1, mu1, M1, st.w[i], n2, mu2, M2, T, mu, M);
+    mp[a] = mu;
+    qp[a] = M;
+  }
+  if (mo) {
+    double mu = 0.0, M = 0.0;
+    if (n0_final > 0) {
+      mu = mp[j];
+      M = qp[j];
+    }
+    mo[j] = mu;
+    qo[j] = M;
+  }
+}
+
+// S1 = op(S1, S2) in place, two separate buffers (one pairwise step of a
+// distributed reduction: S2 just arrived from another rank or device).
+__global__ __launch_bounds__(kBlock) void k_chan_pair(double *m1, double *q1, const double *__restrict__ m2,
+                                                      const double *__restrict__ q2, double n1, double n2, double w,
+                                                      int64_t n) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  double mu1 = 0.0, M1 = 0.0, mu2 = 0.0, M2 = 0.0;
+  if (n1 > 0) {
+    mu1 = m1[j];
+    M1 = q1[j];
+  }
+  if (n2 > 0) {
+    mu2 = m2[j];
+    M2 = q2[j];
+  }
+  double mu, M;
+  som(n1, mu1, M1, w, n2, mu2, M2, n1 + n2, mu, M);
+  m1[j] = mu;
+  q1[j] = M;
 }
 
 __global__ __launch_bounds__(kBlock) void k_sum_splits(const double *__restrict__ parts, int np, int64_t n,
@@ -1497,6 +1582,19 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const double *__restrict__ 
   const int64_t a = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (a >= n_sel) return;
   out[a] = sqrt((m2[3 * a] + m2[3 * a + 1] + m2[3 * a + 2]) / nf);
+}
+
+// k_finalize behind rmsf_fold_balanced_finalize for the plan the workspace
+// header names: a flat plan (hdr[6] = 4 coordinates per lane, whose fold
+// cannot finalise per lane) is finalised here from the M2 the fold just
+// stored; an atom plan (finalised in the fold) leaves at once.  The decision
+// is the workspace's own, read on the device -- no host record of plans.
+__global__ __launch_bounds__(kBlock) void k_finalize_flat(const int64_t *__restrict__ hdr,
+                                                          const double *__restrict__ m2, int64_t n_sel, double nf,
+                                                          double *__restrict__ out) {
+  if (hdr[6] != 4) return;
+  for (int64_t a = (int64_t)blockIdx.x * kBlock + threadIdx.x; a < n_sel; a += (int64_t)gridDim.x * kBlock)
+    out[a] = sqrt((m2[3 * a] + m2[3 * a + 1] + m2[3 * a + 2]) / nf);
 }
 
 __global__ __launch_bounds__(kBlock) void k_qcp_batch(const double *__restrict__ A, const double *__restrict__ E0,
@@ -1598,6 +1696,18 @@ __global__ __launch_bounds__(kBlock) void k_planes_to_rows(const double *__restr
   if (i >= 3 * n) return;
   const int64_t a = i / 3, c = i - 3 * a;
   dst[i] = src[c * n + a];
+}
+
+// The generator's per-atom noise scale sigma(a) (k_synth's expression): the
+// expected RMSF of an unaligned synthetic atom is sqrt(3) sigma(a), the
+// reference figure of the bench's sanity check (rmsf_amd.synth).
+__global__ __launch_bounds__(kBlock) void k_synth_sigma(double *__restrict__ out, int64_t a0, int64_t n,
+                                                        uint64_t seed) {
+#pragma clang fp contract(off)
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const double two53 = 1.1102230246251565e-16;  // 2^-53
+  out[i] = 0.2 + (double)(skey(seed, 2, (uint64_t)(a0 + i), 0) >> 11) * two53 * 1.8;
 }
 
 __global__ __launch_bounds__(kBlock) void k_synth(float *__restrict__ out, int64_t fstride, int64_t n_atoms,
@@ -2065,23 +2175,34 @@ int fold_shift_launch(const int64_t *hdr, const double *p0, int64_t n_coord, int
   return after_launch("k_fold_sk");
 }
 
-// The layout (coordinates per lane) of the plan each balanced accumulate last
-// wrote into a workspace, kept on the host: the plan header itself is in HBM,
-// and rmsf_fold_balanced_finalize must refuse a flat (4 per lane) plan, which
-// cannot finalise in the fold, instead of writing NaN with RMSF_OK.
-std::mutex g_plan_mu;
-std::unordered_map<const void *, int> g_plan_cpl;
-
-void note_plan(const void *d_work, int cpl) {
-  std::lock_guard<std::mutex> lk(g_plan_mu);
-  if (g_plan_cpl.size() > 4096) g_plan_cpl.clear();  // freed workspaces: forget them all
-  g_plan_cpl[d_work] = cpl;
+// n1 n2 / T of RMSF.py:39 (`S1[0] * S2[0]/T`: an exact integer product, one
+// correctly rounded division -- exact as computed here while n1 n2 < 2^53);
+// 0 for T = 0, a step that is never launched.
+double merge_weight(int64_t n1, int64_t n2) {
+  const int64_t T = n1 + n2;
+  return T > 0 ? (double)(n1 * n2) / (double)T : 0.0;
 }
 
-int plan_cpl(const void *d_work) {  // 0 = not written by this library's accumulate
-  std::lock_guard<std::mutex> lk(g_plan_mu);
-  const auto it = g_plan_cpl.find(d_work);
-  return it == g_plan_cpl.end() ? 0 : it->second;
+// The order in which RMSF.py:143's comm.reduce(S, op=second_order_moments)
+// applies its op over the ranks' partials, as (dst, src) steps
+// S[dst] = op(S[dst], S[src]); S[0] is the result.
+//   RMSF_MERGE_MPI4PY: mpi4py's object reduce with rc.fast_reduce (its
+//     default) -- PyMPI_reduce_p2p's binomial tree: for mask = 1, 2, 4, ...
+//     rank r with r % (2 mask) == 0 receives S[r + mask] (if that rank
+//     exists) and computes op(result, received); ranks with the mask bit set
+//     send and stop.  (mpi4py is upstream, not vendored here: restated from
+//     its published source, unverified in this container.)
+//   RMSF_MERGE_RANK: res = S0, res = op(res, S_i) for i = 1..P-1 -- mpi4py's
+//     naive reduce (rc.fast_reduce = False: a gather, then _py_reduce).
+std::vector<std::pair<int, int>> reduce_schedule(int n_parts, int order) {
+  std::vector<std::pair<int, int>> st;
+  if (order == RMSF_MERGE_RANK) {
+    for (int i = 1; i < n_parts; ++i) st.push_back({0, i});
+    return st;
+  }
+  for (int64_t mask = 1; mask < n_parts; mask <<= 1)
+    for (int64_t r = 0; r + mask < n_parts; r += 2 * mask) st.push_back({(int)r, (int)(r + mask)});
+  return st;
 }
 
 }  // namespace
@@ -2116,11 +2237,9 @@ RMSF_EXPORT int rmsf_accumulate_balanced(const float *d_xyz, int64_t fstride, in
     if (work_bytes < sk_bytes(pl, two)) return fail(RMSF_ENOMEM, "rmsf_accumulate_balanced: workspace too small");
     double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
     double *p1 = p0 + (size_t)pl.G * pl.P * kBlock * 4;
-    note_plan(d_work, 4);
     hipLaunchKernelGGL((k_welford_flat_sk<4>), dim3(pl.G), dim3(kBlock), 0, s, d_xyz, fstride / 4, pl, hdr, p0, p1);
     return after_launch("k_welford_flat_sk");
   }
-  note_plan(d_work, 3);
   const bool g = d_sel != nullptr, al = d_xform != nullptr;
   const bool split = al && RMSF_SHIFTED_SUMS;  // aligned: the frame-split kernel
   const int per_cu = !al ? kSkPerCuAtoms : !split ? kSkPerCuAligned : two ? kSkPerCuSplitWel : kSkPerCuSplitSum;
@@ -2178,7 +2297,6 @@ RMSF_EXPORT int rmsf_accumulate_balanced_planes(const float *d_xyz, int64_t fstr
   int64_t *hdr = static_cast<int64_t *>(d_work);
   double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
   double *p1 = two ? p0 + (size_t)pl.G * pl.P * kBlock * 3 : nullptr;
-  note_plan(d_work, 3);
   if (!d_xform) {  // unaligned: one atom per lane (k_accum_atoms_sk), the row form's kernel for a selection
 #define SK_LAUNCH(M_, G_) \
   hipLaunchKernelGGL((k_accum_atoms_sk<M_, false, G_, 4, true>), dim3(pl.G), dim3(kBlock), 0, s, d_xyz, fstride, d_sel, nullptr, nullptr, pl, hdr, p0, p1, pstride)
@@ -2225,16 +2343,18 @@ RMSF_EXPORT int rmsf_fold_balanced_finalize(const void *d_work, int64_t n_coord,
                                             double *d_acc1, int64_t n_total, double *d_rmsf, void *stream) {
   if (!d_work || !d_acc0 || !d_acc1 || !d_rmsf || n_coord < 3 || n_coord % 3 != 0 || acc_n < 0 || n_total < 1)
     return fail(RMSF_EINVAL, "rmsf_fold_balanced_finalize: bad arguments");
-  if (plan_cpl(d_work) == 4)
-    return fail(RMSF_EINVAL,
-                "rmsf_fold_balanced_finalize: the workspace holds a flat (4 coordinates per lane) plan, which cannot "
-                "finalise in the fold; call rmsf_fold_balanced + rmsf_finalize");
   const int64_t *hdr = static_cast<const int64_t *>(d_work);
   const double *p0 = reinterpret_cast<const double *>(hdr + kSkHdr);
   hipLaunchKernelGGL((k_fold_sk<0, true>), dim3(grid1((n_coord + 2) / 3)), dim3(kBlock), 0, S(stream), hdr, p0,
                      n_coord, (double)acc_n, d_acc0, d_acc1, nullptr, nullptr, nullptr, (int64_t)0, INT64_MAX, n_coord,
                      (int64_t)0, d_rmsf, (double)n_total);
-  return after_launch("k_fold_sk<FIN>");
+  int rc = after_launch("k_fold_sk<FIN>");
+  if (rc) return rc;
+  // the workspace's plan decides on the device (hdr[6]); an atom plan exits here
+  const int64_t n_sel = n_coord / 3;
+  hipLaunchKernelGGL(k_finalize_flat, dim3((unsigned)std::min<int64_t>(grid1(n_sel), 1024)), dim3(kBlock), 0,
+                     S(stream), hdr, d_acc1, n_sel, (double)n_total, d_rmsf);
+  return after_launch("k_finalize_flat");
 }
 
 RMSF_EXPORT int rmsf_fold_balanced_shift(const void *d_work, int64_t n_coord, int64_t acc_n, double *d_acc0,
@@ -2288,7 +2408,6 @@ RMSF_EXPORT int rmsf_accumulate_balanced_slab(const float *d_xyz, int64_t fstrid
   int64_t *hdr = static_cast<int64_t *>(d_work);
   double *p0 = reinterpret_cast<double *>(hdr + kSkHdr);
   double *p1 = p0 + (size_t)pl.G * pl.P * kBlock * 4;
-  note_plan(d_work, 4);
   hipLaunchKernelGGL((k_welford_flat_sk<4>), dim3((unsigned)(pl.Cs * pl.S)), dim3(kBlock), 0, S(stream), d_xyz,
                      fstride / 4, pl, hdr, p0, p1);
   return after_launch("k_welford_flat_sk");
@@ -2321,18 +2440,96 @@ RMSF_EXPORT int rmsf_chan_merge(const double *d_mean_parts, const double *d_m2_p
   }
   if (total == 0) return fail(RMSF_EEMPTY, "rmsf_chan_merge: every partial is empty (no frames)");
   hipStream_t s = S(stream);
-  double acc_n = 0.0;
+  int64_t acc_n = 0;
   for (int g0 = 0; g0 < n_parts; g0 += kMergeGroup) {
     const int np = std::min(kMergeGroup, n_parts - g0);
     MergeCounts c{};
-    for (int i = 0; i < np; ++i) c.n[i] = (double)h_counts[g0 + i];
-    hipLaunchKernelGGL(k_chan_merge, dim3(grid1(n_coord)), dim3(kBlock), 0, s, d_mean, d_m2, acc_n,
-                       d_mean_parts + (int64_t)g0 * n_coord, d_m2_parts + (int64_t)g0 * n_coord, c, np, n_coord,
-                       d_mean, d_m2);
+    int64_t run = acc_n;  // the running count before part g0 + i
+    for (int i = 0; i < np; ++i) {
+      const int64_t n2 = h_counts[g0 + i];
+      c.n[i] = (double)n2;
+      c.w[i] = merge_weight(run, n2);
+      run = (g0 == 0 && i == 0) ? n2 : run + n2;
+    }
+    hipLaunchKernelGGL(k_chan_merge, dim3(grid1(n_coord)), dim3(kBlock), 0, s, d_mean, d_m2, (double)acc_n,
+                       d_mean_parts + (int64_t)g0 * n_coord, d_m2_parts + (int64_t)g0 * n_coord, c, np,
+                       g0 == 0 ? 1 : 0, n_coord, d_mean, d_m2);
     int rc = after_launch("k_chan_merge");
     if (rc) return rc;
-    for (int i = 0; i < np; ++i) acc_n += (double)h_counts[g0 + i];
+    acc_n = run;
   }
+  return RMSF_OK;
+}
+
+RMSF_EXPORT int rmsf_chan_merge_pair(double *d_mean1, double *d_m21, int64_t n1, const double *d_mean2,
+                                     const double *d_m22, int64_t n2, int64_t n_coord, void *stream) {
+  if (!d_mean1 || !d_m21 || !d_mean2 || !d_m22 || n1 < 0 || n2 < 0 || n_coord < 1)
+    return fail(RMSF_EINVAL, "rmsf_chan_merge_pair: bad arguments");
+  if (n1 + n2 == 0)
+    return fail(RMSF_EEMPTY, "rmsf_chan_merge_pair: both partials are empty (RMSF.py:39 ZeroDivisionError)");
+  hipLaunchKernelGGL(k_chan_pair, dim3(grid1(n_coord)), dim3(kBlock), 0, S(stream), d_mean1, d_m21, d_mean2, d_m22,
+                     (double)n1, (double)n2, merge_weight(n1, n2), n_coord);
+  return after_launch("k_chan_pair");
+}
+
+RMSF_EXPORT int rmsf_chan_reduce_steps(int n_parts, int order, int *h_dst, int *h_src, int capacity) {
+  if (n_parts < 1 || (order != RMSF_MERGE_RANK && order != RMSF_MERGE_MPI4PY) || capacity < 0)
+    return fail(RMSF_EINVAL, "rmsf_chan_reduce_steps: bad arguments");
+  const std::vector<std::pair<int, int>> st = reduce_schedule(n_parts, order);
+  if ((h_dst || h_src) && capacity < (int)st.size())
+    return fail(RMSF_EINVAL, "rmsf_chan_reduce_steps: capacity below n_parts - 1");
+  for (size_t i = 0; i < st.size() && (h_dst || h_src); ++i) {
+    if (h_dst) h_dst[i] = st[i].first;
+    if (h_src) h_src[i] = st[i].second;
+  }
+  return (int)st.size();
+}
+
+RMSF_EXPORT int rmsf_chan_reduce(double *d_mean_parts, double *d_m2_parts, const int64_t *h_counts, int n_parts,
+                                 int64_t n_coord, int order, double *d_mean, double *d_m2, void *stream) {
+  if (!d_mean_parts || !d_m2_parts || !h_counts || n_parts < 1 || n_coord < 1 || !d_mean || !d_m2 ||
+      (order != RMSF_MERGE_RANK && order != RMSF_MERGE_MPI4PY))
+    return fail(RMSF_EINVAL, "rmsf_chan_reduce: bad arguments");
+  std::vector<int64_t> cnt(h_counts, h_counts + n_parts);
+  int64_t total = 0;
+  for (int64_t v : cnt) {
+    if (v < 0) return fail(RMSF_EINVAL, "rmsf_chan_reduce: negative count");
+    total += v;
+  }
+  if (total == 0) return fail(RMSF_EEMPTY, "rmsf_chan_reduce: every partial is empty (no frames)");
+  // the schedule with its counts, on the host; T = 0 steps (two empty
+  // states, where RMSF.py:39 raises) are dropped: their dst stays empty
+  const std::vector<std::pair<int, int>> sched = reduce_schedule(n_parts, order);
+  std::vector<std::pair<int, int>> keep;
+  std::vector<int64_t> n1s, n2s;
+  for (const auto &p : sched) {
+    const int64_t a = cnt[p.first], b = cnt[p.second];
+    if (a + b == 0) continue;
+    keep.push_back(p);
+    n1s.push_back(a);
+    n2s.push_back(b);
+    cnt[p.first] = a + b;
+  }
+  hipStream_t s = S(stream);
+  const size_t ns = keep.size();
+  size_t i0 = 0;
+  do {
+    const int k = (int)std::min<size_t>(kMaxSteps, ns - i0);
+    ChanSteps st{};
+    for (int i = 0; i < k; ++i) {
+      st.dst[i] = keep[i0 + i].first;
+      st.src[i] = keep[i0 + i].second;
+      st.n1[i] = (double)n1s[i0 + i];
+      st.n2[i] = (double)n2s[i0 + i];
+      st.w[i] = merge_weight(n1s[i0 + i], n2s[i0 + i]);
+    }
+    const bool last = i0 + k >= ns;
+    hipLaunchKernelGGL(k_chan_steps, dim3(grid1(n_coord)), dim3(kBlock), 0, s, d_mean_parts, d_m2_parts, st, k,
+                       (double)cnt[0], n_coord, last ? d_mean : nullptr, last ? d_m2 : nullptr);
+    const int rc = after_launch("k_chan_steps");
+    if (rc) return rc;
+    i0 += k;
+  } while (i0 < ns);
   return RMSF_OK;
 }
 
@@ -2538,6 +2735,12 @@ RMSF_EXPORT int rmsf_planes_to_rows(const double *d_src, int64_t n, double *d_ds
   if (!d_src || !d_dst || n < 1 || d_src == d_dst) return fail(RMSF_EINVAL, "rmsf_planes_to_rows: bad arguments");
   hipLaunchKernelGGL(k_planes_to_rows, dim3(grid1(3 * n)), dim3(kBlock), 0, S(stream), d_src, n, d_dst);
   return after_launch("k_planes_to_rows");
+}
+
+RMSF_EXPORT int rmsf_synth_sigma(double *d_sigma, int64_t a0, int64_t n, uint64_t seed, void *stream) {
+  if (!d_sigma || a0 < 0 || n < 1) return fail(RMSF_EINVAL, "rmsf_synth_sigma: bad arguments");
+  hipLaunchKernelGGL(k_synth_sigma, dim3(grid1(n)), dim3(kBlock), 0, S(stream), d_sigma, a0, n, seed);
+  return after_launch("k_synth_sigma");
 }
 
 RMSF_EXPORT int rmsf_synth_frames(float *d_out, int64_t fstride, int64_t n_atoms, int64_t f0, int64_t nf,

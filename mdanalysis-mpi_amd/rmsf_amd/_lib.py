@@ -68,6 +68,9 @@ SIGNATURES = {
     "rmsf_accumulate_balanced_planes": (c_int, [P, c_int64, c_int64, c_int64, c_int64, P, P, P, c_int, c_int, P,
                                                 c_size_t, P]),
     "rmsf_chan_merge": (c_int, [P, P, P, c_int, c_int64, P, P, P]),
+    "rmsf_chan_reduce_steps": (c_int, [c_int, c_int, P, P, c_int]),
+    "rmsf_chan_reduce": (c_int, [P, P, P, c_int, c_int64, c_int, P, P, P]),
+    "rmsf_chan_merge_pair": (c_int, [P, P, c_int64, P, P, c_int64, c_int64, P]),
     "rmsf_sum_splits": (c_int, [P, c_int, c_int64, P, P]),
     "rmsf_divide": (c_int, [P, c_double, c_int64, P, P]),
     "rmsf_chan_weight": (c_int, [P, c_double, c_int64, P, P]),
@@ -87,6 +90,7 @@ SIGNATURES = {
     "rmsf_qcp_batch": (c_int, [P, P, P, c_int64, P, P, P]),
     "rmsf_calc_rmsd_rotational_matrix": (c_int, [P, P, c_int64, P, P, POINTER(c_double)]),
     "rmsf_synth_frames": (c_int, [P, c_int64, c_int64, c_int64, c_int64, c_uint64, P, P]),
+    "rmsf_synth_sigma": (c_int, [P, c_int64, c_int64, c_uint64, P]),
     "rmsf_gather_frames": (c_int, [P, c_int64, P, c_int64, c_int64, P, P, P]),
     "rmsf_gather_planes": (c_int, [P, c_int64, c_int64, P, c_int64, c_int64, P, P, P]),
     "rmsf_planes_to_rows": (c_int, [P, c_int64, P, P]),
@@ -147,6 +151,7 @@ SIGNATURES = {
     "rmsf_multi_chan_merge": (c_int, [P, c_int]),
     "rmsf_set_merge_shift_frame": (c_int, [P, P, c_int]),
     "rmsf_multi_chan_merge_root": (c_int, [P, c_int, c_int]),
+    "rmsf_multi_chan_merge_exact": (c_int, [P, c_int, c_int, c_int]),
     "rmsf_multi_push_frames": (c_int, [P, c_int, P, P, c_int64, c_int, c_int, P, P, c_int]),
     "rmsf_multi_set_transport": (c_int, [P, c_int, c_int]),
 }
@@ -158,6 +163,31 @@ RMSF_UNIQUE_ID_BYTES = 128
 RMSF_TIME_ACCUMULATE, RMSF_TIME_SUPERPOSE = 0, 1
 RMSF_MULTI_RESET = 1
 RMSF_TRANSPORT_AUTO, RMSF_TRANSPORT_NOOP = 0, 1
+RMSF_MERGE_RANK, RMSF_MERGE_MPI4PY = 0, 1
+MERGE_ORDERS = {"rank": RMSF_MERGE_RANK, "mpi4py": RMSF_MERGE_MPI4PY}
+
+
+def merge_order(order) -> int:
+    """``"mpi4py"`` (RMSF.py:143's comm.reduce: mpi4py's default binomial
+    tree) or ``"rank"`` (rank order) -> the ABI's RMSF_MERGE_* value."""
+    if isinstance(order, int) and order in MERGE_ORDERS.values():
+        return order
+    try:
+        return MERGE_ORDERS[order]
+    except (KeyError, TypeError):
+        raise ValueError(f"merge_order must be one of {sorted(MERGE_ORDERS)}, got {order!r}") from None
+
+
+def reduce_steps(n_parts: int, order="mpi4py") -> list[tuple[int, int]]:
+    """The (dst, src) steps S[dst] = op(S[dst], S[src]) of the reduction
+    (rmsf_chan_reduce_steps; host-only, no device needed)."""
+    lib = load()
+    o = merge_order(order)
+    k = lib.rmsf_chan_reduce_steps(int(n_parts), o, None, None, 0)
+    check(min(k, 0), "rmsf_chan_reduce_steps")
+    d, s = (c_int * max(k, 1))(), (c_int * max(k, 1))()
+    lib.rmsf_chan_reduce_steps(int(n_parts), o, d, s, k)
+    return [(d[i], s[i]) for i in range(k)]
 
 _lib = None
 

@@ -362,6 +362,18 @@ class Context:
         call("rmsf_multi_chan_merge_root", h, n, -1 if root is None else int(root))
 
     @staticmethod
+    def multi_chan_merge_exact(ctxs, root: int | None = None, order="mpi4py") -> None:
+        """RMSF.py:141-143 as the script computes it, over contexts holding
+        ranks' exact states (PUSH_EXACT; context i = rank i): the states are
+        reduced with second_order_moments in ``order`` ("mpi4py": comm.reduce's
+        default binomial tree; "rank": rank order), device to device (peer
+        copies, rmsf_multi_chan_merge_exact) -- bit for bit with RMSF.py:143.
+        root=None: every context gets the result; root=r: context r only."""
+        from ._lib import merge_order
+        h, n = Context._handles(ctxs)
+        call("rmsf_multi_chan_merge_exact", h, n, -1 if root is None else int(root), merge_order(order))
+
+    @staticmethod
     def multi_set_transport(ctxs, transport: int) -> None:
         """TRANSPORT_AUTO (RCCL / host fold) or TRANSPORT_NOOP (timing
         rehearsal: the exchanges move nothing, results are not global)."""

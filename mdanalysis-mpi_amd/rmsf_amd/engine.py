@@ -192,6 +192,25 @@ class Engine:
         call("rmsf_chan_merge", mean_parts.data_ptr(), m2_parts.data_ptr(), ctypes.cast(c, ctypes.c_void_p),
              len(counts), n_coord, mean_out.data_ptr(), m2_out.data_ptr(), self.stream)
 
+    def chan_reduce(self, mean_parts: torch.Tensor, m2_parts: torch.Tensor, counts, n_coord: int,
+                    mean_out: torch.Tensor, m2_out: torch.Tensor, order="mpi4py") -> None:
+        """RMSF.py:143's comm.reduce of the partials (rank order in the rows)
+        with second_order_moments in ``order`` ("mpi4py": mpi4py's default
+        binomial tree; "rank": rank order).  The parts are overwritten (the
+        schedule's working storage)."""
+        c = _lib.i64p(counts)
+        call("rmsf_chan_reduce", mean_parts.data_ptr(), m2_parts.data_ptr(), ctypes.cast(c, ctypes.c_void_p),
+             len(counts), n_coord, _lib.merge_order(order), mean_out.data_ptr(), m2_out.data_ptr(), self.stream)
+
+    def chan_merge_pair(self, mean1: torch.Tensor, m21: torch.Tensor, n1: int, mean2: torch.Tensor,
+                        m22: torch.Tensor, n2: int) -> None:
+        """(mean1, m21) = second_order_moments((n1, mean1, m21), (n2, mean2, m22)) in place."""
+        n = mean1.numel()
+        if m21.numel() != n or mean2.numel() != n or m22.numel() != n:
+            raise ValueError("chan_merge_pair: buffer sizes")
+        call("rmsf_chan_merge_pair", mean1.data_ptr(), m21.data_ptr(), int(n1), mean2.data_ptr(), m22.data_ptr(),
+             int(n2), n, self.stream)
+
     def sum_splits(self, parts: torch.Tensor, n_parts: int, n: int, out: torch.Tensor) -> None:
         call("rmsf_sum_splits", parts.data_ptr(), n_parts, n, out.data_ptr(), self.stream)
 

@@ -345,31 +345,23 @@ def _set_frame(c: Context, fr, setter: str) -> None:
         getattr(c, setter)(fr)
 
 
-def _exact_merge(ctxs, home_dev) -> dict:
+def _exact_merge(ctxs, root: int, order: str) -> dict:
     """RMSF.py:141-146 for exact=True: the contexts' states (each a block's S
-    of RMSF.py:140) folded in device order by k_chan_merge (RMSF.py:36-41
-    bit for bit) on ``home_dev``, then RMSF.py:146."""
-    import torch
-
-    from .engine import Engine
-    parts = [c.partial() for c in ctxs]
-    n_coord = parts[0][1].size
-    eng = Engine(torch.device("cuda", home_dev))
-    with torch.cuda.device(eng.device):
-        means = torch.tensor(np.stack([p[1].reshape(-1) for p in parts]), device=eng.device)
-        m2s = torch.tensor(np.stack([p[2].reshape(-1) for p in parts]), device=eng.device)
-        mean, m2, rmsf = eng.empty(n_coord), eng.empty(n_coord), eng.empty(n_coord // 3)
-        counts = [int(p[0]) for p in parts]
-        eng.chan_merge(means, m2s, counts, n_coord, mean, m2)
-        eng.finalize(m2, n_coord // 3, sum(counts), rmsf)
-        torch.cuda.current_stream(eng.device).synchronize()
-        return dict(rmsf=rmsf.cpu().numpy(), mean=mean.cpu().numpy().reshape(-1, 3),
-                    sumsquares=m2.cpu().numpy().reshape(-1, 3), n_frames=sum(counts))
+    of RMSF.py:140) reduced with second_order_moments (RMSF.py:36-41 bit for
+    bit) in RMSF.py:143's comm.reduce order, device to device
+    (rmsf_multi_chan_merge_exact: each step's state crosses xGMI by a peer
+    copy and merges on the receiving device), to context ``root``; then
+    RMSF.py:146 there."""
+    Context.multi_chan_merge_exact(ctxs, root=root, order=order)
+    home = ctxs[root]
+    n, mean, m2 = home.partial()
+    return dict(rmsf=home.rmsf(), mean=mean, sumsquares=m2, n_frames=n)
 
 
 def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int = 0, start=None, stop=None,
               step=None, batch_frames: int | None = None, frames=None, collect_rmsd: bool = False,
-              layout: str = "fac", merge_root: int | None = None, exact: bool = False) -> dict:
+              layout: str = "fac", merge_root: int | None = None, exact: bool = False,
+              merge_order: str = "mpi4py") -> dict:
     """RMSF.py's computation over the devices ``gpus`` from one process.
     Returns the ``results`` fields (rmsf, mean, sumsquares, n_frames, ...;
     ``rmsd`` with ``collect_rmsd``: per-frame QCP rmsd of the last sweep in
@@ -378,8 +370,11 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
     and the results are read from it; None = an all-reduce, read from
     device index 0 (the same numbers).  ``exact`` (align=None): every
     device runs RMSF.py:137-138's recurrence over its block (RMSF_PUSH_EXACT)
-    and the blocks are folded in device order by second_order_moments
-    (k_chan_merge on the home device): the script's arithmetic bit for bit."""
+    and the blocks are reduced by second_order_moments in ``merge_order``
+    (RMSF.py:143's comm.reduce: "mpi4py", its default binomial tree, or
+    "rank"), device to device: the script's arithmetic bit for bit."""
+    from ._lib import merge_order as _order
+    _order(merge_order)
     if exact and align is not None:
         raise NotImplementedError("exact=True covers align=None (RMSF.py:120-146 on an aligned trajectory)")
     if align not in (None, "frame0", "average"):
@@ -510,8 +505,8 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
         else:
             each(lambda i: push(i, last))
         if exact:
-            out.update(_exact_merge(ctxs, devs[merge_root or 0]), blocks=[(int(b0), int(b1)) for b0, b1 in spans],
-                       devices=devs)
+            out.update(_exact_merge(ctxs, merge_root or 0, merge_order),
+                       blocks=[(int(b0), int(b1)) for b0, b1 in spans], devices=devs, merge_order=merge_order)
             return out
         Context.multi_chan_merge(ctxs, root=merge_root)
         home = ctxs[merge_root or 0]

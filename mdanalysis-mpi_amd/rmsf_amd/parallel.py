@@ -199,27 +199,100 @@ def all_gather_(t: torch.Tensor) -> torch.Tensor:
     return out.to(t.device) if staged else out
 
 
-def global_chan_exact(ops, mean_k: torch.Tensor, m2_k: torch.Tensor, counts: list[int], root: int | None = None):
-    """RMSF.py:141-143 with second_order_moments' own arithmetic: every
-    rank's (mean_k, M2_k) gathered, then folded in rank order by
-    k_chan_merge (RMSF.py:36-41 bit for bit; ``counts`` = the ranks' frame
-    counts, RMSF.py:65-69's blocks).  MPI may combine a commutative
-    user-defined reduce in any order; rank order is the canonical one (the
-    oracle's chan_fold).  ``root``: the result on that rank only (None
-    elsewhere), as comm.reduce(root=0); None: on every rank (all-gather).
-    Returns (mean, M2) or (None, None)."""
+def _send(t: torch.Tensor, dst: int) -> None:
+    dist.send(t.cpu() if _staged(t) else t, dst)
+
+
+def _recv(like: torch.Tensor, src: int) -> torch.Tensor:
+    if _staged(like):
+        h = torch.empty(like.shape, dtype=like.dtype)
+        dist.recv(h, src)
+        return h.to(like.device)
+    t = torch.empty_like(like)
+    dist.recv(t, src)
+    return t
+
+
+MERGE_ORDERS = ("mpi4py", "rank")
+
+
+def global_chan_exact(ops, mean_k: torch.Tensor, m2_k: torch.Tensor, counts: list[int], root: int | None = None,
+                      order: str = "mpi4py"):
+    """RMSF.py:141-143 with second_order_moments' own arithmetic (the
+    device's k_chan_pair / k_chan_merge: RMSF.py:36-41 bit for bit), applied
+    in the order RMSF.py:143's ``comm.reduce(S, root=0, op=...)`` applies it.
+    ``counts`` = the ranks' frame counts (RMSF.py:65-69's blocks).
+
+    ``order="mpi4py"`` (default): mpi4py's object reduce as it runs by default
+    (``rc.fast_reduce``: PyMPI_reduce_p2p, upstream, unverified here) --
+    point to point, a binomial tree: for mask = 1, 2, 4, ... a rank with the
+    mask bit set sends its result (mean | M2) to ``rank & ~mask`` and stops;
+    the others receive from ``rank | mask`` and compute op(result, received)
+    on the device.  ``order="rank"``: mpi4py's naive reduce
+    (``rc.fast_reduce = False``): every S gathered, folded in rank order.
+    The two coincide up to 3 ranks and differ in the last bits from 4.
+
+    ``root``: the result on that rank only (None elsewhere), as
+    comm.reduce(root=...); None: on every rank.  Returns (mean, M2) or
+    (None, None).  Merges of two empty states (T = 0, where RMSF.py:39
+    raises) are skipped."""
+    if order not in MERGE_ORDERS:
+        raise ValueError(f"merge order must be one of {MERGE_ORDERS}, got {order!r}")
     rank, size = world()
     if size == 1:
         return mean_k, m2_k
+    counts = [int(c) for c in counts]
+    if len(counts) != size:
+        raise ValueError("global_chan_exact: one frame count per rank expected")
+    if sum(counts) == 0:
+        raise ZeroDivisionError("global_chan_exact: no frames on any rank")
     n = mean_k.numel()
-    both = torch.cat([mean_k.reshape(-1), m2_k.reshape(-1)])
-    g = all_gather_(both) if root is None else gather_(both, root)
-    if g is None:
+    if order == "rank":
+        both = torch.cat([mean_k.reshape(-1), m2_k.reshape(-1)])
+        g = all_gather_(both) if root is None else gather_(both, root)
+        if g is None:
+            return None, None
+        g = g.view(size, 2, n)
+        mean, m2 = torch.empty_like(mean_k), torch.empty_like(m2_k)
+        ops.chan_merge(g[:, 0].contiguous(), g[:, 1].contiguous(), counts, n, mean, m2)
+        return mean, m2
+    # the binomial tree, each rank's `result` in its own buffer
+    res = torch.cat([mean_k.reshape(-1), m2_k.reshape(-1)])
+    have = counts[rank]
+    mask = 1
+    while mask < size:
+        if rank & mask:
+            _send(res, rank & ~mask)
+            res = None
+            break
+        src = rank | mask
+        if src < size:
+            got = _recv(res, src)
+            n_src = sum(counts[src:min(src + mask, size)])   # the frames of src's subtree
+            if have + n_src > 0:
+                ops.chan_merge_pair(res[:n], res[n:], have, got[:n], got[n:], n_src)
+            have += n_src
+        mask <<= 1
+    # rank 0 holds comm.reduce's result: forward it to root (as mpi4py does),
+    # or to every rank (root=None)
+    if root is None:
+        if res is None:
+            res = torch.empty(2 * n, dtype=mean_k.dtype, device=mean_k.device)
+        if _staged(res):
+            h = res.cpu()
+            dist.broadcast(h, 0)
+            res = h.to(mean_k.device)
+        else:
+            dist.broadcast(res, 0)
+    elif root != 0:
+        if rank == 0:
+            _send(res, root)
+            res = None
+        elif rank == root:
+            res = _recv(torch.empty(2 * n, dtype=mean_k.dtype, device=mean_k.device), 0)
+    if res is None or (root is not None and rank != root):
         return None, None
-    g = g.view(size, 2, n)
-    mean, m2 = torch.empty_like(mean_k), torch.empty_like(m2_k)
-    ops.chan_merge(g[:, 0].contiguous(), g[:, 1].contiguous(), [int(c) for c in counts], n, mean, m2)
-    return mean, m2
+    return res[:n].clone(), res[n:].clone()
 
 
 def global_chan_scatter(ops, mean_k: torch.Tensor, m2_k: torch.Tensor, n_k: int, n_total: int, shift: torch.Tensor,

@@ -346,7 +346,7 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                  ref_owner: int | None = None, block: tuple[int, int] | None = None,
                  timer: KernelTimer | None = None, collect_transforms: bool = False,
                  merge_slabs: int | None = None, merge_root: int | None = None,
-                 merge_scatter: bool = False, exact: bool = False) -> PipelineResult:
+                 merge_scatter: bool = False, exact: bool = False, merge_order: str = "mpi4py") -> PipelineResult:
     """``merge_slabs`` (N > 1, no alignment, HBM-resident block in one batch,
     flat chunk-aligned plan): cut the final sweep into that many atom slabs
     so each slab's cross-rank all-reduce overlaps the next slab's stream;
@@ -361,9 +361,10 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     "slice_mean", "slice_m2").
     ``exact`` (no alignment): RMSF.py:120-146 with the reference's own
     arithmetic -- each rank's block through the sequential Welford
-    (rmsf_welford_sequential), the ranks folded in rank order by
-    second_order_moments (parallel.global_chan_exact), RMSF.py:146: results
-    bit-identical to RMSF.py's recurrence, ~1.2x the balanced path's time."""
+    (rmsf_welford_sequential), the ranks reduced by second_order_moments in
+    RMSF.py:143's comm.reduce order (``merge_order``: "mpi4py", mpi4py's
+    default binomial tree, or "rank"; parallel.global_chan_exact), RMSF.py:146:
+    results bit-identical to RMSF.py's, ~1.3x the balanced path's time."""
     if align not in ALIGN_MODES:
         raise ValueError(f"align must be one of {ALIGN_MODES}, got {align!r}")
     if exact:
@@ -372,7 +373,7 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
         if n_splits or merge_scatter or merge_slabs not in (None, 0, 1) or collect_rmsd or collect_transforms:
             raise ValueError("exact=True runs the sequential Welford: no n_splits, merge_scatter, merge_slabs, "
                              "collect_rmsd or collect_transforms")
-        return _run_exact(eng, source, frames, max_batch, block, timer, merge_root)
+        return _run_exact(eng, source, frames, max_batch, block, timer, merge_root, merge_order)
     rank, size = parallel.world()
     n_total = len(frames)
     if n_total == 0:
@@ -541,7 +542,8 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                           transforms=xf_last, transforms_sweep1=xf_first)
 
 
-def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, merge_root) -> PipelineResult:
+def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, merge_root,
+               merge_order: str = "mpi4py") -> PipelineResult:
     """run_pipeline(exact=True): RMSF.py:120-146 bit for bit (see there)."""
     rank, size = parallel.world()
     n_total = len(frames)
@@ -566,16 +568,16 @@ def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, 
             work = eng.welford_sequential(b.ptr, b.fstride, b.n_frames, n_sel, b.sel, k, mean, ss, work)
         k += b.n_frames
         b.done()
-    if size > 1:                                             # RMSF.py:141-143, rank order
+    if size > 1:                                             # RMSF.py:141-143, comm.reduce's order
         with _span(timer, "merge"):
-            mean, ss = parallel.global_chan_exact(eng, mean, ss, [e - s for s, e in blocks], root)
+            mean, ss = parallel.global_chan_exact(eng, mean, ss, [e - s for s, e in blocks], root, merge_order)
     rmsf = None
     if mean is not None:
         rmsf = eng.empty(n_sel)
         eng.finalize(ss, n_sel, n_total, rmsf)               # RMSF.py:146
     return PipelineResult(rmsf=rmsf, mean=None if mean is None else mean.view(n_sel, 3),
                           m2=None if ss is None else ss.view(n_sel, 3), n_frames=n_total, n_local=n_local,
-                          block=(b0, b1), extras={"exact": True, "merge_root": root})
+                          block=(b0, b1), extras={"exact": True, "merge_root": root, "merge_order": merge_order})
 
 
 class CapturedPipeline:

@@ -94,11 +94,20 @@ class RMSF:
         ``align=None`` only: compute RMSF.py:120-146 with the reference's own
         arithmetic -- each rank's frames through the per-frame Welford of
         RMSF.py:137-138 in order (rmsf_welford_sequential), the ranks folded
-        in rank order by second_order_moments, RMSF.py:146 -- so
-        ``results`` are bit-identical to the script's recurrence on the same
-        float32 coordinates (``mean``, ``sumsquares`` and ``rmsf``).  About
-        1.2x the time of the default frame-parallel path, which agrees with
-        it to ~1e-13.
+        by second_order_moments in RMSF.py:143's reduce order
+        (``merge_order``), RMSF.py:146 -- so ``results`` are bit-identical to
+        the script's on the same float32 coordinates (``mean``,
+        ``sumsquares`` and ``rmsf``).  About 1.3x the time of the default
+        frame-parallel path, which agrees with it to ~1e-13.
+    merge_order : "mpi4py" | "rank"
+        ``exact=True`` with several ranks or devices: the order in which
+        RMSF.py:143's ``comm.reduce(S, op=second_order_moments)`` applies
+        the op.  "mpi4py" (default): mpi4py's default object reduce
+        (``rc.fast_reduce``), a binomial tree -- at 4 ranks
+        op(op(S0, S1), op(S2, S3)) -- run point to point as mpi4py runs it;
+        "rank": op folded in rank order (``rc.fast_reduce = False``).  The
+        two agree up to 3 ranks and differ in the last bits from 4.  (mpi4py
+        is upstream; its order is restated, not verified, here.)
     gpus : int | list of int, optional
         Drive this many devices (or these device ids) from one process: each
         takes the RMSF.py:65-69 block of its index and the blocks merge over
@@ -113,7 +122,7 @@ class RMSF:
                  device=None, batch_frames: int | None = None, n_splits: int | None = None,
                  collect_rmsd: bool = False, verbose: bool = False, gpus=None,
                  collect_transforms: bool = False, layout: str = "fac", merge_root: int | None = None,
-                 merge_scatter: bool = False, exact: bool = False, **kwargs):
+                 merge_scatter: bool = False, exact: bool = False, merge_order: str = "mpi4py", **kwargs):
         if layout not in ("fac", "soa"):
             raise ValueError(f"layout must be 'fac' or 'soa', got {layout!r}")
         if layout == "soa" and not (isinstance(atomgroup, np.ndarray) or isinstance(atomgroup, torch.Tensor)):
@@ -123,6 +132,9 @@ class RMSF:
         self.merge_root = merge_root
         self.merge_scatter = bool(merge_scatter)
         self.exact = bool(exact)
+        from ._lib import merge_order as _order
+        _order(merge_order)
+        self.merge_order = merge_order
         self._input = atomgroup
         self.select = select
         self.align = align
@@ -161,7 +173,7 @@ class RMSF:
             res = run_pipeline(eng, src, fl, align=self.align, masses=masses, ref_frame=self.ref_frame,
                                max_batch=self.batch_frames, n_splits=self.n_splits, collect_rmsd=self.collect_rmsd,
                                collect_transforms=self.collect_transforms, merge_root=self.merge_root,
-                               merge_scatter=self.merge_scatter, exact=self.exact)
+                               merge_scatter=self.merge_scatter, exact=self.exact, merge_order=self.merge_order)
             torch.cuda.current_stream(eng.device).synchronize()
             r = self.results
             host = lambda t: None if t is None else t.cpu().numpy()  # noqa: E731  (None: a non-root rank)
@@ -196,7 +208,8 @@ class RMSF:
         out = run_multi(self._input, self.gpus, select=self.select, align=self.align, masses=self.masses,
                         ref_frame=self.ref_frame, start=start, stop=stop, step=step,
                         batch_frames=self.batch_frames, frames=frames, collect_rmsd=self.collect_rmsd,
-                        layout=self.layout, merge_root=self.merge_root, exact=self.exact)
+                        layout=self.layout, merge_root=self.merge_root, exact=self.exact,
+                        merge_order=self.merge_order)
         r = self.results
         r.update(out)
         r.m2 = r.sumsquares

@@ -47,7 +47,10 @@ def main(argv=None) -> int:
                     help="N>1: reduce to rank 0 (RMSF.py:143, default), all-reduce, or reduce-scatter by atom slices")
     ap.add_argument("--exact", action="store_true",
                     help="with --align none: RMSF.py:120-146 with the script's own arithmetic, bit for bit "
-                         "(per-frame Welford, ranks reduced in rank order by second_order_moments)")
+                         "(per-frame Welford, ranks reduced by second_order_moments in comm.reduce's order)")
+    ap.add_argument("--merge-order", choices=["mpi4py", "rank"], default="mpi4py",
+                    help="--exact, N>1: the order RMSF.py:143's comm.reduce applies second_order_moments in "
+                         "(mpi4py: its default binomial tree; rank: rank order)")
     a = ap.parse_args(argv)
     if a.exact and (a.align != "none" or a.merge == "scatter"):
         ap.error("--exact needs --align none and --merge root or all")
@@ -78,7 +81,7 @@ def main(argv=None) -> int:
         shard = generate(eng, n_atoms, b0, max(b1 - b0, 1), seed=a.seed, motion=motion)[: b1 - b0]
         res = run_pipeline(eng, DeviceSource(shard, offset=b0, n_traj=n_frames), FrameList(n_frames),
                            align=align, ref_frame=a.ref_frame, merge_root=root, merge_scatter=a.merge == "scatter",
-                           exact=a.exact)
+                           exact=a.exact, merge_order=a.merge_order)
         rmsf = None if res.rmsf is None else res.rmsf.cpu().numpy()   # None on the non-root ranks
     else:
         if not (a.topology and a.trajectory):
@@ -91,7 +94,8 @@ def main(argv=None) -> int:
             u = mda.Universe(a.topology, a.trajectory)
             ag = u.select_atoms(a.select)
             rmsf = RMSF(ag, align=align, ref_frame=a.ref_frame, verbose=True, merge_root=root,
-                        exact=a.exact).run().results.rmsf
+                        merge_scatter=a.merge == "scatter", exact=a.exact,
+                        merge_order=a.merge_order).run().results.rmsf
         else:
             # native fallback: GRO or PSF topology + selection subset; XTC, DCD (or
             # multi-frame GRO) trajectory.  PSF masses (GRO: masses guessed from
@@ -108,7 +112,8 @@ def main(argv=None) -> int:
             traj = (a.trajectory if a.trajectory.lower().endswith((".xtc", ".dcd"))
                     else GroTopology(a.trajectory).frames)
             rmsf = RMSF(traj, select=sel, align=align, masses=masses, ref_frame=a.ref_frame,
-                        verbose=True, merge_root=root, exact=a.exact).run().results.rmsf
+                        verbose=True, merge_root=root, merge_scatter=a.merge == "scatter", exact=a.exact,
+                        merge_order=a.merge_order).run().results.rmsf
     if rank == 0:
         print(f"RMSF over {len(rmsf)} atoms: mean {rmsf.mean():.6f} A, max {rmsf.max():.6f} A", flush=True)
         if a.out:

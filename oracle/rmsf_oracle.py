@@ -202,18 +202,75 @@ def second_order_moments(S1, S2):
     return T, mu, M
 
 
-def chan_fold(parts):
-    """comm.reduce(S, op=second_order_moments) folded in rank order, skipping
-    empty partials (the reference raises ZeroDivisionError when two empty
-    partials meet, RMSF.py:39)."""
-    acc = None
-    for S in parts:
-        if S[0] == 0:
-            continue
-        acc = S if acc is None else second_order_moments(acc, S)
-    if acc is None:
+def _op_or_skip(S1, S2):
+    """second_order_moments, except where RMSF.py:39 raises (two empty
+    states, T = 0): the build continues with the empty state instead."""
+    if S1[0] + S2[0] == 0:
+        return S1
+    return second_order_moments(S1, S2)
+
+
+def _empty_as_zeros(S):
+    """An empty rank's S is (0, zeros, zeros) (RMSF.py:119-121 with no frame);
+    whatever arrays a caller passes for it are replaced by those zeros."""
+    if S[0] == 0:
+        z = np.zeros_like(np.asarray(S[1], dtype=np.float64))
+        return (0, z, z.copy())
+    return S
+
+
+def mpi4py_reduce(parts, op):
+    """mpi4py's lowercase ``comm.reduce(sendobj, op=op, root=0)`` as RMSF.py:143
+    calls it, evaluated for every rank at once: ``parts[r]`` is rank r's
+    ``sendobj``; returns rank 0's result.
+
+    Restated from mpi4py's published ``msgpickle.pxi`` (upstream, NOT vendored
+    or installed here, so unverified in this container): with
+    ``mpi4py.rc.fast_reduce`` (its default) an intracommunicator's object
+    reduce is ``PyMPI_reduce_p2p`` -- each rank starts from a copy of its own
+    object; for mask = 1, 2, 4, ...: a rank with the mask bit set sends its
+    result to ``rank & ~mask`` and is done; otherwise it receives from
+    ``rank | mask`` (when that rank exists) and computes
+    ``result = op(result, received)``.  Rank 0 ends with the result (and
+    forwards it to root when root != 0, which does not change it)."""
+    result = list(parts)
+    size = len(result)
+    mask = 1
+    while mask < size:
+        for r in range(0, size, 2 * mask):  # the ranks still receiving at this mask
+            if r + mask < size:
+                result[r] = op(result[r], result[r + mask])
+        mask <<= 1
+    return result[0]
+
+
+def naive_reduce(parts, op):
+    """mpi4py's object reduce with ``rc.fast_reduce = False`` (a gather to
+    root, then ``_py_reduce``): ``res = parts[0]; res = op(res, parts[i])``
+    in rank order."""
+    res = parts[0]
+    for S in parts[1:]:
+        res = op(res, S)
+    return res
+
+
+MERGE_ORDERS = ("mpi4py", "rank")
+
+
+def chan_fold(parts, order: str = "mpi4py"):
+    """RMSF.py:143 ``comm.reduce(S, root=0, op=second_order_moments)`` over the
+    ranks' S (rank order in ``parts``), applying the op in mpi4py's order
+    (``"mpi4py"``: the default binomial tree, ``mpi4py_reduce``; ``"rank"``:
+    rank order, ``naive_reduce``).  Empty ranks are RMSF.py's (0, zeros,
+    zeros) and enter the op like any other; a merge of two empty states
+    (where RMSF.py:39 raises ZeroDivisionError) is skipped, and a run with no
+    frame at all raises ZeroDivisionError."""
+    if order not in MERGE_ORDERS:
+        raise ValueError(f"order must be one of {MERGE_ORDERS}")
+    if sum(S[0] for S in parts) == 0:
         raise ZeroDivisionError("no frames on any rank")
-    return acc
+    parts = [_empty_as_zeros(S) for S in parts]
+    return (mpi4py_reduce if order == "mpi4py" else naive_reduce)(parts, _op_or_skip)
 
 
 # ---------------------------------------------------------------------------
@@ -277,7 +334,7 @@ def _frame_list(n_traj, start, stop, step):
 
 
 def rmsf_script(traj, sel=None, masses=None, size: int = 1, ref_frame: int = 0, align: str | None = "average",
-                start=None, stop=None, step=None, average_f32: bool = False):
+                start=None, stop=None, step=None, average_f32: bool = False, merge_order: str = "mpi4py"):
     """RMSF.py end to end, emulating ``mpirun -n size`` by running the ranks
     one after another.  align="average" is the script itself; "frame0" skips
     sweep 1 and aligns on frame ``ref_frame``; None is the bare Welford.
@@ -304,7 +361,7 @@ def rmsf_script(traj, sel=None, masses=None, size: int = 1, ref_frame: int = 0, 
         average = positions.reshape(-1, 3)
         ref_com, ref_coordinates = centred_reference(average.astype(np.float32) if average_f32 else average, masses)
     parts = [rank_sweep2(sub, sel, masses, b.start, b.stop, ref_coordinates, ref_com) for b in blocks]
-    Data = chan_fold(parts)
+    Data = chan_fold(parts, merge_order)  # RMSF.py:143
     RMSF = np.sqrt(Data[2].sum(axis=1) / Data[0])
     return dict(rmsf=RMSF, mean=Data[1], m2=Data[2], n=Data[0], parts=parts, average=average)
 

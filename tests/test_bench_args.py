@@ -108,3 +108,41 @@ def test_script_exact_needs_unaligned_root_or_all():
         r = subprocess.run([sys.executable, script, "--synthetic", "10", "5", "--exact", *extra],
                            capture_output=True, text=True, timeout=120)
         assert r.returncode == 2 and "--exact needs --align none" in r.stderr, (extra, r.stderr[-500:])
+
+
+def test_script_file_input_forwards_merge_scatter_and_order(tmp_path, monkeypatch):
+    """rmsf_mi355x.py with file input passes --merge scatter (and
+    --merge-order) on to RMSF, as the --synthetic branch passes them to the
+    pipeline (recorded by a stand-in RMSF; CPU only, no device work)."""
+    import sys
+    import types
+
+    import numpy as np
+    import torch
+
+    from conftest import PKG, ROOT
+    sys.path[:0] = [PKG]
+    import rmsf_amd
+    from rmsf_amd.topology import write_gro
+    seen = {}
+
+    class FakeRMSF:
+        def __init__(self, inp, **kw):
+            seen.update(kw, inp=inp)
+
+        def run(self):
+            return types.SimpleNamespace(results=types.SimpleNamespace(rmsf=np.ones(2)))
+
+    monkeypatch.setattr(rmsf_amd, "RMSF", FakeRMSF)
+    monkeypatch.setattr(torch.cuda, "set_device", lambda *a: None)
+    gro = str(tmp_path / "t.gro")
+    write_gro(gro, np.array([1, 1, 2, 2]), np.array(["ALA"] * 4), np.array(["N", "CA", "N", "CA"]),
+              np.zeros((4, 3), np.float32))
+    sys.path.insert(0, f"{ROOT}/mdanalysis-mpi_amd")
+    import importlib
+    script = importlib.import_module("rmsf_mi355x")
+    assert script.main(["--topology", gro, "--trajectory", str(tmp_path / "t.xtc"), "--merge", "scatter",
+                        "--merge-order", "rank"]) == 0
+    assert seen["merge_scatter"] is True and seen["merge_root"] == 0 and seen["merge_order"] == "rank"
+    assert script.main(["--topology", gro, "--trajectory", str(tmp_path / "t.xtc"), "--merge", "all"]) == 0
+    assert seen["merge_scatter"] is False and seen["merge_root"] is None and seen["merge_order"] == "mpi4py"

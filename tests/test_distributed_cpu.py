@@ -66,11 +66,23 @@ class OracleOps:
     @staticmethod
     def chan_merge(means, m2s, counts, n, mean_out, m2_out):
         """k_chan_merge: second_order_moments (RMSF.py:36-41) folded over the
-        parts in order, empty parts skipped (the oracle's chan_fold)."""
+        parts in rank order (the oracle's chan_fold, order "rank")."""
         from oracle import rmsf_oracle as O
-        S = O.chan_fold([(c, means[i].numpy(), m2s[i].numpy()) for i, c in enumerate(counts)])
+        S = O.chan_fold([(c, means[i].numpy(), m2s[i].numpy()) for i, c in enumerate(counts)], "rank")
         mean_out.copy_(torch.from_numpy(np.asarray(S[1])))
         m2_out.copy_(torch.from_numpy(np.asarray(S[2])))
+
+    @staticmethod
+    def chan_merge_pair(mean1, m21, n1, mean2, m22, n2):
+        """k_chan_pair: (mean1, m21) = second_order_moments(S1, S2) in place,
+        an empty side being RMSF.py's (0, zeros, zeros)."""
+        from oracle import rmsf_oracle as O
+        z = np.zeros(mean1.numel())
+        a = (n1, mean1.numpy().copy(), m21.numpy().copy()) if n1 else (0, z, z)
+        b = (n2, mean2.numpy(), m22.numpy()) if n2 else (0, z, z)
+        _, mu, M = O.second_order_moments(a, b)
+        mean1.copy_(torch.from_numpy(np.asarray(mu)))
+        m21.copy_(torch.from_numpy(np.asarray(M)))
 
     @staticmethod
     def chan_shift_finish(t, shift, off3, n_sel, n, mean, m2, rmsf):
@@ -82,7 +94,7 @@ class OracleOps:
         rmsf.copy_(torch.from_numpy(np.sqrt(q.reshape(-1, 3).sum(axis=1) / n)))
 
 
-def _worker(rank, size, port, n_frames, q, merge="two"):
+def _worker(rank, size, port, n_frames, q, merge="two", order="mpi4py"):
     sys.path[:0] = [ROOT, PKG]
     from conftest import init_gloo
     init_gloo(port, rank, size)
@@ -113,7 +125,7 @@ def _worker(rank, size, port, n_frames, q, merge="two"):
             # exact=True's merge: every rank's S gathered, folded in rank order
             counts = [b - a for a, b in parallel.blocks(n_frames, size)]
             mean, m2 = parallel.global_chan_exact(OracleOps, mean_k, m2_k, counts,
-                                                  root=1 % size if merge == "exact_root" else None)
+                                                  root=1 % size if merge == "exact_root" else None, order=order)
             rmsf = None if m2 is None else np.sqrt(m2.numpy().reshape(-1, 3).sum(axis=1) / n_frames)
         else:
             # the pipeline's one-all-reduce merge, shifted by the sweep-2
@@ -197,3 +209,33 @@ def test_scatter_layout_single_process():
     np.testing.assert_array_equal(rmsf.numpy(), rmsf2.numpy())
     np.testing.assert_array_equal(mean_s.numpy(), mean.numpy())
     np.testing.assert_array_equal(m2_s.numpy(), m2.numpy())
+
+
+@pytest.mark.parametrize("order", ["mpi4py", "rank"])
+@pytest.mark.parametrize("size,n_frames,to_root", [(4, 41, False), (5, 53, True), (4, 3, True), (5, 23, False)])
+def test_gloo_exact_merge_order(size, n_frames, to_root, order):
+    """RMSF.py:143's comm.reduce at 4 and 5 ranks through the product's
+    exact merge (parallel.global_chan_exact): order "mpi4py" runs mpi4py's
+    binomial tree point to point (send / recv between the gloo ranks),
+    "rank" gathers and folds in rank order; each equals the oracle's
+    rmsf_script with that order bit for bit, on the root (or every rank).
+    3 frames on 4 ranks: empty ranks 0-2 (a skipped empty-empty merge)."""
+    from oracle import rmsf_oracle as O
+    from oracle import synth as SY
+    from rmsf_amd.synth import motion_table
+
+    from conftest import spawn_ranks
+    out = spawn_ranks(_worker, size, lambda r, init, q: (r, size, init, n_frames, q,
+                                                         "exact_root" if to_root else "exact", order))
+    traj = SY.frames(8, 60, 0, n_frames, motion_table(9, n_frames))
+    want = O.rmsf_script(traj, np.arange(0, 60, 3), None, size=size, align="average", merge_order=order)
+    other = O.rmsf_script(traj, np.arange(0, 60, 3), None, size=size, align="average",
+                          merge_order="rank" if order == "mpi4py" else "mpi4py")
+    got_root = 1 % size if to_root else None
+    for rank, rmsf, _ in out:
+        if got_root is not None and rank != got_root:
+            assert rmsf is None
+            continue
+        np.testing.assert_array_equal(rmsf.view(np.uint64), want["rmsf"].view(np.uint64))
+    if n_frames > size:   # the two orders differ in bits here (the option matters)
+        assert not np.array_equal(want["m2"].view(np.uint64), other["m2"].view(np.uint64))
