@@ -98,6 +98,8 @@ def parse(argv=None):
                     help="frames per CPU process for the RMSF.py two-sweep baseline sample")
     ap.add_argument("--no-modes", action="store_true", help="skip the aligned-mode measurements at N=1")
     ap.add_argument("--mode-steps", type=int, default=3)
+    ap.add_argument("--no-io-modes", action="store_true",
+                    help="N=1: skip the C4-share and C5-XTC modes (30 GB of frames, a 2.7 GB XTC file)")
     ap.add_argument("--stager-threads", type=int, default=4)
     ap.add_argument("--stager-batch", type=int, default=None, help="c5: frames per staged batch")
     ap.add_argument("--xtc-decode", choices=["gpu", "host"], default="gpu",
@@ -264,7 +266,8 @@ def c1_latency(eng, no_cpu: bool) -> dict:
     graph_ms = (time.perf_counter() - t0) / reps * 1e3
     same = bool(torch.equal(cap.result.rmsf, res.rmsf))
     out = {"workload": "C1 shape: 3341 atoms, 214 selected, 98 frames, RMSF.py two-sweep",
-           "gpu_ms_eager": gpu_ms, "gpu_ms_hipgraph": graph_ms, "hipgraph_bitwise_equal": same}
+           "gpu_ms_eager": gpu_ms, "gpu_ms_hipgraph": graph_ms, "hipgraph_bitwise_equal": same,
+           "sanity": sanity(eng, res.rmsf, nf, seed=11, atoms=sel)}
     if not no_cpu:
         from oracle import rmsf_oracle as O
 
@@ -274,6 +277,161 @@ def c1_latency(eng, no_cpu: bool) -> dict:
         out["cpu_ms_1core_numpy"] = (time.perf_counter() - t0) * 1e3
         out["note"] = "CPU: oracle restatement on 1 core (no XTC decode, no re-selection): optimistic"
     return out
+
+
+def sanity(eng, rmsf, n_frames: int, seed: int = 0, atoms=None) -> dict:
+    """Package-side result check of a timed mode (rmsf_amd.synth.rmsf_sanity:
+    every atom's RMSF against the generator's sqrt(3) sigma); a failed check
+    ends the bench -- a fast wrong result is not a measurement."""
+    from rmsf_amd.synth import rmsf_sanity
+
+    chk = rmsf_sanity(eng, rmsf, n_frames, seed=seed, atoms=atoms)
+    if not chk["ok"]:
+        raise SystemExit(f"bench sanity check failed: {chk}")
+    return chk
+
+
+def c4_share_mode(eng, a, headline_avg_ms: float | None, n_atoms: int = 1_000_000, nf: int = 2_500) -> dict:
+    """Config C4's per-rank step at N = 8 (BASELINE configs[3]: 1M atoms x
+    20k frames over 8 GPUs = 1M x 2,500 per rank), on this one device: the
+    one-process form's context step -- rmsf_multi_push_frames with the merge
+    shift frame, the sweep recorded for the 2-slab merge, then
+    rmsf_multi_chan_merge_root(root=0) streaming it slab by slab (each slab's
+    accumulate + fold-pack) -- with the no-op transport (no peers: the
+    collective moves nothing; the RMSF is this block's, RMSF.py:65-69)."""
+    import torch
+
+    from rmsf_amd.context import PUSH_WELFORD, TRANSPORT_NOOP, Context
+    from rmsf_amd.synth import generate
+
+    traj = generate(eng, n_atoms, 0, nf, seed=0)
+    torch.cuda.synchronize()
+    c = Context(n_atoms, device=eng.device.index)
+    try:
+        c.set_timing(True)
+        Context.multi_set_transport([c], TRANSPORT_NOOP)
+        frame0 = traj[0]
+
+        def step():
+            Context.multi_push_frames([c], [traj], PUSH_WELFORD, shift_frames=[frame0], merge_slabs=2,
+                                      after_torch=False)
+            Context.multi_chan_merge([c], root=0)
+
+        step()
+        for w in ("accumulate", "merge"):
+            c.kernel_time(w)
+        t0 = time.perf_counter()
+        for _ in range(a.mode_steps):
+            step()
+        c.synchronize()
+        dt = time.perf_counter() - t0
+        k, ms, af = c.kernel_time("accumulate")
+        km, mms, _ = c.kernel_time("merge")
+        rmsf = c.rmsf()
+    finally:
+        c.close()
+    step_ms = dt / a.mode_steps * 1e3
+    peak_ms = B_PER_ATOM_FRAME * n_atoms * nf / (HBM_PEAK_GBS * 1e9) * 1e3
+    out = {"workload": f"C4 share: {n_atoms} atoms x {nf} frames (1M x 2,500 = one rank's block of configs[3] at "
+                       "N = 8); the one-process context step (2 atom slabs, fold-pack, reduce to root) with a "
+                       "no-op transport",
+           "atom_frames_per_s": n_atoms * nf * a.mode_steps / dt, "ms_per_step": step_ms,
+           "accumulate_launches_per_step": k / a.mode_steps, "accumulate_ms_per_step": ms / a.mode_steps,
+           "accumulate_frac": B_PER_ATOM_FRAME * af / (ms / 1e3) / 1e9 / HBM_PEAK_GBS if ms else None,
+           "exposed_merge_ms_per_step": mms / max(1, km),
+           "floor_peak_ms": peak_ms, "step_over_peak_floor": step_ms / peak_ms,
+           "sanity": sanity(eng, rmsf, nf)}
+    if headline_avg_ms:
+        # the headline stream's measured rate applied to the share's bytes
+        # (100k x 2,500 at 0.446 ms scales by 10 to 1M atoms)
+        fl = headline_avg_ms * (n_atoms * nf) / (100_000 * 20_000)
+        out.update(floor_headline_rate_ms=fl, step_over_headline_rate=step_ms / fl)
+    del traj
+    torch.cuda.empty_cache()
+    return out
+
+
+def c5_xtc_mode(eng, a, n_atoms: int = 250_000, nf: int = 2048) -> dict:
+    """Config C5 (BASELINE configs[4]): a 250k-atom XTC file streamed from the
+    host, written untimed from the synthetic generator, then per step read
+    (pread into pinned slots), copied to HBM and decompressed on the GPU
+    (XtcSource decode="gpu"), the Welford stream consuming each batch --
+    read + PCIe + decode inclusive.  The decode kernel's own time is
+    measured apart on HBM-resident records (HIP events, torch's stream)."""
+    import shutil
+    import tempfile
+
+    import numpy as np
+    import torch
+
+    from rmsf_amd._lib import call
+    from rmsf_amd.pipeline import KernelTimer, run_pipeline
+    from rmsf_amd.sources import FrameList, XtcSource
+    from rmsf_amd.synth import generate
+    from rmsf_amd.xtc import XTCFile, write_xtc
+
+    d = tempfile.mkdtemp(prefix="rmsf_c5_")
+    path = os.path.join(d, "c5.xtc")
+    try:
+        t_w = time.perf_counter()
+        for f in range(0, nf, 256):
+            n = min(256, nf - f)
+            write_xtc(path, generate(eng, n_atoms, f, n, seed=0).cpu().numpy(), append=f > 0)
+        t_w = time.perf_counter() - t_w
+        src = XtcSource(path, None, decode="gpu", n_threads=16, n_slots=3)
+        fl = FrameList(nf)
+        run_pipeline(eng, src, fl)
+        torch.cuda.synchronize()
+        timer = KernelTimer()
+        t0 = time.perf_counter()
+        for _ in range(a.mode_steps):
+            res = run_pipeline(eng, src, fl, timer=timer)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        k, ms, af = timer.totals("accumulate")
+        xbytes = os.path.getsize(path)
+        # the decode kernel alone: the first 512 frames' records in HBM
+        nk = min(512, nf)
+        with XTCFile(path) as f:
+            rec = [f.record(i) for i in range(nk)]
+        o0 = rec[0][0]
+        raw = np.fromfile(path, dtype=np.uint32, count=(rec[-1][0] + rec[-1][1] - o0) // 4, offset=o0)
+        off = torch.tensor([(o - o0) // 4 for o, _ in rec], dtype=torch.int64, device=eng.device)
+        ln = torch.tensor([n // 4 for _, n in rec], dtype=torch.int64, device=eng.device)
+        words = torch.as_tensor(raw.view(np.int32)).to(eng.device)
+        out = torch.empty((nk, n_atoms, 3), dtype=torch.float32, device=eng.device)
+        st = torch.empty(nk, dtype=torch.int32, device=eng.device)
+        s = torch.cuda.current_stream(eng.device)
+
+        def dec():
+            call("rmsf_xtc_decode_records", words.data_ptr(), off.data_ptr(), ln.data_ptr(), nk, n_atoms,
+                 out.data_ptr(), 3 * n_atoms, st.data_ptr(), s.cuda_stream)
+
+        dec()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+        for e0, e1 in evs:
+            e0.record(s)
+            dec()
+            e1.record(s)
+        torch.cuda.synchronize()
+        dec_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / len(evs)
+        ok_status = bool((st == 0).all())
+        chk = sanity(eng, res.rmsf, nf)
+        del src, words, out
+        torch.cuda.empty_cache()
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return {"workload": "C5: 250k-atom XTC (precision 1000, written untimed from the generator) streamed from the "
+                        "host: pread into pinned slots, H2D of the compressed records, GPU decode, Welford stream",
+            "n_atoms": n_atoms, "n_frames": nf, "frames_per_s": nf * a.mode_steps / dt,
+            "atom_frames_per_s": n_atoms * nf * a.mode_steps / dt, "ms_per_step": dt / a.mode_steps * 1e3,
+            "xtc_bytes": xbytes, "h2d_gbs": xbytes * a.mode_steps / dt / 1e9, "host_link_spec_gbs": 63.0,
+            "h2d_over_link": xbytes * a.mode_steps / dt / 1e9 / 63.0,
+            "decoded_frame_gbs": B_PER_ATOM_FRAME * n_atoms * nf * a.mode_steps / dt / 1e9,
+            "decode_kernel": {"frames": nk, "avg_ms": dec_ms, "frames_per_s": nk / (dec_ms / 1e3),
+                              "decoded_gbs": B_PER_ATOM_FRAME * n_atoms * nk / (dec_ms / 1e3) / 1e9,
+                              "all_frames_ok": ok_status},
+            "accumulate_avg_ms": ms / max(1, k), "xtc_write_s_untimed": t_w, "sanity": chk}
 
 
 def cpu_baselines(a, wl) -> tuple[dict | None, dict | None]:
@@ -379,7 +537,7 @@ def main_single_process(a, wl, cpu) -> None:
     for _ in range(a.warmup):
         step()
     for c in ctxs:  # drop the warm-up's launch records (synchronises)
-        c.kernel_time("accumulate"), c.kernel_time("superpose")
+        c.kernel_time("accumulate"), c.kernel_time("superpose"), c.kernel_time("merge")
         c.synchronize()
     t0 = time.perf_counter()
     host_s = 0.0
@@ -392,6 +550,7 @@ def main_single_process(a, wl, cpu) -> None:
     dt = time.perf_counter() - t0
     acc = [c.kernel_time("accumulate") for c in ctxs]
     sup = [c.kernel_time("superpose") for c in ctxs]
+    mer = [c.kernel_time("merge") for c in ctxs]
     rmsf = ctxs[root or 0].rmsf()
     transport = ("REHEARSAL: device 0 listed %d times, %s" % (n, "no-op exchanges (host-cost timing; the merged "
                  "result is not global)" if noop else "in-process host fold") if rehearsal
@@ -410,8 +569,19 @@ def main_single_process(a, wl, cpu) -> None:
         ms, af = sum(x[1] for x in sup), sum(x[2] for x in sup)
         out["superpose"] = {"launches": sum(x[0] for x in sup), "avg_launch_ms": ms / max(1, sum(x[0] for x in sup)),
                             "gflops": FLOP_PER_ATOM_FRAME_SUPERPOSE * af / (ms / 1e3) / 1e9 if ms else None}
+    if n > 1:
+        # each context's merge as its stream saw it: HIP events from its packed
+        # moments to its finished result (the collective, the wait for the
+        # slowest context, the unpack; with slabs the part after the last slab)
+        per = [m[1] / max(1, m[0]) for m in mer]
+        out["merge_timing"] = {"per_device_ms_per_step": per, "max_ms_per_step": max(per),
+                               "rule": "HIP events on each context's stream around its part of "
+                                       "rmsf_multi_chan_merge_root, per timed step (rmsf_ctx_kernel_time MERGE)"}
     out["cpu_baseline"] = cpu
     out["rmsf_checksum"] = float(rmsf.sum())
+    if not noop:
+        with torch.cuda.device(devs[root or 0]):
+            out["sanity"] = sanity(Engine(torch.device("cuda", devs[root or 0])), rmsf, n_total)
     print(json.dumps(out), flush=True)
     for c in ctxs:
         c.close()
@@ -583,6 +753,8 @@ def main():
     out["cpu_baseline"] = cpu
     # the merged result (on rank 0 only with the default reduce-to-root merge)
     out["rmsf_checksum"] = float(res.rmsf.sum()) if res.rmsf is not None else None
+    if res.rmsf is not None:
+        out["sanity"] = sanity(eng, res.rmsf, n_total)
     # whole-step rate in algorithmic bytes (incl. merges, finalise, launch gaps)
     out["pipeline_hbm_gbs"] = B_PER_ATOM_FRAME * n_atoms * n_local * a.steps / dt / 1e9
     if wl["align"]:
@@ -643,7 +815,9 @@ def main():
             "avg_launch_ms": x_ms / max(1, k_x),
             "hbm_frac": B_PER_ATOM_FRAME * x_af / (x_ms / 1e3) / 1e9 / HBM_PEAK_GBS if x_ms > 0 else None,
             "max_abs_rmsf_diff_vs_headline": float((res_x.rmsf - res.rmsf).abs().max()),
-            "note": "RMSF.py:120-146 with the reference's own arithmetic, bit for bit (tests/test_gpu_exact.py)"}
+            "sanity": sanity(eng, res_x.rmsf, n_total),
+            "note": "RMSF.py:120-146 with the reference's own arithmetic, bit for bit (tests/test_gpu_exact.py, "
+                    "tests/test_reduce_order.py)"}
         del traj, src
         torch.cuda.empty_cache()
         motion = motion_table(1, n_total)
@@ -652,7 +826,7 @@ def main():
         src = DeviceSource(traj, offset=b0, n_traj=n_total)
         modes = {"c2_exact": exact_mode}
         for name, align in (("c3_frame0", "frame0"), ("rmsf_py_average", "average")):
-            mdt, mt, _ = timed(align, a.mode_steps, 1)
+            mdt, mt, mres = timed(align, a.mode_steps, 1)
             sweeps = 2 if align == "average" else 1
             af = n_total * n_atoms * a.mode_steps / mdt
             k_s, s_ms, s_af = mt.totals("superpose")
@@ -667,12 +841,23 @@ def main():
                 "superpose_hbm_gbs": B_PER_ATOM_FRAME * s_af / (s_ms / 1e3) / 1e9,
                 "accumulate_avg_ms": a_ms / max(1, k_a),
                 "accumulate_hbm_gbs": B_PER_ATOM_FRAME * a_af / (a_ms / 1e3) / 1e9,
+                "sanity": sanity(eng, mres.rmsf, n_total),
             }
+            # the aligned design reads each frame twice per sweep (DESIGN §4,
+            # "Why the aligned path reads each frame twice"); against a
+            # roofline of ONE read per sweep (12 B per atom-frame per sweep)
+            # the whole computation runs at:
+            modes[name]["frac_of_single_read_roofline"] = af * B_PER_ATOM_FRAME * sweeps / 1e9 / HBM_PEAK_GBS
         if cpu is not None:
             modes["rmsf_py_average"]["cpu_baseline"] = {
                 "value": cpu["value"], "cores": cpu["cores"], "sample": cpu["sample"],
                 "gpu_over_cpu": modes["rmsf_py_average"]["atom_frames_per_s"] / cpu["value"]}
         modes["c1_rmsf_py"] = c1_latency(eng, a.no_cpu_baseline)
+        del traj, src
+        torch.cuda.empty_cache()
+        if not a.no_io_modes:
+            modes["c4_share"] = c4_share_mode(eng, a, out["roofline"]["avg_launch_ms"])
+            modes["c5_xtc"] = c5_xtc_mode(eng, a)
         out["modes"] = modes
     if rank == 0:
         print(json.dumps(out), flush=True)

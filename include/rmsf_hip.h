@@ -609,6 +609,11 @@ int rmsf_ctx_set_staging(rmsf_ctx *ctx, int64_t batch_frames, int n_slots,
  * that family's record.                                                      */
 #define RMSF_TIME_ACCUMULATE 0 /* rmsf_accumulate_balanced (RMSF.py:99-103,133-138) */
 #define RMSF_TIME_SUPERPOSE 1  /* rmsf_superpose (RMSF.py:94-97 + qcprot, :43-51)  */
+/* the cross-context merge, per context: from its packed moments to its
+ * finished result on its stream (collective, waits for the slowest context,
+ * unpack/finalise; with atom slabs the part after the last slab's pack);
+ * atom_frames = 0                                                           */
+#define RMSF_TIME_MERGE 2
 int rmsf_ctx_set_timing(rmsf_ctx *ctx, int on);
 int rmsf_ctx_kernel_time(rmsf_ctx *ctx, int which, int64_t *launches,
                          double *ms, double *atom_frames);

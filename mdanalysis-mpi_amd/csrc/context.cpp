@@ -276,11 +276,13 @@ struct rmsf_ctx {
   // accumulate launch on the context stream, with the atom-frames it covered
   struct Span {
     hipEvent_t a, b;
-    int which;  // RMSF_TIME_ACCUMULATE / RMSF_TIME_SUPERPOSE
+    int which;  // RMSF_TIME_ACCUMULATE / RMSF_TIME_SUPERPOSE / RMSF_TIME_MERGE
     int64_t atom_frames;
+    bool closed;  // b recorded
   };
   bool timing = false;
   std::vector<Span> spans;
+  int open_merge = -1;  // index of the merge span awaiting its end event
   std::vector<hipEvent_t> event_pool;  // events of read spans, reused by the next ones
   // per-frame QCP rmsd of the aligned Welford pushes (rmsf_ctx_collect_rmsd)
   bool collect_rmsd = false;
@@ -366,7 +368,7 @@ int ensure_zeroed(rmsf_ctx *c, Running &r, bool two) {
 template <class F>
 int timed(rmsf_ctx *c, int which, int64_t atom_frames, F &&launch) {
   if (!c->timing) return launch();
-  rmsf_ctx::Span sp{nullptr, nullptr, which, atom_frames};
+  rmsf_ctx::Span sp{nullptr, nullptr, which, atom_frames, true};
   auto take = [c](hipEvent_t *e) -> hipError_t {
     if (c->event_pool.empty()) return hipEventCreate(e);
     *e = c->event_pool.back();
@@ -382,6 +384,39 @@ int timed(rmsf_ctx *c, int which, int64_t atom_frames, F &&launch) {
   CX_HIP(hipEventRecord(sp.a, c->stream));
   CX_OK(launch());
   CX_HIP(hipEventRecord(sp.b, c->stream));
+  return RMSF_OK;
+}
+
+// The merge's span (RMSF_TIME_MERGE): opened on `s` where the context's
+// exchange starts (its moments packed), closed on `s2` where its result is
+// finished -- the collective, the wait for the slowest rank and the unpack,
+// as each device's stream sees them.
+int merge_open(rmsf_ctx *c, hipStream_t s) {
+  if (!c->timing) return RMSF_OK;
+  hipEvent_t a = nullptr, b = nullptr;
+  auto take = [c](hipEvent_t *e) -> hipError_t {
+    if (c->event_pool.empty()) return hipEventCreate(e);
+    *e = c->event_pool.back();
+    c->event_pool.pop_back();
+    return hipSuccess;
+  };
+  CX_HIP(take(&a));
+  if (take(&b) != hipSuccess) {
+    c->event_pool.push_back(a);
+    return fail(RMSF_EHIP, "hipEventCreate failed");
+  }
+  c->spans.push_back({a, b, RMSF_TIME_MERGE, 0, false});
+  c->open_merge = (int)c->spans.size() - 1;
+  CX_HIP(hipEventRecord(a, s));
+  return RMSF_OK;
+}
+
+int merge_close(rmsf_ctx *c, hipStream_t s) {
+  if (!c->timing || c->open_merge < 0) return RMSF_OK;
+  rmsf_ctx::Span &sp = c->spans[c->open_merge];
+  c->open_merge = -1;
+  CX_HIP(hipEventRecord(sp.b, s));
+  sp.closed = true;
   return RMSF_OK;
 }
 
@@ -401,6 +436,9 @@ void drop_spans(rmsf_ctx *c, int which) {
     }
   }
   c->spans.swap(keep);
+  c->open_merge = -1;
+  for (size_t i = 0; i < c->spans.size(); ++i)
+    if (c->spans[i].which == RMSF_TIME_MERGE && !c->spans[i].closed) c->open_merge = (int)i;
   if (which < 0) {
     for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
     c->event_pool.clear();
@@ -710,6 +748,7 @@ int exchange_chan(rmsf_ctx **cs, int n, const Reduce &red, bool host_counts) {
     DeviceScope ds(c->dev);
     CX_OK(c->xa.ensure(sizeof(double) * nc, c->stream));
     CX_OK(c->xb.ensure(sizeof(double) * nc, c->stream));
+    CX_OK(merge_open(c, c->stream));
     CX_OK(rmsf_chan_weight(c->wel.parts0.d(), (double)local[i] / (double)total, nc, c->xa.d(), c->stream));
     a[i] = c->xa.d();
     b[i] = c->xb.d();
@@ -730,6 +769,7 @@ int exchange_chan(rmsf_ctx **cs, int n, const Reduce &red, bool host_counts) {
     CX_HIP(hipMemcpyAsync(c->wel.parts1.p, c->xb.p, sizeof(double) * nc, hipMemcpyDeviceToDevice, c->stream));
     c->wel.n = total;
     c->rmsf_valid = false;
+    CX_OK(merge_close(c, c->stream));
   }
   return RMSF_OK;
 }
@@ -795,17 +835,17 @@ int exchange_chan_shifted(rmsf_ctx **cs, int n, const Reduce &red, bool host_cou
                                  c->xa.d(), c->stream));
     }
     t[i] = c->xa.d();
-    return RMSF_OK;
+    return merge_open(c, c->stream);
   }));
   CX_OK(red(2 * nc, t.data(), root));
   return for_each_ctx(cs, n, [&](int i) -> int {
     rmsf_ctx *c = cs[i];
+    DeviceScope ds(c->dev);
     if (root >= 0 && i != root) {
       c->merged_away = true;
       c->rmsf_valid = false;
-      return RMSF_OK;
+      return merge_close(c, c->stream);  // its part of the reduce was queued on its stream
     }
-    DeviceScope ds(c->dev);
     const ShiftArgs sh = shift_of(c, kind);
     CX_OK(c->rmsf.ensure(sizeof(double) * c->n_sel, c->stream));
     CX_OK(rmsf_chan_shift_finish(c->xa.d(), sh.p, sh.f32, sh.off3, c->n_sel, total, c->wel.parts0.d(),
@@ -813,7 +853,7 @@ int exchange_chan_shifted(rmsf_ctx **cs, int n, const Reduce &red, bool host_cou
     c->wel.n = total;
     c->rmsf_valid = true;
     c->merged_away = false;
-    return RMSF_OK;
+    return merge_close(c, c->stream);
   });
 }
 
@@ -978,7 +1018,7 @@ int slab_merge(rmsf_ctx **cs, int n, int kind, const Reduce &red, int root) {
     c->wel.n += sp.n_frames;
     c->wel.stale = false;
     c->wel_aligned = false;
-    return RMSF_OK;
+    return merge_open(c, c->stream);  // the exposed part: after the last slab's pack
   }));
   std::vector<double *> bufs(n);
   std::vector<hipStream_t> st(n);
@@ -1004,12 +1044,13 @@ int slab_merge(rmsf_ctx **cs, int n, int kind, const Reduce &red, int root) {
   }
   for (int i = 0; i < n; ++i) {
     rmsf_ctx *c = cs[i];
+    DeviceScope ds(c->dev);
     if (root >= 0 && i != root) {
       c->merged_away = true;
       c->rmsf_valid = false;
+      CX_OK(merge_close(c, rc_l ? c->comm_stream : c->stream));  // after its last slab's collective
       continue;
     }
-    DeviceScope ds(c->dev);
     CX_OK(c->rmsf.ensure(sizeof(double) * c->n_sel, c->stream));
     for (size_t s = 0; s < ns; ++s) {
       const int64_t j0 = 1024 * bounds[s].first, j1 = std::min(1024 * bounds[s].second, nc);
@@ -1021,6 +1062,7 @@ int slab_merge(rmsf_ctx **cs, int n, int kind, const Reduce &red, int root) {
     c->wel.n = total;
     c->rmsf_valid = true;
     c->merged_away = false;
+    CX_OK(merge_close(c, c->stream));
   }
   return RMSF_OK;
 }
@@ -1069,6 +1111,10 @@ int exact_merge(rmsf_ctx **cs, int n, int root, int order) {
   for (int64_t v : cnt) total += v;
   if (total == 0) return fail(RMSF_EEMPTY, "rmsf exact merge: no frames on any rank (RMSF.py:39 ZeroDivisionError)");
   const int64_t nc = cs[0]->n_coord;
+  for (int i = 0; i < n; ++i) {
+    DeviceScope ds(cs[i]->dev);
+    CX_OK(merge_open(cs[i], cs[i]->stream));
+  }
   const int ns = rmsf_chan_reduce_steps(n, order, nullptr, nullptr, 0);
   if (ns < 0) return ns;
   std::vector<int> dst(std::max(ns, 1)), src(std::max(ns, 1));
@@ -1106,6 +1152,10 @@ int exact_merge(rmsf_ctx **cs, int n, int root, int order) {
   if (root > 0) {  // rank 0 only sent its result on
     cs[0]->merged_away = true;
     cs[0]->rmsf_valid = false;
+  }
+  for (int i = 0; i < n; ++i) {
+    DeviceScope ds(cs[i]->dev);
+    CX_OK(merge_close(cs[i], cs[i]->stream));
   }
   return RMSF_OK;
 }
@@ -1238,7 +1288,7 @@ RMSF_EXPORT int rmsf_ctx_set_timing(rmsf_ctx *c, int on) {
 
 RMSF_EXPORT int rmsf_ctx_kernel_time(rmsf_ctx *c, int which, int64_t *launches, double *ms, double *atom_frames) {
   CX_OK(check_ctx(c, "rmsf_ctx_kernel_time"));
-  if (which != RMSF_TIME_ACCUMULATE && which != RMSF_TIME_SUPERPOSE)
+  if (which != RMSF_TIME_ACCUMULATE && which != RMSF_TIME_SUPERPOSE && which != RMSF_TIME_MERGE)
     return fail(RMSF_EINVAL, "rmsf_ctx_kernel_time: bad kernel");
   DeviceScope ds(c->dev);
   CX_OK(flush_slab(c));  // a recorded slab push is part of what was timed
@@ -1246,7 +1296,7 @@ RMSF_EXPORT int rmsf_ctx_kernel_time(rmsf_ctx *c, int which, int64_t *launches, 
   int64_t k = 0;
   double t = 0.0, af = 0.0;
   for (auto &sp : c->spans) {
-    if (sp.which != which) continue;
+    if (sp.which != which || !sp.closed) continue;
     float e = 0.f;
     CX_HIP(hipEventElapsedTime(&e, sp.a, sp.b));
     ++k;

@@ -509,7 +509,11 @@ __global__ __launch_bounds__(kBlock) void k_welford_seq(const float *__restrict_
   };
   // two register blocks in turn, one always loading while the other folds
   // (no copies between them: a copy makes the compiler wait on the
-  // coefficients' scalar loads where it is made)
+  // coefficients' scalar loads where it is made).  The coefficients stay a
+  // table read by scalar loads: computing each 64-frame window's c and r in
+  // the wave (one division per lane) and broadcasting them by v_readlane is
+  // bit-identical but slower -- 4.98 vs 4.20 ms at 100k x 20k
+  // (tools/ab_seq_lane.py, profiles/r05_workloads/seq_welford_lane.txt).
   int64_t f = 0;
   if (nf >= U) {
     float a[U], b[U];

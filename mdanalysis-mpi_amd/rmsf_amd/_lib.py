@@ -160,7 +160,7 @@ SIGNATURES = {
 ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int64, c_void_p, c_void_p)
 RMSF_PUSH_WELFORD, RMSF_PUSH_ALIGN_SUM, RMSF_PUSH_ALIGN_WELFORD, RMSF_PUSH_SUM, RMSF_PUSH_EXACT = 0, 1, 2, 3, 4
 RMSF_UNIQUE_ID_BYTES = 128
-RMSF_TIME_ACCUMULATE, RMSF_TIME_SUPERPOSE = 0, 1
+RMSF_TIME_ACCUMULATE, RMSF_TIME_SUPERPOSE, RMSF_TIME_MERGE = 0, 1, 2
 RMSF_MULTI_RESET = 1
 RMSF_TRANSPORT_AUTO, RMSF_TRANSPORT_NOOP = 0, 1
 RMSF_MERGE_RANK, RMSF_MERGE_MPI4PY = 0, 1

@@ -28,8 +28,8 @@ import ctypes
 import numpy as np
 
 from ._lib import (ALLREDUCE_FN, RMSF_MULTI_RESET, RMSF_PUSH_ALIGN_SUM, RMSF_PUSH_ALIGN_WELFORD, RMSF_PUSH_EXACT,
-                   RMSF_PUSH_SUM, RMSF_PUSH_WELFORD, RMSF_TIME_ACCUMULATE, RMSF_TIME_SUPERPOSE, RMSF_TRANSPORT_AUTO,
-                   RMSF_TRANSPORT_NOOP, RMSF_UNIQUE_ID_BYTES, call, load)
+                   RMSF_PUSH_SUM, RMSF_PUSH_WELFORD, RMSF_TIME_ACCUMULATE, RMSF_TIME_MERGE, RMSF_TIME_SUPERPOSE,
+                   RMSF_TRANSPORT_AUTO, RMSF_TRANSPORT_NOOP, RMSF_UNIQUE_ID_BYTES, call, load)
 
 PUSH_WELFORD = RMSF_PUSH_WELFORD
 PUSH_ALIGN_SUM = RMSF_PUSH_ALIGN_SUM
@@ -133,13 +133,16 @@ class Context:
         call("rmsf_ctx_set_staging", self._h, batch_frames, n_slots, n_threads)
 
     def set_timing(self, on: bool = True) -> None:
-        """HIP events around every superpose / accumulate launch (measurement)."""
+        """HIP events around every superpose / accumulate launch and around
+        this context's part of each cross-context merge (measurement)."""
         call("rmsf_ctx_set_timing", self._h, 1 if on else 0)
 
     def kernel_time(self, which: str = "accumulate") -> tuple[int, float, float]:
         """(launches, summed ms, atom-frames) of one kernel family since the
-        last call (``which``: "accumulate" or "superpose"); synchronises."""
-        k = {"accumulate": RMSF_TIME_ACCUMULATE, "superpose": RMSF_TIME_SUPERPOSE}[which]
+        last call (``which``: "accumulate", "superpose", or "merge" -- the
+        context's merges: from its packed moments to its finished result,
+        atom-frames 0); synchronises."""
+        k = {"accumulate": RMSF_TIME_ACCUMULATE, "superpose": RMSF_TIME_SUPERPOSE, "merge": RMSF_TIME_MERGE}[which]
         n, ms, af = ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
         call("rmsf_ctx_kernel_time", self._h, k, ctypes.byref(n), ctypes.byref(ms), ctypes.byref(af))
         self._alive.clear()  # kernel_time synchronised the stream

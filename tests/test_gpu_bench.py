@@ -30,6 +30,12 @@ def test_single_process_rehearsal_matches_oracle(align, capsys):
     assert line["scaling"] == "strong" and line["config"]["n_frames_total"] == 61
     assert line["roofline"]["launches"] == 3 * 2 * (2 if align == "average" else 1)
     assert 0 < line["roofline"]["frac"] < 1.0
+    # the one-process N > 1 line reports its merge, per device
+    mt = line["merge_timing"]
+    assert len(mt["per_device_ms_per_step"]) == 3 and mt["max_ms_per_step"] == max(mt["per_device_ms_per_step"])
+    assert all(v > 0 for v in mt["per_device_ms_per_step"])
+    assert len(line["roofline"]["per_device_gbs"]) == 3
+    assert line["sanity"]["ok"]
     from rmsf_amd.synth import motion_table
 
     mt = motion_table(1, 61) if align != "none" else None
@@ -38,9 +44,25 @@ def test_single_process_rehearsal_matches_oracle(align, capsys):
     assert abs(line["rmsf_checksum"] - float(exp.sum())) < 1e-6 * len(exp)
 
 
+def test_io_modes_small(capsys):
+    """modes.c4_share / modes.c5_xtc at reduced sizes: the one-process slab
+    step's timings and the XTC stream's figures, each with its sanity check
+    (rmsf_amd.synth.rmsf_sanity) passing."""
+    from rmsf_amd.engine import Engine
+    eng = Engine()
+    a = bench.parse(["--mode-steps", "2"])
+    c4 = bench.c4_share_mode(eng, a, 3.6, n_atoms=1_000_000, nf=33)
+    assert c4["accumulate_launches_per_step"] == 2          # two atom slabs
+    assert c4["sanity"]["ok"] and c4["ms_per_step"] > 0 and 0 < c4["accumulate_frac"] < 1
+    assert c4["exposed_merge_ms_per_step"] > 0
+    c5 = bench.c5_xtc_mode(eng, a, n_atoms=20000, nf=300)
+    assert c5["sanity"]["ok"] and c5["decode_kernel"]["all_frames_ok"]
+    assert c5["frames_per_s"] > 0 and c5["h2d_gbs"] > 0 and c5["decode_kernel"]["avg_ms"] > 0
+
+
 def test_bench_cli_small_json_line():
     cmd = [sys.executable, "bench.py", "--n-atoms", "20000", "--frames", "300", "--steps", "3", "--warmup", "1",
-           "--no-cpu-baseline", "--mode-steps", "1"]
+           "--no-cpu-baseline", "--mode-steps", "1", "--no-io-modes"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
