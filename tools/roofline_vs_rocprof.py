@@ -8,10 +8,11 @@
 that run's stdout (its JSON line).  For the line's dominant kernel
 (``roofline.kernel``) it reports
 
-  * the stats CSV average over every launch (warm-up included) and the
-    trace-derived average of the LAST ``steps`` launches (the timed ones:
-    bench.py's aligned modes launch other kernels, so the headline kernel's
-    last launches are the timed region's);
+  * the stats CSV average over every launch of that kernel name (warm-up
+    and later modes included: since round 5 the C4-share and C5 modes launch
+    the same kernel at other sizes) and the trace-derived average of the
+    headline's timed launches: the kernel's launches [warmup, warmup +
+    steps) in trace order (the headline runs first in bench.py);
   * frac recomputed from each as algorithmic bytes per launch (the line's
     ``algorithmic_bytes_per_launch``: 12 B per atom-frame)
     / duration / 8 TB/s, against the line's own frac (HIP events);
@@ -68,7 +69,8 @@ def main(argv):
         if row["Kernel_Name"] == stats["Name"]:
             launches.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
     launches.sort()
-    timed = launches[-steps:]
+    warm = int(line["warmup"])
+    timed = launches[warm:warm + steps]
     avg_all_ms = float(stats["AverageNs"]) / 1e6
     avg_timed_ms = sum(b - a for a, b in timed) / len(timed) / 1e6
     frac = lambda ms: bytes_launch / (ms / 1e3) / 1e9 / PEAK_GBS  # noqa: E731
@@ -78,7 +80,9 @@ def main(argv):
                  "avg_launch_ms": rf["avg_launch_ms"], "frac": rf["frac"], "achieved_gbs": rf["achieved"]},
         "rocprof_stats": {"calls": int(stats["Calls"]), "avg_ms": avg_all_ms, "min_ms": float(stats["MinNs"]) / 1e6,
                           "max_ms": float(stats["MaxNs"]) / 1e6, "frac": frac(avg_all_ms)},
-        "rocprof_timed_launches": {"n": len(timed), "avg_ms": avg_timed_ms, "frac": frac(avg_timed_ms)},
+        "rocprof_timed_launches": {"n": len(timed), "which": f"launches {warm}..{warm + steps - 1} of the kernel in "
+                                                             "trace order (the headline's timed region)",
+                                   "avg_ms": avg_timed_ms, "frac": frac(avg_timed_ms)},
         "algorithmic_bytes_per_launch": bytes_launch,
     }
     rel = abs(res["rocprof_timed_launches"]["frac"] - rf["frac"]) / rf["frac"]
