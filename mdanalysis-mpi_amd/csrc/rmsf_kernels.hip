@@ -514,6 +514,8 @@ __global__ __launch_bounds__(kBlock) void k_welford_seq(const float *__restrict_
   // the wave (one division per lane) and broadcasting them by v_readlane is
   // bit-identical but slower -- 4.98 vs 4.20 ms at 100k x 20k
   // (tools/ab_seq_lane.py, profiles/r05_workloads/seq_welford_lane.txt).
+  // A ring of 2-6 blocks (more loads in flight while one folds) spills
+  // SGPRs and loses 10-17 % (tools/ab_seq_ring.py, seq_welford_ring.txt).
   int64_t f = 0;
   if (nf >= U) {
     float a[U], b[U];

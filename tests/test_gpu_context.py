@@ -127,6 +127,8 @@ def test_context_group_in_process(c1, P, align):
     d, traj = c1
     if P == 120 and align is None:
         pytest.skip("one empty-rank case is enough")
+    import os
+    print(f"\n[P={P}] process threads before: {len(os.listdir('/proc/self/task'))}", flush=True)
     ctxs = [Context(traj.shape[1], sel=d["sel"]) for _ in range(P)]
     bl = blocks(98, P)
     if align:
