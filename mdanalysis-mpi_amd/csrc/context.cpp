@@ -642,28 +642,55 @@ int ensure_stager(rmsf_ctx *c) {
   return RMSF_OK;
 }
 
-// fn(i) for every context, each on its own worker thread (context 0 on the
-// calling thread); the first failure is reported on the calling thread.
+// fn(i) for every context, one host thread per DEVICE: the contexts of one
+// device run in context order on one thread (the worker of the device's
+// first context; context 0's device on the calling thread) -- they share that
+// device's queues, so more threads would only contend for them -- and the
+// devices' threads run at once, so N devices start their work together
+// instead of one after another behind a single thread's launch latency.  The
+// first failure (in context order) is reported on the calling thread.
 int for_each_ctx(rmsf_ctx **cs, int n, const std::function<int(int)> &fn) {
   if (n == 1) return fn(0);
-  // every worker exists before any job is posted: a job must never outlive
-  // this frame (it refers to fn)
-  for (int i = 1; i < n; ++i) {
-    if (!cs[i]->worker) cs[i]->worker = new (std::nothrow) Worker;
-    if (!cs[i]->worker) return fail(RMSF_ENOMEM, "rmsf_multi: cannot start a worker thread");
-  }
-  for (int i = 1; i < n; ++i) cs[i]->worker->post([&fn, i] { return fn(i); });
-  int rc = fn(0);
-  std::string msg = rc ? std::string(rmsf_last_error()) : std::string();
-  for (int i = 1; i < n; ++i) {
-    std::string e;
-    const int r = cs[i]->worker->wait(&e);
-    if (r && !rc) {
-      rc = r;
-      msg = e;
+  std::vector<std::vector<int>> groups;  // per device, in order of first appearance
+  std::vector<int> gdev;
+  for (int i = 0; i < n; ++i) {
+    size_t g = 0;
+    while (g < gdev.size() && gdev[g] != cs[i]->dev) ++g;
+    if (g == gdev.size()) {
+      gdev.push_back(cs[i]->dev);
+      groups.emplace_back();
     }
+    groups[g].push_back(i);
   }
-  return rc ? fail(rc, msg) : RMSF_OK;
+  std::vector<int> rcs(n, RMSF_OK);
+  std::vector<std::string> msgs(n);
+  auto run_group = [&](const std::vector<int> &grp) -> int {
+    for (int i : grp) {
+      rcs[i] = fn(i);
+      if (rcs[i] != RMSF_OK) {
+        msgs[i] = rmsf_last_error();
+        return rcs[i];
+      }
+    }
+    return RMSF_OK;
+  };
+  // every worker exists before any job is posted: a job must never outlive
+  // this frame (it refers to fn and the vectors above)
+  for (size_t g = 1; g < groups.size(); ++g) {
+    rmsf_ctx *c = cs[groups[g][0]];
+    if (!c->worker) c->worker = new (std::nothrow) Worker;
+    if (!c->worker) return fail(RMSF_ENOMEM, "rmsf_multi: cannot start a worker thread");
+  }
+  for (size_t g = 1; g < groups.size(); ++g)
+    cs[groups[g][0]]->worker->post([&run_group, &groups, g] { return run_group(groups[g]); });
+  run_group(groups[0]);
+  for (size_t g = 1; g < groups.size(); ++g) {
+    std::string e;
+    (void)cs[groups[g][0]]->worker->wait(&e);
+  }
+  for (int i = 0; i < n; ++i)
+    if (rcs[i] != RMSF_OK) return fail(rcs[i], msgs[i]);
+  return RMSF_OK;
 }
 
 // ---- cross-rank exchange ----------------------------------------------------

@@ -2140,6 +2140,7 @@ SkPlan sk_plan(int64_t lanes, int cpl, int64_t nf, int n_groups, int mode, int p
     // the split grid's locality (C4 at 1M x 20k: 38.1 vs 39.0 ms).
     S = std::max<int64_t>((nf + kCoefN - 1) / kCoefN, (kAccumBlocks + p.C - 1) / p.C);
     S = std::min<int64_t>(S, std::max<int64_t>(1, nf / kSkMinSeg));
+    if (const char *e = getenv("RMSF_SK_S")) S = std::max<int64_t>(1, atoi(e));  // TEMPORARY A/B (round 5)
     G = p.C * S;
   } else if (n_groups <= 0) {
     G = std::min<int64_t>(G, std::max<int64_t>(1, p.T / kSkMinSeg));
