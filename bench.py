@@ -477,7 +477,7 @@ def base_line(a, wl, n_gpus: int, dt: float, parallelism: str) -> dict:
 def main_single_process(a, wl, cpu) -> None:
     """``--gpus N`` with no WORLD_SIZE: one context per device, each device's
     RMSF.py:65-69 block generated in its HBM; every step pushes all blocks at
-    once (rmsf_multi_push_frames: one host thread per context, no host
+    once (rmsf_multi_push_frames: one host thread per device, no host
     synchronisation), then the contexts' merge -- the torchrun rank step's
     shape: one collective of moments about frame 0 (unaligned) or the
     reference (aligned), a reduce to context 0 with ``--merge root``

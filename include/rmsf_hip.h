@@ -754,7 +754,7 @@ int rmsf_multi_chan_merge_root(rmsf_ctx **ctxs, int n, int root);
 int rmsf_multi_chan_merge_exact(rmsf_ctx **ctxs, int n, int root, int order);
 /* Push each context's HBM frames d_frames[i] (n_frames[i] frames,
  * frame_stride floats apart, 0 = 3*n_atoms) in `mode`, the n contexts'
- * launches enqueued from one host thread per context (asynchronous: the
+ * launches enqueued from one host thread per device (asynchronous: the
  * frames must stay valid until the contexts are synchronised).  Per context,
  * first: flags & RMSF_MULTI_RESET resets the state `mode` accumulates into;
  * d_ref_frames[i] (device frame, may be NULL) sets the reference

@@ -20,7 +20,7 @@
 // folds and packs in one launch); a reset only marks the state, which is
 // zeroed if it is read before a fold overwrites it; rmsf_multi_push_frames
 // may record a push for the atom-slab merge, which any other call runs whole.
-// Host side: one worker thread per context for the rmsf_multi_* calls, a side
+// Host side: one worker thread per device for the rmsf_multi_* calls, a side
 // stream for digests and the shift frame's gather, a communicator stream for
 // the slab merge's collectives.
 #include <hip/hip_runtime.h>
@@ -845,7 +845,7 @@ int exchange_chan_shifted(rmsf_ctx **cs, int n, const Reduce &red, bool host_cou
   if (total == 0) return fail(RMSF_EEMPTY, "rmsf chan merge: no frames on any rank (RMSF.py:39 ZeroDivisionError)");
   const int64_t nc = cs[0]->n_coord;
   std::vector<double *> t(n);
-  // each context's pack (and below its finish) from its own worker thread:
+  // each context's pack (and below its finish) from its device's host thread:
   // with one device per context the launches leave in parallel
   CX_OK(for_each_ctx(cs, n, [&](int i) -> int {
     rmsf_ctx *c = cs[i];
@@ -1110,8 +1110,19 @@ int ensure_event(hipEvent_t *e) {
   return RMSF_OK;
 }
 
+// d's device may read s's memory directly (xGMI peer mapping) where the
+// platform allows; otherwise hipMemcpyPeerAsync stages the copy itself
+void enable_peer(int dev, int peer) {
+  if (dev == peer) return;
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, dev, peer) != hipSuccess || !can) return;
+  DeviceScope ds(dev);
+  if (hipDeviceEnablePeerAccess(peer, 0) != hipSuccess) (void)hipGetLastError();  // already enabled: fine
+}
+
 // d's stream copies s's Welford state (mean, M2) into d->xb after s's queued work
 int pull_state(rmsf_ctx *d, rmsf_ctx *s, int64_t nc) {
+  enable_peer(d->dev, s->dev);
   {
     DeviceScope ds(s->dev);
     CX_OK(ensure_event(&s->ev_sent));

@@ -2137,10 +2137,11 @@ SkPlan sk_plan(int64_t lanes, int cpl, int64_t nf, int n_groups, int mode, int p
     // several chunks put the resident workgroups on far-apart frames (a TLB
     // page per wave).  Cut every chunk into S equal frame ranges instead and
     // order them chunk-major, so resident workgroups share frame rows --
-    // the split grid's locality (C4 at 1M x 20k: 38.1 vs 39.0 ms).
+    // the split grid's locality (C4 at 1M x 20k: 38.1 vs 39.0 ms).  At C4's
+    // per-rank share (1M x 2,500) S = 1..4 are within 1 %, whole or in the
+    // merge's two slabs; S = 6 loses 4 % (profiles/r05_workloads/c4_share_s.txt).
     S = std::max<int64_t>((nf + kCoefN - 1) / kCoefN, (kAccumBlocks + p.C - 1) / p.C);
     S = std::min<int64_t>(S, std::max<int64_t>(1, nf / kSkMinSeg));
-    if (const char *e = getenv("RMSF_SK_S")) S = std::max<int64_t>(1, atoi(e));  // TEMPORARY A/B (round 5)
     G = p.C * S;
   } else if (n_groups <= 0) {
     G = std::min<int64_t>(G, std::max<int64_t>(1, p.T / kSkMinSeg));
