@@ -287,3 +287,28 @@ def test_context_exact_push_and_merge(red, P, root):
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 5, 6, 7, 8, 9, 16, 33])
+def test_abi_schedule_drives_oracle_fold(P):
+    """The C ABI's schedule (rmsf_chan_reduce_steps), applied on the host
+    with RMSF.py's second_order_moments and the kernels' empty-state rules
+    (T = 0 skipped, an empty side as zeros), equals the oracle's
+    chan_fold(order) bit for bit on random partials with empty ranks -- the
+    device schedule and the Python restatement of mpi4py agree."""
+    from rmsf_amd._lib import reduce_steps
+    rng = np.random.default_rng(P)
+    counts = [int(c) if rng.random() > 0.3 else 0 for c in rng.integers(1, 50, P)]
+    if sum(counts) == 0:
+        counts[-1] = 7
+    parts = [(c, rng.normal(20, 5, (6, 3)) if c else np.zeros((6, 3)), rng.uniform(0, 9, (6, 3)) if c
+              else np.zeros((6, 3))) for c in counts]
+    for order in ("mpi4py", "rank"):
+        S = list(parts)
+        for d, s in reduce_steps(P, order):
+            if S[d][0] + S[s][0] > 0:
+                S[d] = O.second_order_moments(S[d], S[s])
+        want = O.chan_fold(parts, order)
+        _same(S[0][1], want[1], f"{order} mean")
+        _same(S[0][2], want[2], f"{order} m2")
+        assert S[0][0] == want[0] == sum(counts)
