@@ -7,7 +7,10 @@
  *   rmsf_demo FRAMES.f32 N_FRAMES N_ATOMS SEL.i64|- N_SEL P MODE OUT.f64 [--rccl] [--device]
  *
  * FRAMES.f32: float32 [N_FRAMES][N_ATOMS][3]; SEL.i64: int64 [N_SEL] atom
- * indices ("-" = atoms 0..N_SEL-1); MODE: none | frame0 | average;
+ * indices ("-" = atoms 0..N_SEL-1); MODE: none | frame0 | average | exact
+ * (exact: RMSF.py:120-146 with the script's own arithmetic -- RMSF_PUSH_EXACT
+ * per block, the blocks reduced in mpi4py's comm.reduce order by
+ * rmsf_multi_chan_merge_exact, device to device);
  * OUT.f64: the RMSF, float64 [N_SEL].  Every context gets its RMSF.py:65-69
  * frame block (rmsf_block_range) and pushes it from host memory in two
  * halves (exercising the stager and the running Chan fold).  --device: each
@@ -56,7 +59,8 @@ int main(int argc, char **argv) {
     use_rccl |= strcmp(argv[a], "--rccl") == 0;
     on_device |= strcmp(argv[a], "--device") == 0;
   }
-  const int align = strcmp(mode, "none") != 0, average = strcmp(mode, "average") == 0;
+  const int exact = strcmp(mode, "exact") == 0;
+  const int align = strcmp(mode, "none") != 0 && !exact, average = strcmp(mode, "average") == 0;
   if (P < 1 || P > 64 || n_frames < 1) return 2;
 
   float *xyz = (float *)slurp(argv[1], sizeof(float) * 3 * (size_t)(n_frames * n_atoms));
@@ -77,7 +81,15 @@ int main(int argc, char **argv) {
   if (use_rccl) CHECK(rmsf_multi_init_all(ctx, P));
   const size_t fsz = 3 * (size_t)n_atoms;
   double *rmsf = (double *)malloc(sizeof(double) * (size_t)n_sel);
-  if (on_device) {
+  if (exact) {
+    for (int r = 0; r < P; ++r) { /* RMSF.py:120-138, the recurrence continued across the halves */
+      const int64_t n = b1[r] - b0[r], h = n / 2;
+      CHECK(rmsf_push_frames(ctx[r], xyz + b0[r] * fsz, h, 0, RMSF_PUSH_EXACT, 0));
+      CHECK(rmsf_push_frames(ctx[r], xyz + (b0[r] + h) * fsz, n - h, 0, RMSF_PUSH_EXACT, 0));
+    }
+    CHECK(rmsf_multi_chan_merge_exact(ctx, P, 0, RMSF_MERGE_MPI4PY)); /* RMSF.py:140-143 */
+    CHECK(rmsf_get_rmsf(ctx[0], rmsf));                               /* RMSF.py:145-146 */
+  } else if (on_device) {
     /* every block (and frame 0) in its context's HBM, then the one-process
      * step with no host synchronisation until the result */
     const float *d_block[64], *d_frame0[64];

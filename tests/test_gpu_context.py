@@ -208,7 +208,8 @@ def test_plain_c_host_program(c1, tmp_path):
     """mdanalysis-mpi_amd/lib/rmsf_demo: RMSF.py's script written against the
     C ABI alone, P contexts, host pushes in halves; --device: the blocks in
     HBM and the one-process step (rmsf_multi_push_frames +
-    rmsf_multi_chan_merge_root)."""
+    rmsf_multi_chan_merge_root); exact: RMSF_PUSH_EXACT and
+    rmsf_multi_chan_merge_exact, the script's own bits."""
     d, traj = c1
     exe = os.path.join(PKG, "lib", "rmsf_demo")
     f = tmp_path / "traj.f32"
@@ -228,6 +229,14 @@ def test_plain_c_host_program(c1, tmp_path):
         assert r.returncode == 0, r.stderr
         assert r.stdout.count("Process:") == P
         np.testing.assert_allclose(np.fromfile(out, dtype=np.float64), d[tag], rtol=0, atol=TOL)
+    # exact: RMSF_PUSH_EXACT + rmsf_multi_chan_merge_exact (mpi4py's order), bit for bit
+    for P in (1, 4, 5):
+        out = tmp_path / f"rmsf_{P}_exact.f64"
+        r = subprocess.run([exe, str(f), "98", str(traj.shape[1]), str(s), "214", str(P), "exact", str(out)],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        want = O.rmsf_script(traj, d["sel"], None, size=P, align=None, merge_order="mpi4py")["rmsf"]
+        np.testing.assert_array_equal(np.fromfile(out, dtype=np.float64).view(np.uint64), want.view(np.uint64))
 
 
 # ---- callback transport across processes (gloo on cuda:0) -------------------
