@@ -16,19 +16,23 @@ import torch  # noqa: E402
 from rmsf_amd.engine import Engine  # noqa: E402
 from rmsf_amd.synth import generate  # noqa: E402
 
+ENV = os.environ.get("AB_SWITCH", "RMSF_SEQ_RING")  # RMSF_SEQ_BUF: the buffer-load ring (contiguous only)
 VARIANTS = sys.argv[1:] or ["kept", "82", "84", "86", "44", "48", "64"]
 
 
 def setv(v):
     if v == "kept":
-        os.environ.pop("RMSF_SEQ_RING", None)
+        os.environ.pop(ENV, None)
     else:
-        os.environ["RMSF_SEQ_RING"] = v
+        os.environ[ENV] = v
 
 
 eng = Engine()
 nf = 20_000
-for label, n_atoms, n_sel in (("contiguous 100k", 100_000, 100_000), ("gathered 100k of 120k", 120_000, 100_000)):
+CASES = (("contiguous 100k", 100_000, 100_000), ("gathered 100k of 120k", 120_000, 100_000))
+if os.environ.get("AB_CONTIGUOUS_ONLY"):
+    CASES = CASES[:1]
+for label, n_atoms, n_sel in CASES:
     traj = generate(eng, n_atoms, 0, nf, seed=0)
     sel = None if n_sel == n_atoms else eng.sel_tensor(np.sort(np.random.default_rng(1).choice(n_atoms, n_sel,
                                                                                               replace=False)))
