@@ -515,7 +515,9 @@ __global__ __launch_bounds__(kBlock) void k_welford_seq(const float *__restrict_
   // bit-identical but slower -- 4.98 vs 4.20 ms at 100k x 20k
   // (tools/ab_seq_lane.py, profiles/r05_workloads/seq_welford_lane.txt).
   // A ring of 2-6 blocks (more loads in flight while one folds) spills
-  // SGPRs and loses 10-17 % (tools/ab_seq_ring.py, seq_welford_ring.txt).
+  // SGPRs and loses 10-17 % (tools/ab_seq_ring.py, seq_welford_ring.txt);
+  // the same ring over raw buffer loads (no per-frame address SGPRs, no
+  // spills) ties with this form, -1.3 to +4 % (seq_welford_buf.txt).
   int64_t f = 0;
   if (nf >= U) {
     float a[U], b[U];
@@ -541,84 +543,6 @@ __global__ __launch_bounds__(kBlock) void k_welford_seq(const float *__restrict_
     }
   }
   for (; f < nf; ++f) step(__builtin_nontemporal_load(p + f * fstride), coef[f], (double)(k0 + f));
-  mean[j] = m;
-  ss[j] = q;
-}
-
-// EXPERIMENT (round 5): the contiguous sequential Welford with its frames
-// read by raw buffer loads -- a per-block resource at the block's first
-// frame, the lane's byte offset in a VGPR and the frame's offset u * stride
-// as a scalar offset -- so the frames in flight cost no 64-bit address
-// registers, and a ring of NB blocks of U frames can stay in flight; one
-// coefficient block in SGPRs, reloaded right after its last use.
-template <int U, int NB>
-__global__ __launch_bounds__(kBlock) void k_welford_seq_buf(const float *__restrict__ xyz, int64_t fstride, int64_t nf,
-                                                            int64_t n_coord, int64_t k0,
-                                                            const SeqCoef *__restrict__ coef,
-                                                            double *__restrict__ mean, double *__restrict__ ss) {
-  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (j >= n_coord) return;
-  double m = k0 > 0 ? mean[j] : 0.0, q = k0 > 0 ? ss[j] : 0.0;
-  const int64_t jw = uni64(j - (int64_t)(threadIdx.x & 63));  // the wave's first coordinate
-  const int vo = (int)(threadIdx.x & 63) * 4;                  // the lane's byte offset
-  const int st4 = (int)(fstride * 4);                          // frame stride in bytes (host-checked)
-  auto step = [&](float v, const SeqCoef cf, double k) {
-    const double x = (double)v;
-    const double d = x - m;
-    q = q + cf.c * (d * d);
-    m = seq_div(k * m + x, k + 1.0, cf.r);
-  };
-  auto step_fast = [&](float v, const SeqCoef cf, double k) {
-    const double x = (double)v;
-    const double d = x - m;
-    q = q + cf.c * (d * d);
-    const double num = k * m + x, k1 = k + 1.0;
-    const double q0 = num * cf.r;
-    m = __builtin_fma(__builtin_fma(-k1, q0, num), cf.r, q0);
-  };
-  const int64_t nb = nf / U;
-  float v[NB][U];
-  SeqCoef c[U];
-  auto loadv = [&](float (&w)[U], int64_t blk) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(xyz + jw + blk * U * fstride), (short)0, 0x7fffffff, 0x00020000);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      w[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, u * st4, 2));
-  };
-  auto loadc = [&](int64_t blk) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) c[u] = coef[blk * U + u];
-  };
-  auto run = [&](const float (&w)[U], int64_t f) {
-    const double kb = (double)(k0 + f);
-    bool special = __builtin_isinf(m);
-#pragma unroll
-    for (int u = 0; u < U; ++u) special |= (w[u] == 0.0f) | __builtin_isinf(w[u]);
-    if (!__any((int)special)) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) step_fast(w[u], c[u], kb + (double)u);
-      return;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) step(w[u], c[u], kb + (double)u);
-  };
-#pragma unroll
-  for (int i = 0; i < NB; ++i)
-    if (i < nb) loadv(v[i], i);
-  if (nb > 0) loadc(0);
-  for (int64_t b0 = 0; b0 < nb; b0 += NB) {
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int64_t b = b0 + i;
-      if (b < nb) {
-        run(v[i], b * U);
-        if (b + 1 < nb) loadc(b + 1);
-        if (b + NB < nb) loadv(v[i], b + NB);
-      }
-    }
-  }
-  for (int64_t f = nb * U; f < nf; ++f) step(__builtin_nontemporal_load(xyz + j + f * fstride), coef[f], (double)(k0 + f));
   mean[j] = m;
   ss[j] = q;
 }
@@ -2726,26 +2650,6 @@ RMSF_EXPORT int rmsf_welford_sequential(const float *d_xyz, int64_t fstride, int
   // (100k x 20k: 4.25 ms at 1 coordinate per lane, 4.74 at 2, 5.45 at 4;
   // DESIGN section 4)
   const int64_t n_coord = 3 * n_sel;
-  // TEMPORARY A/B switch (round 5): RMSF_SEQ_BUF=<U><NB> (contiguous only)
-  const char *ev = getenv("RMSF_SEQ_BUF");
-  const int bufv = ev ? atoi(ev) : 0;
-  if (!d_sel && bufv && fstride * 4 * 16 < (int64_t(1) << 31)) {
-#define BUFV(U_, NB_)                                                                                          \
-    if (bufv == U_ * 10 + NB_) {                                                                               \
-      hipLaunchKernelGGL((k_welford_seq_buf<U_, NB_>), dim3(grid1(n_coord)), dim3(kBlock), 0, s, d_xyz, fstride, \
-                         n_frames, n_coord, k0, coef, d_mean, d_sumsquares);                                     \
-      return after_launch("k_welford_seq_buf");                                                                \
-    }
-    BUFV(8, 2)
-    BUFV(8, 3)
-    BUFV(8, 4)
-    BUFV(4, 4)
-    BUFV(4, 6)
-    BUFV(4, 8)
-    BUFV(6, 4)
-    BUFV(16, 2)
-#undef BUFV
-  }
   if (d_sel)
     hipLaunchKernelGGL((k_welford_seq<kSeqU, true>), dim3(grid1(n_coord)), dim3(kBlock), 0, s, d_xyz, fstride,
                        n_frames, n_coord, d_sel, k0, coef, d_mean, d_sumsquares);

@@ -16,7 +16,7 @@ import torch  # noqa: E402
 from rmsf_amd.engine import Engine  # noqa: E402
 from rmsf_amd.synth import generate  # noqa: E402
 
-ENV = os.environ.get("AB_SWITCH", "RMSF_SEQ_RING")  # RMSF_SEQ_BUF: the buffer-load ring (contiguous only)
+ENV = os.environ.get("AB_SWITCH", "RMSF_SEQ_RING")  # RMSF_SEQ_BUF: the buffer-load ring (both switches since removed)
 VARIANTS = sys.argv[1:] or ["kept", "82", "84", "86", "44", "48", "64"]
 
 
