@@ -98,6 +98,9 @@ def parse(argv=None):
                     help="frames per CPU process for the RMSF.py two-sweep baseline sample")
     ap.add_argument("--no-modes", action="store_true", help="skip the aligned-mode measurements at N=1")
     ap.add_argument("--mode-steps", type=int, default=3)
+    ap.add_argument("--mode-warmup", type=int, default=3,
+                    help="untimed steps before each mode's timed steps (the first 2-3 exact runs of a fresh "
+                         "process are 5-15 %% slower: tools/probe_seq_bench.py)")
     ap.add_argument("--no-io-modes", action="store_true",
                     help="N=1: skip the C4-share and C5-XTC modes (30 GB of frames, a 2.7 GB XTC file)")
     ap.add_argument("--stager-threads", type=int, default=4)
@@ -317,7 +320,8 @@ def c4_share_mode(eng, a, headline_avg_ms: float | None, n_atoms: int = 1_000_00
                                       after_torch=False)
             Context.multi_chan_merge([c], root=0)
 
-        step()
+        for _ in range(max(1, a.mode_warmup)):
+            step()
         for w in ("accumulate", "merge"):
             c.kernel_time(w)
         t0 = time.perf_counter()
@@ -799,7 +803,8 @@ def main():
         def run_exact(timer=None):
             return run_pipeline(eng, src, fl, block=(b0, b1), max_batch=a.batch_frames, timer=timer, exact=True)
 
-        run_exact()
+        for _ in range(max(1, a.mode_warmup)):
+            run_exact()
         torch.cuda.synchronize()
         xt = KernelTimer()
         t0 = time.perf_counter()
@@ -826,7 +831,7 @@ def main():
         src = DeviceSource(traj, offset=b0, n_traj=n_total)
         modes = {"c2_exact": exact_mode}
         for name, align in (("c3_frame0", "frame0"), ("rmsf_py_average", "average")):
-            mdt, mt, mres = timed(align, a.mode_steps, 1)
+            mdt, mt, mres = timed(align, a.mode_steps, max(1, a.mode_warmup))
             sweeps = 2 if align == "average" else 1
             af = n_total * n_atoms * a.mode_steps / mdt
             k_s, s_ms, s_af = mt.totals("superpose")
