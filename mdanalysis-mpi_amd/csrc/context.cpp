@@ -141,6 +141,14 @@ struct DevBuf {
   // so it is drained first (keep: the old contents are carried over)
   int ensure(size_t need, hipStream_t s, bool keep = false) {
     if (need <= bytes) return RMSF_OK;
+    // the buffer is allocated on the current device: it must be the stream's
+    // (a context's buffers live on its own device; a caller that forgot its
+    // DeviceScope would hand the kernels another device's pointer)
+    int cur = -1;
+    hipDevice_t sd = -1;
+    if (s && hipGetDevice(&cur) == hipSuccess && hipStreamGetDevice(s, &sd) == hipSuccess && sd != cur)
+      return fail(RMSF_EHIP, "internal: buffer for a device-" + std::to_string(sd) + " stream allocated while device " +
+                                 std::to_string(cur) + " is current");
     if (p) {
       hipError_t e0 = hipStreamSynchronize(s);
       if (e0 != hipSuccess) return fail(RMSF_EHIP, std::string("hipStreamSynchronize: ") + hipGetErrorString(e0));

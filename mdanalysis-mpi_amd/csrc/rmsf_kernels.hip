@@ -467,12 +467,12 @@ __global__ __launch_bounds__(kBlock) void k_welford_seq(const float *__restrict_
   // RMSF.py:119-120: np.zeros; later batches continue the running state
   double m = k0 > 0 ? mean[j] : 0.0, q = k0 > 0 ? ss[j] : 0.0;
   const float *__restrict__ p = xyz + (GATHER ? 3 * (int64_t)sel[j / 3] + j % 3 : j);
-  // k = k0 + f exactly (integers below 2^53)
-  auto step = [&](float v, const SeqCoef cf, double k) {
+  // k = k0 + f and k1 = k + 1 exactly (integers below 2^53)
+  auto step = [&](float v, const SeqCoef cf, double k, double k1) {
     const double x = (double)v;
     const double d = x - m;
     q = q + cf.c * (d * d);
-    m = seq_div(k * m + x, k + 1.0, cf.r);
+    m = seq_div(k * m + x, k1, cf.r);
   };
   auto load = [&](float (&v)[U], SeqCoef (&c)[U], int64_t f) {
 #pragma unroll
@@ -486,26 +486,33 @@ __global__ __launch_bounds__(kBlock) void k_welford_seq(const float *__restrict_
   // finite and nonzero, or an exact cancellation to +0 that the closing steps
   // also return as +0 (-0 needs x = -0).  Checked once per block and wave:
   // 2 % faster at 100k x 20k, the same bits (tools/ab_seq_hoist.py).
-  auto step_fast = [&](float v, const SeqCoef cf, double k) {
+  auto step_fast = [&](float v, const SeqCoef cf, double k, double k1) {
     const double x = (double)v;
     const double d = x - m;
     q = q + cf.c * (d * d);
-    const double num = k * m + x, k1 = k + 1.0;
+    const double num = k * m + x;
     const double q0 = num * cf.r;
     m = __builtin_fma(__builtin_fma(-k1, q0, num), cf.r, q0);
   };
-  auto run = [&](const float (&v)[U], const SeqCoef (&c)[U], int64_t f) {
-    const double kb = (double)(k0 + f);
+  // kb = k0 + f carried across blocks: the block's U + 1 frame counts cost U
+  // adds (frame u's k + 1 is frame u + 1's k), not a 64-bit conversion and
+  // 2U - 1 adds
+  auto run = [&](const float (&v)[U], const SeqCoef (&c)[U], double &kb) {
+    double kk[U + 1];
+    kk[0] = kb;
+#pragma unroll
+    for (int u = 1; u <= U; ++u) kk[u] = kb + (double)u;
+    kb = kk[U];
     bool special = __builtin_isinf(m);
 #pragma unroll
     for (int u = 0; u < U; ++u) special |= (v[u] == 0.0f) | __builtin_isinf(v[u]);
     if (!__any((int)special)) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) step_fast(v[u], c[u], kb + (double)u);
+      for (int u = 0; u < U; ++u) step_fast(v[u], c[u], kk[u], kk[u + 1]);
       return;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) step(v[u], c[u], kb + (double)u);
+    for (int u = 0; u < U; ++u) step(v[u], c[u], kk[u], kk[u + 1]);
   };
   // two register blocks in turn, one always loading while the other folds
   // (no copies between them: a copy makes the compiler wait on the
@@ -517,32 +524,35 @@ __global__ __launch_bounds__(kBlock) void k_welford_seq(const float *__restrict_
   // A ring of 2-6 blocks (more loads in flight while one folds) spills
   // SGPRs and loses 10-17 % (tools/ab_seq_ring.py, seq_welford_ring.txt);
   // the same ring over raw buffer loads (no per-frame address SGPRs, no
-  // spills) ties with this form, -1.3 to +4 % (seq_welford_buf.txt).
+  // spills) ties with this form, -1.3 to +4 % (seq_welford_buf.txt), and so
+  // do this form's two blocks read by buffer loads (+1 %, 7 % fewer VALU
+  // instructions, seq_welford_kk.txt).
   int64_t f = 0;
+  double kb = (double)k0;
   if (nf >= U) {
     float a[U], b[U];
     SeqCoef ca[U], cb[U];
     load(a, ca, 0);
     for (;;) {
       if (f + 2 * U > nf) {
-        run(a, ca, f);
+        run(a, ca, kb);
         f += U;
         break;
       }
       load(b, cb, f + U);
-      run(a, ca, f);
+      run(a, ca, kb);
       f += U;
       if (f + 2 * U > nf) {
-        run(b, cb, f);
+        run(b, cb, kb);
         f += U;
         break;
       }
       load(a, ca, f + U);
-      run(b, cb, f);
+      run(b, cb, kb);
       f += U;
     }
   }
-  for (; f < nf; ++f) step(__builtin_nontemporal_load(p + f * fstride), coef[f], (double)(k0 + f));
+  for (; f < nf; ++f, kb += 1.0) step(__builtin_nontemporal_load(p + f * fstride), coef[f], kb, kb + 1.0);
   mean[j] = m;
   ss[j] = q;
 }

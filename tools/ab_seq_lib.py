@@ -70,8 +70,8 @@ def main():
         same = all(np.array_equal(bits(out["old"][i]), bits(out["new"][i])) for i in (0, 1))
         ok &= same
         o, n = float(np.median(t["old"])), float(np.median(t["new"]))
-        print(f"{label} x {nf}: old {o:.3f} ms ({12 * n_sel * nf / o / 1e9 / 8000:.3f} of 8 TB/s)  "
-              f"new {n:.3f} ms ({12 * n_sel * nf / n / 1e9 / 8000:.3f})  {(n / o - 1) * 100:+.1f} %  "
+        print(f"{label} x {nf}: old {o:.3f} ms ({12 * n_sel * nf / (o / 1e3) / 1e9 / 8000:.3f} of 8 TB/s)  "
+              f"new {n:.3f} ms ({12 * n_sel * nf / (n / 1e3) / 1e9 / 8000:.3f})  {(n / o - 1) * 100:+.1f} %  "
               f"bits equal {same}", flush=True)
         print(f"   old [{' '.join(f'{x:.3f}' for x in t['old'])}]\n   new [{' '.join(f'{x:.3f}' for x in t['new'])}]",
               flush=True)
