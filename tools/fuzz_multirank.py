@@ -8,8 +8,9 @@ random rank (merge_root); ``--planes``: half the shards are HBM coordinate
 planes; ``--scatter``: a third of the other cases merge as a reduce-scatter
 by atom slices with the RMSF gathered to a random root (merge_scatter);
 ``--exact``: half the unaligned cases run exact=True and must equal the
-oracle's P-rank script bit for bit.
-python tools/fuzz_multirank.py [n_cases [--root] [--planes] [--scatter] [--exact]]"""
+oracle's P-rank script bit for bit (``--exact-wide``: those with 4-6 ranks,
+the default mpi4py reduce order, frames possibly fewer than ranks).
+python tools/fuzz_multirank.py [n_cases [--root] [--planes] [--scatter] [--exact [--exact-wide]]]"""
 import os
 import sys
 import tempfile
@@ -103,6 +104,10 @@ def main():
             case["root"] = int(rng.integers(0, P))
         if "--exact" in sys.argv[2:] and align is None and not big and not case.get("scatter") and rng.random() < 0.5:
             case["exact"] = True  # RMSF.py's own arithmetic: bit for bit with the oracle's P-rank script
+            if "--exact-wide" in sys.argv[2:]:
+                # 4-6 ranks, where mpi4py's reduce tree and rank order differ
+                # in bits; frames may be fewer than ranks (empty blocks)
+                P = case["P"] = int(rng.integers(4, 7))
         out = run_case(case)
         if any(o[2] == -1 for o in out):
             print(f"case {k}: FAILED {[o[1] for o in out if o[2] == -1][:1]}", flush=True)
