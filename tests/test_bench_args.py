@@ -13,6 +13,9 @@ def test_default_is_strong_scaling_of_c2():
     assert wl["scaling"] == "strong" and wl["n_total"] == 20_000 and wl["n_atoms"] == 100_000
     assert wl["align"] is None
     assert bench.resolve(bench.parse([]), 1)["n_total"] == 20_000
+    # the N = 1 modes: 3 untimed steps before their 3 timed ones
+    d = bench.parse([])
+    assert d.mode_warmup == 3 and d.mode_steps == 3
 
 
 def test_weak_scaling_and_c4():
