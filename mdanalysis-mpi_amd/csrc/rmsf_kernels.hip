@@ -557,6 +557,112 @@ __global__ __launch_bounds__(kBlock) void k_welford_seq(const float *__restrict_
   ss[j] = q;
 }
 
+// The gathered recurrence with one selected atom per lane (round 5): its
+// three coordinates are three independent chains, the frame's row is one
+// dwordx3 load per atom, and a wave gathers 64 atoms per load instruction
+// instead of 21 -- a third of the address work for the texture path, which
+// bounds the coordinate-per-lane gather (0.47 of HBM at 100k of 120k atoms).
+// A third of the waves, too: it pays from ~50k selected atoms (0.75 waves
+// per SIMD) and loses below (profiles/r05_workloads/seq_welford_atoms.txt).
+// Same operations per coordinate as k_welford_seq, so the same bits.
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_welford_seq_atoms(const float *__restrict__ xyz, int64_t fstride,
+                                                              int64_t nf, int64_t n_sel,
+                                                              const int32_t *__restrict__ sel, int64_t k0,
+                                                              const SeqCoef *__restrict__ coef,
+                                                              double *__restrict__ mean, double *__restrict__ ss) {
+  const int64_t a = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (a >= n_sel) return;
+  double m[3], q[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    m[c] = k0 > 0 ? mean[3 * a + c] : 0.0;
+    q[c] = k0 > 0 ? ss[3 * a + c] : 0.0;
+  }
+  const float *__restrict__ p = xyz + 3 * (int64_t)sel[a];
+  auto step = [&](int c, float v, const SeqCoef cf, double k, double k1) {
+    const double x = (double)v;
+    const double d = x - m[c];
+    q[c] = q[c] + cf.c * (d * d);
+    m[c] = seq_div(k * m[c] + x, k1, cf.r);
+  };
+  auto step_fast = [&](int c, float v, const SeqCoef cf, double k, double k1) {
+    const double x = (double)v;
+    const double d = x - m[c];
+    q[c] = q[c] + cf.c * (d * d);
+    const double num = k * m[c] + x;
+    const double q0 = num * cf.r;
+    m[c] = __builtin_fma(__builtin_fma(-k1, q0, num), cf.r, q0);
+  };
+  auto load = [&](float (&v)[U][3], SeqCoef (&cc)[U], int64_t f) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float *r = p + (f + u) * fstride;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[u][c] = __builtin_nontemporal_load(r + c);
+      cc[u] = coef[f + u];
+    }
+  };
+  auto run = [&](const float (&v)[U][3], const SeqCoef (&cc)[U], double &kb) {
+    double kk[U + 1];
+    kk[0] = kb;
+#pragma unroll
+    for (int u = 1; u <= U; ++u) kk[u] = kb + (double)u;
+    kb = kk[U];
+    bool special = __builtin_isinf(m[0]) | __builtin_isinf(m[1]) | __builtin_isinf(m[2]);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) special |= (v[u][c] == 0.0f) | __builtin_isinf(v[u][c]);
+    if (!__any((int)special)) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) step_fast(c, v[u][c], cc[u], kk[u], kk[u + 1]);
+      return;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) step(c, v[u][c], cc[u], kk[u], kk[u + 1]);
+  };
+  int64_t f = 0;
+  double kb = (double)k0;
+  if (nf >= U) {
+    float va[U][3], vb[U][3];
+    SeqCoef ca[U], cb[U];
+    load(va, ca, 0);
+    for (;;) {
+      if (f + 2 * U > nf) {
+        run(va, ca, kb);
+        f += U;
+        break;
+      }
+      load(vb, cb, f + U);
+      run(va, ca, kb);
+      f += U;
+      if (f + 2 * U > nf) {
+        run(vb, cb, kb);
+        f += U;
+        break;
+      }
+      load(va, ca, f + U);
+      run(vb, cb, kb);
+      f += U;
+    }
+  }
+  for (; f < nf; ++f, kb += 1.0) {
+    const float *r = p + f * fstride;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) step(c, __builtin_nontemporal_load(r + c), coef[f], kb, kb + 1.0);
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    mean[3 * a + c] = m[c];
+    ss[3 * a + c] = q[c];
+  }
+}
+
 template <int MODE, bool ALIGN, bool GATHER, int U, bool PLANES = false>
 __global__ __launch_bounds__(kBlock) void k_accum_atoms_sk(const float *__restrict__ xyz, int64_t fstride,
                                                            const int32_t *__restrict__ sel,
@@ -2129,6 +2235,12 @@ constexpr int kQWel = 2, kSkPerCuSplitWel = 8, kQSum = 4, kSkPerCuSplitSum = 4;
 // Sequential Welford (k_welford_seq): frames per register block (two blocks
 // in turn: 8 frames folding while the next 8 load; 4, 6 and 12 are slower).
 constexpr int kSeqU = 8;
+// gathered selections of >= kSeqAtomsMinSel atoms: one atom per lane, blocks
+// of 4 frames (100k of 120k atoms x 20k frames: 5.01 ms against 6.30 for the
+// coordinate-per-lane gather; 8 frames 5.28, 2 frames 5.18; 20k atoms: 2x
+// slower, too few waves -- profiles/r05_workloads/seq_welford_atoms.txt)
+constexpr int kSeqAtomsU = 4;
+constexpr int64_t kSeqAtomsMinSel = 49152;
 
 
 // Balanced-grid plan for `lanes` lanes (cpl coordinates each) over nf frames.
@@ -2658,8 +2770,14 @@ RMSF_EXPORT int rmsf_welford_sequential(const float *d_xyz, int64_t fstride, int
   // one coordinate per lane: the recurrence is serial in frames, so the
   // coordinates are the only parallelism, and more waves beat wider loads
   // (100k x 20k: 4.25 ms at 1 coordinate per lane, 4.74 at 2, 5.45 at 4;
-  // DESIGN section 4)
+  // DESIGN section 4) -- except a large gathered selection, where the
+  // gather's address work bounds the stream and one atom per lane wins
   const int64_t n_coord = 3 * n_sel;
+  if (d_sel && n_sel >= kSeqAtomsMinSel) {
+    hipLaunchKernelGGL((k_welford_seq_atoms<kSeqAtomsU>), dim3(grid1(n_sel)), dim3(kBlock), 0, s, d_xyz, fstride,
+                       n_frames, n_sel, d_sel, k0, coef, d_mean, d_sumsquares);
+    return after_launch("k_welford_seq_atoms");
+  }
   if (d_sel)
     hipLaunchKernelGGL((k_welford_seq<kSeqU, true>), dim3(grid1(n_coord)), dim3(kBlock), 0, s, d_xyz, fstride,
                        n_frames, n_coord, d_sel, k0, coef, d_mean, d_sumsquares);

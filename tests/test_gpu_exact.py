@@ -29,7 +29,9 @@ def _same(got, want, what):
 
 
 @pytest.mark.parametrize("n_atoms,nf,gather", [(4096, 700, False), (1001, 333, True), (5, 40, False),
-                                               (3, 1, False), (257, 4097, True)])
+                                               (3, 1, False), (257, 4097, True),
+                                               # >= 49,152 selected atoms: the atom-per-lane gather
+                                               (160_000, 37, True), (150_000, 9, True)])
 def test_sequential_kernel_is_rmsf_py_recurrence(n_atoms, nf, gather):
     from rmsf_amd.engine import Engine
     from rmsf_amd.synth import generate
@@ -219,25 +221,32 @@ def test_rmsf_exact_one_process_devices(inp, gpus):
     _same(r.sumsquares, want["m2"], "sumsquares")
 
 
-def test_sequential_special_values():
+@pytest.mark.parametrize("n_atoms,n_sel", [(64, None), (60_000, 50_000)])
+def test_sequential_special_values(n_atoms, n_sel):
     """Zeros (both signs), infinities and NaNs in the frames: the fast
     division's select passes zero and infinity numerators through, NaN
     propagates -- the reference recurrence's values wherever it has a
-    number, NaN wherever it has NaN."""
+    number, NaN wherever it has NaN.  (60,000 atoms, 50,000 selected: the
+    atom-per-lane gather.)"""
     from rmsf_amd.engine import Engine
     eng = Engine()
-    n_atoms, nf = 64, 50
+    nf = 50
     traj = SY.frames(3, n_atoms, 0, nf)
     rng = np.random.default_rng(9)
+    sel = np.arange(n_atoms) if n_sel is None else \
+        np.union1d([5, 6], rng.choice(n_atoms, n_sel - 2, replace=False))[:n_sel]
     for v in (0.0, -0.0, np.inf, -np.inf, np.nan):
-        idx = rng.integers(0, nf, 6), rng.integers(0, n_atoms, 6), rng.integers(0, 3, 6)
+        k = 6 if n_sel is None else 400
+        idx = rng.integers(0, nf, k), rng.integers(0, n_atoms, k), rng.integers(0, 3, k)
         traj[idx] = np.float32(v)
     traj[:, 5, 0] = 0.0            # a column that is zero throughout
     traj[:, 6, 1] = -0.0           # ... and negative zero throughout
-    S = O.rank_sweep2(traj, np.arange(n_atoms), None, 0, nf)
+    S = O.rank_sweep2(traj, sel, None, 0, nf)
     x = torch.tensor(traj, device="cuda")
-    m, q = eng.empty(3 * n_atoms), eng.empty(3 * n_atoms)
-    eng.welford_sequential(x.data_ptr(), 3 * n_atoms, nf, n_atoms, None, 0, m, q)
+    ns = len(sel)
+    m, q = eng.empty(3 * ns), eng.empty(3 * ns)
+    eng.welford_sequential(x.data_ptr(), 3 * n_atoms, nf, ns, None if n_sel is None else eng.sel_tensor(sel), 0,
+                           m, q)
     torch.cuda.synchronize()
     for got, want, what in ((m.cpu().numpy(), S[1].reshape(-1), "mean"), (q.cpu().numpy(), S[2].reshape(-1),
                                                                          "sumsquares")):

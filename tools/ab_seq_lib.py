@@ -4,7 +4,8 @@ builds of the library in one process: tools/_ab/librmsf_old.so and the
 current one.  HIP-event medians of alternating rounds at 100k x 20k
 (contiguous) and 100k-of-120k atoms (gathered); (mean, sumsquares) compared
 bit for bit there, on ragged frame counts / nonzero k0, and on frames with
-zeros, infinities and NaN (the per-block slow path).
+zeros, infinities and NaN (the per-block slow path), all rows and a
+gathered selection.
   python tools/ab_seq_lib.py [--old LIB] [--new LIB] [--reps 7]"""
 import argparse
 import ctypes
@@ -34,6 +35,7 @@ def main():
     ap.add_argument("--old", default=os.path.join(ROOT, "tools", "_ab", "librmsf_old.so"))
     ap.add_argument("--new", default=LIB_PATH)
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--shapes", action="store_true", help="a sweep of selection sizes and densities instead")
     a = ap.parse_args()
     libs = {"old": lib(a.old), "new": lib(a.new)}
     eng = Engine()
@@ -47,9 +49,23 @@ def main():
     def bits(t):
         return t.cpu().numpy().view(np.uint64)
 
+    def same_bits(a, b):
+        """bit for bit, NaN payloads aside (the NaN pattern must match; as
+        tests/test_gpu_exact.py compares specials)"""
+        fa, fb = a.view(np.float64), b.view(np.float64)
+        na, nb = np.isnan(fa), np.isnan(fb)
+        return bool(np.array_equal(na, nb) and np.array_equal(a[~na], b[~nb]))
+
     ok = True
-    nf = 20_000
-    for label, n_atoms, n_sel in (("contiguous 100k", 100_000, 100_000), ("gathered 100k of 120k", 120_000, 100_000)):
+    cases = (("contiguous 100k", 100_000, 100_000, 20_000),
+             ("gathered 100k of 120k", 120_000, 100_000, 20_000),
+             ("sparse (CA-like) 20k of 300k", 300_000, 20_000, 5_000))
+    if a.shapes:
+        cases = (("dense 20k of 24k", 24_000, 20_000, 20_000), ("dense 50k of 60k", 60_000, 50_000, 10_000),
+                 ("contiguous 20k", 20_000, 20_000, 20_000), ("contiguous 50k", 50_000, 50_000, 10_000),
+                 ("third 100k of 300k", 300_000, 100_000, 4_000), ("sparse 100k of 1.5M", 1_500_000, 100_000, 800),
+                 ("sparse 50k of 750k", 750_000, 50_000, 1_600), ("half 200k of 400k", 400_000, 200_000, 3_000))
+    for label, n_atoms, n_sel, nf in cases:
         traj = generate(eng, n_atoms, 0, nf, seed=0)
         sel = None if n_sel == n_atoms else eng.sel_tensor(np.sort(np.random.default_rng(1).choice(
             n_atoms, n_sel, replace=False)))
@@ -77,6 +93,9 @@ def main():
               flush=True)
         del traj, work
         torch.cuda.empty_cache()
+    if a.shapes:
+        print("full-size shapes bit-equal:", ok, flush=True)
+        return 0 if ok else 1
     # ragged frame counts, nonzero k0, continuing state; then special values
     traj = generate(eng, 5000, 0, 700, seed=3)
     h = traj.cpu().numpy()
@@ -87,20 +106,22 @@ def main():
         hs.reshape(-1)[idx] = val
     trajs = torch.tensor(hs.reshape(h.shape), device=eng.device)
     work = eng.empty(libs["new"].rmsf_welford_sequential_workspace_bytes(700) // 8 + 2)
+    gsel = eng.sel_tensor(np.sort(rng.choice(5000, 1777, replace=False)))
     for name, tr in (("plain", traj), ("zeros/inf/nan", trajs)):
-        for nf2, k0 in ((1, 0), (7, 0), (8, 0), (15, 3), (16, 0), (17, 9), (31, 5), (33, 64), (129, 1000),
-                        (700, 3), (700, 0)):
-            res = {}
-            for k in libs:
-                mm = torch.tensor(np.full(3 * 5000, 50.0), device=eng.device)
-                qq = torch.tensor(np.full(3 * 5000, 1.0), device=eng.device)
-                call(libs[k], tr, 3 * 5000, nf2, 5000, None, k0, mm, qq, work)
-                torch.cuda.synchronize()
-                res[k] = (bits(mm), bits(qq))
-            same = all(np.array_equal(res["old"][i], res["new"][i]) for i in (0, 1))
-            ok &= same
-            if not same:
-                print(f"  DIFF {name} nf={nf2} k0={k0}", flush=True)
+        for sl, ns in ((None, 5000), (gsel, 1777)):
+            for nf2, k0 in ((1, 0), (7, 0), (8, 0), (15, 3), (16, 0), (17, 9), (31, 5), (33, 64), (129, 1000),
+                            (700, 3), (700, 0)):
+                res = {}
+                for k in libs:
+                    mm = torch.tensor(np.full(3 * ns, 50.0), device=eng.device)
+                    qq = torch.tensor(np.full(3 * ns, 1.0), device=eng.device)
+                    call(libs[k], tr, 3 * 5000, nf2, ns, sl, k0, mm, qq, work)
+                    torch.cuda.synchronize()
+                    res[k] = (bits(mm), bits(qq))
+                same = all(same_bits(res["old"][i], res["new"][i]) for i in (0, 1))
+                ok &= same
+                if not same:
+                    print(f"  DIFF {name} sel={'yes' if sl is not None else 'no'} nf={nf2} k0={k0}", flush=True)
     print("ragged / special shapes all bit-equal:", ok, flush=True)
     return 0 if ok else 1
 
