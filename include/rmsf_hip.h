@@ -352,7 +352,8 @@ int rmsf_fold_balanced_shift_slab(const void *d_work, int64_t n_coord,
  * inputs ignored) end as the reference recurrence's own values bit for bit
  * -- a rank's S of RMSF.py:140, which rmsf_chan_merge then combines as
  * RMSF.py:143 does, also bit for bit.  Parallel over coordinates only (one
- * lane per coordinate through every frame); rmsf_accumulate_balanced is the
+ * lane per coordinate through every frame; one lane per atom for a d_sel of
+ * >= 49,152 atoms -- same bits); rmsf_accumulate_balanced is the
  * reassociated, frame-parallel form (faster, equal to ~1e-13).
  * d_work: rmsf_welford_sequential_workspace_bytes(n_frames) bytes (the
  * per-frame coefficients).  Replaces RMSF.py:120-138's loop for one rank.
