@@ -128,8 +128,9 @@ def test_rmsf_exact_ranks(size, n_frames, root):
         _same(m2, want["m2"], f"rank {rank} sumsquares")
 
 
+@pytest.mark.parametrize("n_atoms,nf", [(400, 90), (240_000, 30)])  # 60,000 selected: one atom per lane
 @pytest.mark.parametrize("device", [False, True])
-def test_context_exact_push_is_rmsf_py_rank(device):
+def test_context_exact_push_is_rmsf_py_rank(device, n_atoms, nf):
     """RMSF_PUSH_EXACT through the context ABI (the torch-free boundary an
     mpi4py / C host binds): a rank's S of RMSF.py:140 bit for bit over
     several pushes (host frames through the stager in 7-frame batches, or
@@ -139,7 +140,6 @@ def test_context_exact_push_is_rmsf_py_rank(device):
     A checkpoint (get / set_partial) continues the recurrence exactly."""
     from rmsf_amd import parallel
     from rmsf_amd.context import PUSH_EXACT, Context
-    n_atoms, nf = 400, 90
     traj = SY.frames(21, n_atoms, 0, nf)
     sel = np.arange(3, n_atoms, 4)
     x = torch.tensor(traj, device="cuda") if device else traj
