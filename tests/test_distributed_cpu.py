@@ -212,14 +212,16 @@ def test_scatter_layout_single_process():
 
 
 @pytest.mark.parametrize("order", ["mpi4py", "rank"])
-@pytest.mark.parametrize("size,n_frames,to_root", [(4, 41, False), (5, 53, True), (4, 3, True), (5, 23, False)])
+@pytest.mark.parametrize("size,n_frames,to_root", [(4, 41, False), (5, 53, True), (4, 3, True), (5, 23, False),
+                                                   (6, 40, False), (7, 5, True)])
 def test_gloo_exact_merge_order(size, n_frames, to_root, order):
-    """RMSF.py:143's comm.reduce at 4 and 5 ranks through the product's
+    """RMSF.py:143's comm.reduce at 4-7 ranks through the product's
     exact merge (parallel.global_chan_exact): order "mpi4py" runs mpi4py's
     binomial tree point to point (send / recv between the gloo ranks),
     "rank" gathers and folds in rank order; each equals the oracle's
     rmsf_script with that order bit for bit, on the root (or every rank).
-    3 frames on 4 ranks: empty ranks 0-2 (a skipped empty-empty merge)."""
+    3 frames on 4 ranks: empty ranks 0-2 (a skipped empty-empty merge); 5
+    frames on 7 ranks: only the last rank holds frames (empty subtrees)."""
     from oracle import rmsf_oracle as O
     from oracle import synth as SY
     from rmsf_amd.synth import motion_table
