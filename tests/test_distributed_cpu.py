@@ -6,7 +6,6 @@ HIP kernels, which need a GPU) and then runs the *product's* cross-rank code
 (``rmsf_amd.parallel``): the all-reduce sum of sweep 1 and the exact k-way
 Chan merge.  The element-wise steps of the merge are injected through an
 ``ops`` object -- here the oracle's numpy restatement of the two kernels."""
-import os
 import sys
 
 import numpy as np

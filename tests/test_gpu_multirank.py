@@ -6,7 +6,6 @@ Everything else is the product path of a real multi-GPU run: each rank holds
 only its own frame shard in HBM (RMSF.py:65-69 blocks), the reference frame's
 owner computes and broadcasts it, sweep 1 is all-reduced, and the exact k-way
 Chan merge runs through the HIP kernels."""
-import os
 import sys
 
 import numpy as np

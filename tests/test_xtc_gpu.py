@@ -8,7 +8,6 @@ long division), per-axis bit sizes (large range) and small-integer indices
 up to the end of the magicints table; corrupt records are rejected.
 GPU tier: the device kernel and the pinned-slot decoder give the same bytes,
 and RMSF from a GPU-decoded XTC equals RMSF from the host-decoded one."""
-import ctypes
 
 import numpy as np
 import pytest
