@@ -368,6 +368,67 @@ int rmsf_welford_sequential(const float *d_xyz, int64_t frame_stride,
                             double *d_sumsquares, void *d_work,
                             size_t work_bytes, void *stream);
 
+/* ---- exact=True on the ALIGNED path: RMSF.py:80-146 in the reference's own
+ * summation orders -----------------------------------------------------------
+ * The frame-parallel kernels above (rmsf_reference_setup, rmsf_superpose,
+ * rmsf_accumulate*) reassociate the per-frame sums; their rotations then
+ * differ from the script's in the last bits, which now and then flips an
+ * f32 rounding point of an aligned coordinate (RMSF.py:99-101) -- a few
+ * e-8 A at 100 frames, but up to ~ulp/2 = 2e-6 A at 2 frames.  These three
+ * entry points remove every such source: each sum runs atom by atom or
+ * frame by frame exactly as the reference runs it, so the transform records,
+ * the sweep-1 sums, the average and the Welford state equal the script's
+ * bit for bit.  The orders of the absent upstream dependencies are the
+ * published ones, restated (oracle/rmsf_oracle.py; upstream, unverified):
+ *   AtomGroup.center_of_mass(): einsum('ij,ij->j', x, m[:, None]) / m.sum()
+ *     -- a sequential sum over the atoms of f64(x) * m, divided by
+ *     mass_total = the caller's numpy ``masses.sum()`` (numpy sums pairwise;
+ *     n_sel when d_masses is NULL, i.e. unit masses);
+ *   qcprot InnerProduct: one pass over the atoms, A[3a+b] += mob_a ref_b,
+ *     G1 += x*x + y*y + z*z per atom, E0 = (G1 + G2) * 0.5.
+ *
+ * rmsf_reference_setup_sequential: RMSF.py:84-85 (d_frame, f32, atoms via
+ * d_sel) or RMSF.py:111 + 117-118 (d_avg = the all-reduced f64 sweep-1 sums,
+ * divided by avg_divisor = n_frames as they are read and written to
+ * d_avg_out when non-NULL; d_sel must be NULL): ref_com, d_ref = x - ref_com,
+ * and the refinfo record (ref_com, sum r, G2 of qcprot's loop, mass_total,
+ * n_sel).  One workgroup; serial in the atoms (~1 ms per 100k atoms).     */
+int rmsf_reference_setup_sequential(const float *d_frame, const double *d_avg,
+                                    double avg_divisor, int64_t n_sel,
+                                    const int32_t *d_sel, const double *d_masses,
+                                    double mass_total, double *d_avg_out,
+                                    double *d_ref, double *d_refinfo,
+                                    void *stream);
+/* rmsf_superpose_sequential: RMSF.py:94-97 / 127-131 + get_rotation_matrix
+ * for every frame (one lane per frame): mobile COM atom by atom, centred
+ * coordinates f64(x) - com, InnerProduct against d_ref (G2 from
+ * d_refinfo[6], i.e. a record of rmsf_reference_setup_sequential), QCP ->
+ * d_xform[f * RMSF_XFORM_DOUBLES] as rmsf_superpose writes it (COM absolute).
+ * Rows only (frame, atom, xyz).  Serial in the atoms of a frame: for large
+ * selections this is the exact path's cost.            */
+int rmsf_superpose_sequential(const float *d_xyz, int64_t frame_stride,
+                              int64_t n_frames, int64_t n_sel,
+                              const int32_t *d_sel, const double *d_masses,
+                              double mass_total, const double *d_ref,
+                              const double *d_refinfo, double *d_xform,
+                              void *stream);
+/* rmsf_accumulate_sequential: the frames in order for every selected atom
+ * (one lane per atom), k = k0 + f, each frame transformed first when d_xform
+ * (+ d_refinfo) is given (RMSF.py:99-101 / 133-135, the same f32-faithful
+ * transform as rmsf_accumulate), then
+ *   RMSF_MODE_SUM:     d_acc0 += x                          (RMSF.py:103)
+ *   RMSF_MODE_WELFORD: rmsf_welford_sequential's recurrence (RMSF.py:137-138)
+ *                      on (d_acc0 = mean, d_acc1 = sumsquares)
+ * continuing the running state after k0 frames (k0 = 0: from zeros).  The
+ * WELFORD mode needs d_work of rmsf_welford_sequential_workspace_bytes
+ * (n_frames) bytes; SUM needs none.  Rows only.                            */
+int rmsf_accumulate_sequential(const float *d_xyz, int64_t frame_stride,
+                               int64_t n_frames, int64_t n_sel,
+                               const int32_t *d_sel, const double *d_xform,
+                               const double *d_refinfo, int mode, int64_t k0,
+                               double *d_acc0, double *d_acc1, void *d_work,
+                               size_t work_bytes, void *stream);
+
 /* ---- finalise: RMSF.py:146  rmsf = sqrt(M2.sum(axis=1) / n) ---------------*/
 int rmsf_finalize(const double *d_m2, int64_t n_sel, int64_t n_frames,
                   double *d_rmsf, void *stream);

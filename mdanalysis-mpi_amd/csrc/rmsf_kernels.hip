@@ -663,6 +663,204 @@ __global__ __launch_bounds__(kBlock) void k_welford_seq_atoms(const float *__res
   }
 }
 
+// ---------------------------------------------------------------------------
+// exact=True on the ALIGNED path (round 6): RMSF.py:84-85, 94-97, 99-103,
+// 111, 117-118, 127-138 with the reference's own summation orders, so each
+// frame's rotation, every f32 rounding point of the transform, the sweep-1
+// sum, the average and the Welford state are the script's own values bit
+// for bit (on the restated upstream orders: AtomGroup.center_of_mass =
+// einsum('ij,ij->j', x, m[:, None]) / m.sum(), sequential over the atoms
+// with the caller's numpy m.sum(); qcprot's InnerProduct loop; both as
+// oracle/rmsf_oracle.py restates them -- upstream, unverified here).  The
+// frame-parallel kernels above reassociate these sums, so their rotations
+// can differ in the last bits, which flips an f32 rounding point of an
+// aligned coordinate now and then -- a cost of |x - mean| ulp / (N RMSF)
+// that only a few-frame run can push past 1e-6 A.
+//
+// k_ref_seq: the centred reference, one workgroup.  x = frame[sel[a]]
+// (f32 -> f64) or avg[a] / div (RMSF.py:111, written to avg_out too);
+// com_c = (sum_a x_ac m_a, atom by atom) / mass_total (RMSF.py:84/117);
+// ref = x - com (RMSF.py:85/118); the record [0..15]: com, sum r, G2 =
+// sum_a ((r0 r0 + r1 r1) + r2 r2) in qcprot's per-atom order (the G2 of
+// every InnerProduct call against this reference), mass_total, n_sel.
+template <bool FROM_F32, bool GATHER, bool MASSES>
+__global__ __launch_bounds__(kBlock) void k_ref_seq(const float *__restrict__ frame, const double *__restrict__ avg,
+                                                    double div, int64_t n_sel, const int32_t *__restrict__ sel,
+                                                    const double *__restrict__ masses, double mass_total,
+                                                    double *__restrict__ avg_out, double *__restrict__ ref,
+                                                    double *__restrict__ info) {
+  __shared__ double com[3];
+  auto load = [&](int64_t a, int c) -> double {
+    if (FROM_F32) return (double)frame[3 * (GATHER ? (int64_t)sel[a] : a) + c];
+    return avg[3 * a + c] / div;
+  };
+  if (!FROM_F32 && avg_out)
+    for (int64_t j = threadIdx.x; j < 3 * n_sel; j += kBlock) avg_out[j] = avg[j] / div;
+  if (threadIdx.x < 3) {  // three independent chains, one per axis
+    const int c = threadIdx.x;
+    double s = 0.0;
+#pragma unroll 4
+    for (int64_t a = 0; a < n_sel; ++a) s = s + load(a, c) * (MASSES ? masses[a] : 1.0);
+    com[c] = s / mass_total;
+  }
+  __syncthreads();
+  const double c0 = com[0], c1 = com[1], c2 = com[2];
+  for (int64_t a = threadIdx.x; a < n_sel; a += kBlock) {
+    ref[3 * a] = load(a, 0) - c0;
+    ref[3 * a + 1] = load(a, 1) - c1;
+    ref[3 * a + 2] = load(a, 2) - c2;
+  }
+  if (threadIdx.x == 0) {  // the same r recomputed (same bits), summed in order
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, g = 0.0;
+#pragma unroll 4
+    for (int64_t a = 0; a < n_sel; ++a) {
+      const double r0 = load(a, 0) - c0, r1 = load(a, 1) - c1, r2 = load(a, 2) - c2;
+      s0 = s0 + r0;
+      s1 = s1 + r1;
+      s2 = s2 + r2;
+      g = g + (r0 * r0 + r1 * r1 + r2 * r2);
+    }
+    info[0] = c0;
+    info[1] = c1;
+    info[2] = c2;
+    info[3] = s0;
+    info[4] = s1;
+    info[5] = s2;
+    info[6] = g;
+    info[7] = mass_total;
+    info[8] = (double)n_sel;
+    for (int j = 9; j < 16; ++j) info[j] = 0.0;
+  }
+}
+
+// k_superpose_seq: one lane per frame -- the frame's mobile COM (RMSF.py:94
+// / 127, atom by atom), its centred coordinates f64(x) - com (RMSF.py:95 /
+// 128), qcprot's InnerProduct loop against the reference (A, G1; G2 from the
+// record), E0 = (G1 + G2) * 0.5 and the QCP solve (RMSF.py:43-51) -> the
+// transform record.  The atom index is wave-uniform, so the selection, the
+// masses and the reference rows arrive by scalar loads; each lane walks its
+// own frame (frames are independent chains, atoms are not).
+template <bool GATHER, bool MASSES>
+__global__ __launch_bounds__(64) void k_superpose_seq(const float *__restrict__ xyz, int64_t fstride,
+                                                      int64_t n_frames, int64_t n_sel,
+                                                      const int32_t *__restrict__ sel,
+                                                      const double *__restrict__ masses, double mass_total,
+                                                      const double *__restrict__ ref,
+                                                      const double *__restrict__ refinfo,
+                                                      double *__restrict__ xform) {
+  const int64_t f = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (f >= n_frames) return;
+  const float *__restrict__ fr = xyz + f * fstride;
+  double c0 = 0.0, c1 = 0.0, c2 = 0.0;
+#pragma unroll 4
+  for (int64_t a = 0; a < n_sel; ++a) {
+    const float *p = fr + 3 * (GATHER ? (int64_t)sel[a] : a);
+    const double m = MASSES ? masses[a] : 1.0;
+    c0 = c0 + (double)p[0] * m;
+    c1 = c1 + (double)p[1] * m;
+    c2 = c2 + (double)p[2] * m;
+  }
+  c0 = c0 / mass_total;
+  c1 = c1 / mass_total;
+  c2 = c2 / mass_total;
+  double A[9] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, G1 = 0.0;
+#pragma unroll 2
+  for (int64_t a = 0; a < n_sel; ++a) {
+    const float *p = fr + 3 * (GATHER ? (int64_t)sel[a] : a);
+    const double x1 = (double)p[0] - c0, y1 = (double)p[1] - c1, z1 = (double)p[2] - c2;
+    const double *r = ref + 3 * a;
+    const double x2 = r[0], y2 = r[1], z2 = r[2];
+    G1 = G1 + (x1 * x1 + y1 * y1 + z1 * z1);
+    A[0] = A[0] + x1 * x2;
+    A[1] = A[1] + x1 * y2;
+    A[2] = A[2] + x1 * z2;
+    A[3] = A[3] + y1 * x2;
+    A[4] = A[4] + y1 * y2;
+    A[5] = A[5] + y1 * z2;
+    A[6] = A[6] + z1 * x2;
+    A[7] = A[7] + z1 * y2;
+    A[8] = A[8] + z1 * z2;
+  }
+  const double E0 = (G1 + refinfo[6]) * 0.5;
+  double rot[9], rmsd;
+  qcp_solve(A, E0, (double)n_sel, rot, &rmsd);
+  double *t = xform + f * kXform;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) t[j] = rot[j];
+  t[9] = c0;
+  t[10] = c1;
+  t[11] = c2;
+  t[12] = rmsd;
+  t[13] = t[14] = t[15] = 0.0;
+}
+
+// k_accum_seq: one selected atom per lane, the batch's frames in order
+// (k = k0 + f), each frame's transform applied (ALIGN, RMSF.py:99-101 /
+// 133-135) and then
+//   SUM:     pos += x                                  (RMSF.py:103)
+//   WELFORD: sumsquares += (k / (k + 1.0)) * (x - mean)**2 ;
+//            mean = (k * mean + x) / (k + 1)            (RMSF.py:137-138)
+// with numpy's operations and roundings -- k_welford_seq_atoms' recurrence,
+// the running state continued from acc0/acc1 when k0 > 0.  U frames' loads
+// are issued before they are consumed.
+template <int MODE, bool ALIGN, bool GATHER, int U>
+__global__ __launch_bounds__(kBlock) void k_accum_seq(const float *__restrict__ xyz, int64_t fstride, int64_t nf,
+                                                      int64_t n_sel, const int32_t *__restrict__ sel,
+                                                      const double *__restrict__ xform,
+                                                      const double *__restrict__ refinfo, int64_t k0,
+                                                      const SeqCoef *__restrict__ coef, double *__restrict__ acc0,
+                                                      double *__restrict__ acc1) {
+  const int64_t a = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (a >= n_sel) return;
+  const double rc0 = ALIGN ? refinfo[0] : 0.0, rc1 = ALIGN ? refinfo[1] : 0.0, rc2 = ALIGN ? refinfo[2] : 0.0;
+  double m[3], q[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    m[c] = k0 > 0 ? acc0[3 * a + c] : 0.0;
+    if (MODE == RMSF_MODE_WELFORD && k0 > 0) q[c] = acc1[3 * a + c];
+  }
+  const float *__restrict__ p = xyz + 3 * (GATHER ? (int64_t)sel[a] : a);
+  auto consume = [&](float x, float y, float z, int64_t f, double k) {
+    if (ALIGN) apply_xform(x, y, z, xform + f * kXform, rc0, rc1, rc2);
+    const float v[3] = {x, y, z};
+    if (MODE == RMSF_MODE_SUM) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) m[c] = m[c] + (double)v[c];
+    } else {
+      const SeqCoef cf = coef[f];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const double xx = (double)v[c];
+        const double d = xx - m[c];
+        q[c] = q[c] + cf.c * (d * d);
+        m[c] = seq_div(k * m[c] + xx, k + 1.0, cf.r);
+      }
+    }
+  };
+  int64_t f = 0;
+  double kb = (double)k0;
+  for (; f + U <= nf; f += U) {
+    float v[U][3];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float *r = p + (f + u) * fstride;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[u][c] = __builtin_nontemporal_load(r + c);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u, kb += 1.0) consume(v[u][0], v[u][1], v[u][2], f + u, kb);
+  }
+  for (; f < nf; ++f, kb += 1.0) {
+    const float *r = p + f * fstride;
+    consume(r[0], r[1], r[2], f, kb);
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    acc0[3 * a + c] = m[c];
+    if (MODE == RMSF_MODE_WELFORD) acc1[3 * a + c] = q[c];
+  }
+}
+
 template <int MODE, bool ALIGN, bool GATHER, int U, bool PLANES = false>
 __global__ __launch_bounds__(kBlock) void k_accum_atoms_sk(const float *__restrict__ xyz, int64_t fstride,
                                                            const int32_t *__restrict__ sel,
@@ -1304,25 +1502,6 @@ __global__ __launch_bounds__(kBlock) void k_qcp_frames(
 }
 
 // ---------------------------------------------------------------------------
-template <int N>
-__device__ __forceinline__ void block_sum_1024(double (&v)[N], double (*red)[N]) {
-  wave_sum(v);
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  __syncthreads();
-  if (lane == 0) {
-#pragma unroll
-    for (int j = 0; j < N; ++j) red[w][j] = v[j];
-  }
-  __syncthreads();
-  const int nw = blockDim.x >> 6;
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    double t = 0.0;
-    for (int i = 0; i < nw; ++i) t += red[i][j];
-    v[j] = t;
-  }
-}
-
 // Reference setup, RMSF.py:84-85 / 117-118, as three launches over
 // kRefBlocks-bounded grids with fixed-order (deterministic) reductions whose
 // per-block partials live in the scratch tail of the caller's refinfo record:
@@ -1732,35 +1911,38 @@ __global__ __launch_bounds__(kBlock) void k_qcp_batch(const double *__restrict__
   rmsd[i] = d;
 }
 
-// qcprot InnerProduct (weights optional), single block: A (9) and E0.
-__global__ __launch_bounds__(1024) void k_inner_product(const double *__restrict__ ref,
-                                                        const double *__restrict__ conf,
-                                                        const double *__restrict__ w, int64_t N,
-                                                        double *__restrict__ out) {
-  __shared__ double red[16][11];
-  double v[11];
-  for (int j = 0; j < 11; ++j) v[j] = 0.0;
-  for (int64_t i = threadIdx.x; i < N; i += blockDim.x) {
+// qcprot InnerProduct (weights optional): A (9) and E0, in the published
+// loop's order -- one pass over the atoms, every accumulator updated per atom
+// (Theobald's qcprot.c, restated by MDAnalysis.lib.qcprot; upstream,
+// unverified here; oracle/rmsf_oracle.py:inner_product).  One lane: the
+// host-pointer CalcRMSDRotationalMatrix replaces a single-threaded call, and
+// its A / E0 are then the loop's own bits (no contraction, csrc/Makefile).
+__global__ __launch_bounds__(64) void k_inner_product(const double *__restrict__ ref,
+                                                      const double *__restrict__ conf,
+                                                      const double *__restrict__ w, int64_t N,
+                                                      double *__restrict__ out) {
+  if (threadIdx.x != 0) return;
+  double A[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, G1 = 0.0, G2 = 0.0;
+  for (int64_t i = 0; i < N; ++i) {
+    const double cx = conf[3 * i], cy = conf[3 * i + 1], cz = conf[3 * i + 2];
     const double wi = w ? w[i] : 1.0;
-    const double x1 = wi * conf[3 * i], y1 = wi * conf[3 * i + 1], z1 = wi * conf[3 * i + 2];
+    const double x1 = w ? wi * cx : cx, y1 = w ? wi * cy : cy, z1 = w ? wi * cz : cz;
+    G1 = G1 + (x1 * cx + y1 * cy + z1 * cz);
     const double x2 = ref[3 * i], y2 = ref[3 * i + 1], z2 = ref[3 * i + 2];
-    v[9] += x1 * conf[3 * i] + y1 * conf[3 * i + 1] + z1 * conf[3 * i + 2];
-    v[10] += wi * (x2 * x2 + y2 * y2 + z2 * z2);
-    v[0] += x1 * x2;
-    v[1] += x1 * y2;
-    v[2] += x1 * z2;
-    v[3] += y1 * x2;
-    v[4] += y1 * y2;
-    v[5] += y1 * z2;
-    v[6] += z1 * x2;
-    v[7] += z1 * y2;
-    v[8] += z1 * z2;
+    const double g2 = x2 * x2 + y2 * y2 + z2 * z2;
+    G2 = G2 + (w ? wi * g2 : g2);
+    A[0] = A[0] + x1 * x2;
+    A[1] = A[1] + x1 * y2;
+    A[2] = A[2] + x1 * z2;
+    A[3] = A[3] + y1 * x2;
+    A[4] = A[4] + y1 * y2;
+    A[5] = A[5] + y1 * z2;
+    A[6] = A[6] + z1 * x2;
+    A[7] = A[7] + z1 * y2;
+    A[8] = A[8] + z1 * z2;
   }
-  block_sum_1024(v, red);
-  if (threadIdx.x == 0) {
-    for (int j = 0; j < 9; ++j) out[j] = v[j];
-    out[9] = 0.5 * (v[9] + v[10]);
-  }
+  for (int j = 0; j < 9; ++j) out[j] = A[j];
+  out[9] = (G1 + G2) * 0.5;
 }
 
 // ---------------------------------------------------------------------------
@@ -2787,6 +2969,91 @@ RMSF_EXPORT int rmsf_welford_sequential(const float *d_xyz, int64_t fstride, int
   return after_launch("k_welford_seq");
 }
 
+RMSF_EXPORT int rmsf_reference_setup_sequential(const float *d_frame, const double *d_avg, double avg_divisor,
+                                                int64_t n_sel, const int32_t *d_sel, const double *d_masses,
+                                                double mass_total, double *d_avg_out, double *d_ref,
+                                                double *d_refinfo, void *stream) {
+  if ((d_frame == nullptr) == (d_avg == nullptr))
+    return fail(RMSF_EINVAL, "rmsf_reference_setup_sequential: exactly one of d_frame / d_avg");
+  if (n_sel < 1 || !d_ref || !d_refinfo || (d_avg && !(avg_divisor > 0.0)) || (d_avg && d_sel))
+    return fail(RMSF_EINVAL, "rmsf_reference_setup_sequential: bad arguments");
+  const bool g = d_sel != nullptr, m = d_masses != nullptr;
+  hipStream_t s = S(stream);
+#define SEQREF(F, G, M)                                                                                     \
+  hipLaunchKernelGGL((k_ref_seq<F, G, M>), dim3(1), dim3(kBlock), 0, s, d_frame, d_avg, avg_divisor, n_sel, d_sel, \
+                     d_masses, mass_total, d_avg_out, d_ref, d_refinfo)
+  if (d_frame) {
+    if (g && m) SEQREF(true, true, true);
+    else if (g) SEQREF(true, true, false);
+    else if (m) SEQREF(true, false, true);
+    else SEQREF(true, false, false);
+  } else {
+    if (m) SEQREF(false, false, true);
+    else SEQREF(false, false, false);
+  }
+#undef SEQREF
+  return after_launch("k_ref_seq");
+}
+
+RMSF_EXPORT int rmsf_superpose_sequential(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
+                                          const int32_t *d_sel, const double *d_masses, double mass_total,
+                                          const double *d_ref, const double *d_refinfo, double *d_xform,
+                                          void *stream) {
+  if (!d_xyz || !d_ref || !d_refinfo || !d_xform || n_sel < 1 || n_frames < 0 || fstride < (d_sel ? 3 : 3 * n_sel))
+    return fail(RMSF_EINVAL, "rmsf_superpose_sequential: bad arguments");
+  if (n_frames == 0) return RMSF_OK;
+  const dim3 grid((unsigned)((n_frames + 63) / 64));
+  hipStream_t s = S(stream);
+  const bool g = d_sel != nullptr, m = d_masses != nullptr;
+#define SEQSUP(G, M)                                                                                          \
+  hipLaunchKernelGGL((k_superpose_seq<G, M>), grid, dim3(64), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, \
+                     mass_total, d_ref, d_refinfo, d_xform)
+  if (g && m) SEQSUP(true, true);
+  else if (g) SEQSUP(true, false);
+  else if (m) SEQSUP(false, true);
+  else SEQSUP(false, false);
+#undef SEQSUP
+  return after_launch("k_superpose_seq");
+}
+
+RMSF_EXPORT int rmsf_accumulate_sequential(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
+                                           const int32_t *d_sel, const double *d_xform, const double *d_refinfo,
+                                           int mode, int64_t k0, double *d_acc0, double *d_acc1, void *d_work,
+                                           size_t work_bytes, void *stream) {
+  const bool wel = mode == RMSF_MODE_WELFORD;
+  if ((mode != RMSF_MODE_WELFORD && mode != RMSF_MODE_SUM) || !d_xyz || !d_acc0 || (wel && (!d_acc1 || !d_work)) ||
+      n_sel < 1 || n_frames < 0 || k0 < 0 || k0 + n_frames > (int64_t(1) << 53) ||
+      fstride < (d_sel ? 3 : 3 * n_sel) || (d_xform != nullptr) != (d_refinfo != nullptr))
+    return fail(RMSF_EINVAL, "rmsf_accumulate_sequential: bad arguments");
+  if (n_frames == 0) return RMSF_OK;
+  hipStream_t s = S(stream);
+  const SeqCoef *coef = nullptr;
+  if (wel) {
+    if (work_bytes < rmsf_welford_sequential_workspace_bytes(n_frames))
+      return fail(RMSF_EINVAL, "rmsf_accumulate_sequential: workspace too small");
+    hipLaunchKernelGGL(k_seq_coef, dim3(grid1(n_frames)), dim3(kBlock), 0, s, k0, n_frames,
+                       static_cast<SeqCoef *>(d_work));
+    if (int rc = after_launch("k_seq_coef")) return rc;
+    coef = static_cast<const SeqCoef *>(d_work);
+  }
+  const bool al = d_xform != nullptr, g = d_sel != nullptr;
+  const dim3 grid((unsigned)grid1(n_sel));
+#define SEQACC(MO, A, G)                                                                                    \
+  hipLaunchKernelGGL((k_accum_seq<MO, A, G, 4>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, \
+                     d_xform, d_refinfo, k0, coef, d_acc0, d_acc1)
+  auto launch = [&](auto MOc) {
+    constexpr int MO = decltype(MOc)::value;
+    if (al && g) SEQACC(MO, true, true);
+    else if (al) SEQACC(MO, true, false);
+    else if (g) SEQACC(MO, false, true);
+    else SEQACC(MO, false, false);
+  };
+#undef SEQACC
+  if (wel) launch(std::integral_constant<int, RMSF_MODE_WELFORD>{});
+  else launch(std::integral_constant<int, RMSF_MODE_SUM>{});
+  return after_launch("k_accum_seq");
+}
+
 RMSF_EXPORT int rmsf_finalize(const double *d_m2, int64_t n_sel, int64_t n_frames, double *d_rmsf, void *stream) {
   if (!d_m2 || !d_rmsf || n_sel < 1) return fail(RMSF_EINVAL, "rmsf_finalize: bad arguments");
   if (n_frames < 1) return fail(RMSF_EEMPTY, "rmsf_finalize: no frames");
@@ -2820,7 +3087,7 @@ RMSF_EXPORT int rmsf_calc_rmsd_rotational_matrix(const double *h_ref, const doub
       rc = hip_fail("memcpy", e);
       break;
     }
-    hipLaunchKernelGGL(k_inner_product, dim3(1), dim3(1024), 0, 0, dref, dconf, h_weights ? dw : nullptr, N, dio);
+    hipLaunchKernelGGL(k_inner_product, dim3(1), dim3(64), 0, 0, dref, dconf, h_weights ? dw : nullptr, N, dio);
     if ((rc = after_launch("k_inner_product"))) break;
     const double nd = (double)N;
     if ((e = hipMemcpy(dio + 10, &nd, sizeof nd, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail("memcpy", e); break; }

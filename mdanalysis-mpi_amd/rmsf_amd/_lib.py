@@ -76,6 +76,10 @@ SIGNATURES = {
     "rmsf_chan_weight": (c_int, [P, c_double, c_int64, P, P]),
     "rmsf_chan_deviation": (c_int, [P, P, P, c_double, c_int64, P, P]),
     "rmsf_finalize": (c_int, [P, c_int64, c_int64, P, P]),
+    "rmsf_reference_setup_sequential": (c_int, [P, P, c_double, c_int64, P, P, c_double, P, P, P, P]),
+    "rmsf_superpose_sequential": (c_int, [P, c_int64, c_int64, c_int64, P, P, c_double, P, P, P, P]),
+    "rmsf_accumulate_sequential": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, c_int, c_int64, P, P, P, c_size_t,
+                                           P]),
     "rmsf_welford_sequential_workspace_bytes": (c_size_t, [c_int64]),
     "rmsf_welford_sequential": (c_int, [P, c_int64, c_int64, c_int64, P, c_int64, P, P, P, c_size_t, P]),
     "rmsf_chan_shift_pack": (c_int, [P, P, P, c_int, P, c_double, c_int64, P, P]),

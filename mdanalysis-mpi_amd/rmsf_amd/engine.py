@@ -294,6 +294,43 @@ class Engine:
              sumsquares.data_ptr(), work.data_ptr(), work.numel() * work.element_size(), self.stream)
         return work
 
+    # -- exact=True on the aligned path (the reference's summation orders) ---
+    def reference_setup_seq(self, n_sel: int, mass_total: float, *, frame_ptr: int | None = None,
+                            sel: torch.Tensor | None = None, total: torch.Tensor | None = None,
+                            n_frames: float = 1.0, masses: torch.Tensor | None = None):
+        """RMSF.py:84-85 (``frame_ptr``) or RMSF.py:111 + 117-118 (``total``,
+        the all-reduced sweep-1 sums, divided by ``n_frames`` as read) with
+        the reference's own summation order (rmsf_reference_setup_sequential).
+        Returns (average or None, ref, info)."""
+        ref = self.empty(n_sel, 3)
+        info = self.empty(RMSF_REFINFO_DOUBLES)
+        avg = self.empty(3 * n_sel) if total is not None else None
+        call("rmsf_reference_setup_sequential", frame_ptr, _ptr(total), float(n_frames), n_sel,
+             _ptr(sel if frame_ptr else None), _ptr(masses), float(mass_total), _ptr(avg), ref.data_ptr(),
+             info.data_ptr(), self.stream)
+        return avg, ref, info
+
+    def superpose_seq(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, sel, masses,
+                      mass_total: float, ref: torch.Tensor, refinfo: torch.Tensor, xform: torch.Tensor) -> None:
+        """RMSF.py:94-97,127-131 + get_rotation_matrix per frame in the
+        reference's order (rmsf_superpose_sequential)."""
+        call("rmsf_superpose_sequential", xyz_ptr, fstride, n_frames, n_sel, _ptr(sel), _ptr(masses),
+             float(mass_total), ref.data_ptr(), refinfo.data_ptr(), xform.data_ptr(), self.stream)
+
+    def accumulate_seq(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, sel, xform, refinfo,
+                       mode: int, k0: int, acc0: torch.Tensor, acc1: torch.Tensor | None,
+                       work: torch.Tensor | None = None) -> torch.Tensor | None:
+        """RMSF.py:99-103 (SUM) / 133-138 (WELFORD) frame by frame in order
+        (rmsf_accumulate_sequential); returns the coefficient workspace."""
+        if mode == RMSF_MODE_WELFORD:
+            need = int(self.lib.rmsf_welford_sequential_workspace_bytes(n_frames))
+            if work is None or work.numel() * work.element_size() < need:
+                work = self.empty(max(need, 16) // 8)
+        call("rmsf_accumulate_sequential", xyz_ptr, fstride, n_frames, n_sel, _ptr(sel), _ptr(xform),
+             _ptr(refinfo), mode, k0, acc0.data_ptr(), _ptr(acc1), _ptr(work),
+             0 if work is None else work.numel() * work.element_size(), self.stream)
+        return work
+
     def finalize(self, m2: torch.Tensor, n_sel: int, n_frames: int, out: torch.Tensor) -> None:
         """RMSF.py:146: sqrt(M2.sum(axis=1)/n)."""
         call("rmsf_finalize", m2.data_ptr(), n_sel, n_frames, out.data_ptr(), self.stream)

@@ -49,6 +49,24 @@ def allreduce_sum_(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+def allreduce_sum_ordered_(ops, t: torch.Tensor) -> torch.Tensor:
+    """RMSF.py:110's ``Allreduce(SUM)`` with the ranks' buffers added in rank
+    order, ((s_0 + s_1) + s_2) + ..., identically on every rank (exact=True):
+    every rank's buffer is all-gathered and ``ops.sum_splits`` (the device's
+    k_sum_splits) adds them in that order.  Two ranks' sum is the same bits
+    in any order (RMSF.py's ``mpirun -n 2``); from three ranks an MPI
+    library picks its own order (MPICH: recursive doubling or
+    reduce-scatter/allgather by message size -- upstream, not restated), so
+    rank order is this build's definition there.  In place; no-op for one
+    process."""
+    _, size = world()
+    if size > 1:
+        n = t.numel()
+        g = all_gather_(t.reshape(-1)).view(size, n)
+        ops.sum_splits(g, size, n, t.reshape(-1))
+    return t
+
+
 def broadcast_(t: torch.Tensor, src: int) -> torch.Tensor:
     _, size = world()
     if size > 1:

@@ -219,13 +219,23 @@ class PipelineResult:
     extras: dict = field(default_factory=dict)
 
 
-def reference_from_frame(eng: Engine, source, frame: int, n_sel: int, masses, owner: int | None = None):
+def reference_from_frame(eng: Engine, source, frame: int, n_sel: int, masses, owner: int | None = None,
+                         mass_total: float | None = None):
     """RMSF.py:80-87: centred f64 reference of trajectory frame ``frame``.
 
     RMSF.py has every rank re-read that frame from disk.  Here, if every rank
     holds it (host / full-trajectory sources) each computes it locally;
     otherwise (sharded HBM-resident trajectories) the lowest rank holding it
-    computes it and broadcasts 3*n_sel + 16 doubles."""
+    computes it and broadcasts 3*n_sel + 16 doubles.  ``mass_total`` given:
+    the reference's own summation order (exact=True,
+    rmsf_reference_setup_sequential; numpy's masses.sum())."""
+    if mass_total is not None:
+        def setup(b):
+            _, r, i = eng.reference_setup_seq(n_sel, mass_total, frame_ptr=b.ptr, sel=b.sel, masses=masses)
+            return r, i
+    else:
+        def setup(b):
+            return eng.reference_setup(n_sel, frame_ptr=b.ptr, sel=b.sel, masses=masses)
     rank, size = parallel.world()
     if size > 1:
         if owner is None:
@@ -244,7 +254,7 @@ def reference_from_frame(eng: Engine, source, frame: int, n_sel: int, masses, ow
             info = eng.empty(RMSF_REFINFO_DOUBLES)
             if rank == owner:
                 b = source.reference(frame, eng.stream)
-                r, i = eng.reference_setup(n_sel, frame_ptr=b.ptr, sel=b.sel, masses=masses)
+                r, i = setup(b)
                 b.done()
                 ref.copy_(r)
                 info.copy_(i)
@@ -252,7 +262,7 @@ def reference_from_frame(eng: Engine, source, frame: int, n_sel: int, masses, ow
             parallel.broadcast_(info[:16], owner)  # the record; the rest is setup scratch
             return ref, info
     b = source.reference(frame, eng.stream)
-    r, i = eng.reference_setup(n_sel, frame_ptr=b.ptr, sel=b.sel, masses=masses)
+    r, i = setup(b)
     b.done()
     return r, i
 
@@ -359,21 +369,28 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     the RMSF is gathered to ``merge_root`` (default 0); ``mean``/``m2`` are
     None and each rank's slice of them is in ``extras`` ("atom_slice",
     "slice_mean", "slice_m2").
-    ``exact`` (no alignment): RMSF.py:120-146 with the reference's own
-    arithmetic -- each rank's block through the sequential Welford
-    (rmsf_welford_sequential), the ranks reduced by second_order_moments in
-    RMSF.py:143's comm.reduce order (``merge_order``: "mpi4py", mpi4py's
-    default binomial tree, or "rank"; parallel.global_chan_exact), RMSF.py:146:
-    results bit-identical to RMSF.py's, ~1.3x the balanced path's time."""
+    ``exact``: RMSF.py with the reference's own arithmetic and summation
+    orders -- align=None: RMSF.py:120-146, each rank's block through the
+    sequential Welford (rmsf_welford_sequential), ~1.15x the balanced path's
+    time; aligned: RMSF.py:80-146, every per-frame COM / inner product atom by
+    atom (rmsf_superpose_sequential), the sweep-1 sum and Welford frame by
+    frame (rmsf_accumulate_sequential), the Allreduce of RMSF.py:110 in rank
+    order and the references of RMSF.py:84-85 / 117-118 in order
+    (rmsf_reference_setup_sequential).  The ranks are reduced by
+    second_order_moments in RMSF.py:143's comm.reduce order (``merge_order``:
+    "mpi4py", mpi4py's default binomial tree, or "rank";
+    parallel.global_chan_exact), then RMSF.py:146: results bit-identical to
+    RMSF.py's (on the restated upstream orders)."""
     if align not in ALIGN_MODES:
         raise ValueError(f"align must be one of {ALIGN_MODES}, got {align!r}")
     if exact:
-        if align is not None:
-            raise NotImplementedError("exact=True covers align=None (RMSF.py:120-146 on an aligned trajectory)")
-        if n_splits or merge_scatter or merge_slabs not in (None, 0, 1) or collect_rmsd or collect_transforms:
-            raise ValueError("exact=True runs the sequential Welford: no n_splits, merge_scatter, merge_slabs, "
-                             "collect_rmsd or collect_transforms")
-        return _run_exact(eng, source, frames, max_batch, block, timer, merge_root, merge_order)
+        if n_splits or merge_scatter or merge_slabs not in (None, 0, 1):
+            raise ValueError("exact=True runs the sequential kernels: no n_splits, merge_scatter or merge_slabs")
+        if align is None and (collect_rmsd or collect_transforms):
+            raise ValueError("collect_rmsd / collect_transforms need an aligned run")
+        return _run_exact(eng, source, frames, max_batch, block, timer, merge_root, merge_order, align=align,
+                          masses=masses, ref_frame=ref_frame, ref_owner=ref_owner, collect_rmsd=collect_rmsd,
+                          collect_transforms=collect_transforms)
     rank, size = parallel.world()
     n_total = len(frames)
     if n_total == 0:
@@ -543,8 +560,10 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
 
 
 def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, merge_root,
-               merge_order: str = "mpi4py") -> PipelineResult:
-    """run_pipeline(exact=True): RMSF.py:120-146 bit for bit (see there)."""
+               merge_order: str = "mpi4py", *, align=None, masses=None, ref_frame: int = 0,
+               ref_owner: int | None = None, collect_rmsd: bool = False,
+               collect_transforms: bool = False) -> PipelineResult:
+    """run_pipeline(exact=True): RMSF.py bit for bit (see there)."""
     rank, size = parallel.world()
     n_total = len(frames)
     if n_total == 0:
@@ -559,25 +578,70 @@ def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, 
     n_local = b1 - b0
     n_sel = source.n_sel
     max_batch = max(1, min(max_batch or max(1, n_local), max(1, n_local)))
-    mean, ss = eng.zeros(3 * n_sel), eng.zeros(3 * n_sel)   # RMSF.py:119-120
-    work, k = None, 0
-    for b in source.batches(frames, b0, b1, max_batch, eng.stream):  # rows: (frame, atom, xyz)
-        if b.pstride:
-            raise ValueError("exact=True reads (frame, atom, xyz) rows; this source handed over coordinate planes")
-        with _span(timer, "accumulate", b.n_frames * n_sel):
-            work = eng.welford_sequential(b.ptr, b.fstride, b.n_frames, n_sel, b.sel, k, mean, ss, work)
-        k += b.n_frames
-        b.done()
-    if size > 1:                                             # RMSF.py:141-143, comm.reduce's order
+    aligned = align is not None
+    m_dev, mass_total = None, float(n_sel)
+    if masses is not None:
+        m_np = np.ascontiguousarray(masses, dtype=np.float64)
+        if m_np.size != n_sel:
+            raise ValueError("masses must have one entry per selected atom")
+        # AtomGroup.center_of_mass divides by weights.sum(): numpy's own
+        # (pairwise) sum of the f64 masses -- one host scalar
+        mass_total = float(m_np.sum())
+        m_dev = torch.as_tensor(m_np).to(eng.device)
+    xf = eng.empty(max_batch, RMSF_XFORM_DOUBLES) if aligned else None
+    rmsd = eng.empty(n_local) if (aligned and collect_rmsd) else None
+    xf_last = eng.empty(n_local, RMSF_XFORM_DOUBLES) if (aligned and collect_transforms) else None
+    xf_first = eng.empty(n_local, RMSF_XFORM_DOUBLES) if (collect_transforms and align == "average") else None
+
+    def sweep(mode, acc0, acc1, ref=None, info=None, xf_out=None):
+        work, k = None, 0
+        for b in source.batches(frames, b0, b1, max_batch, eng.stream):  # rows: (frame, atom, xyz)
+            if b.pstride:
+                raise ValueError("exact=True reads (frame, atom, xyz) rows; this source handed over coordinate planes")
+            x = None
+            if aligned:
+                x = xf[:b.n_frames]
+                with _span(timer, "superpose", b.n_frames * n_sel):
+                    eng.superpose_seq(b.ptr, b.fstride, b.n_frames, n_sel, b.sel, m_dev, mass_total, ref, info, x)
+                if rmsd is not None:
+                    rmsd[k:k + b.n_frames].copy_(x[:, 12])
+                if xf_out is not None:
+                    xf_out[k:k + b.n_frames].copy_(x)
+            with _span(timer, "accumulate", b.n_frames * n_sel):
+                if aligned:
+                    work = eng.accumulate_seq(b.ptr, b.fstride, b.n_frames, n_sel, b.sel, x, info, mode, k, acc0,
+                                              acc1, work)
+                else:
+                    work = eng.welford_sequential(b.ptr, b.fstride, b.n_frames, n_sel, b.sel, k, acc0, acc1, work)
+            k += b.n_frames
+            b.done()
+
+    ref = info = average = None
+    if aligned:   # RMSF.py:80-87
+        ref, info = reference_from_frame(eng, source, ref_frame, n_sel, m_dev, ref_owner, mass_total=mass_total)
+    if align == "average":
+        total = eng.zeros(3 * n_sel)                            # RMSF.py:89, selection rows
+        if n_local:
+            sweep(RMSF_MODE_SUM, total, None, ref, info, xf_first)   # RMSF.py:91-103
+        parallel.allreduce_sum_ordered_(eng, total)             # RMSF.py:110, rank order
+        # RMSF.py:111 + 113-118
+        average, ref, info = eng.reference_setup_seq(n_sel, mass_total, total=total, n_frames=float(n_total),
+                                                     masses=m_dev)
+    mean, ss = eng.zeros(3 * n_sel), eng.zeros(3 * n_sel)       # RMSF.py:120-121
+    if n_local:
+        sweep(RMSF_MODE_WELFORD, mean, ss, ref, info, xf_last)  # RMSF.py:123-138
+    if size > 1:                                                # RMSF.py:141-143, comm.reduce's order
         with _span(timer, "merge"):
             mean, ss = parallel.global_chan_exact(eng, mean, ss, [e - s for s, e in blocks], root, merge_order)
     rmsf = None
     if mean is not None:
         rmsf = eng.empty(n_sel)
-        eng.finalize(ss, n_sel, n_total, rmsf)               # RMSF.py:146
+        eng.finalize(ss, n_sel, n_total, rmsf)                  # RMSF.py:146
     return PipelineResult(rmsf=rmsf, mean=None if mean is None else mean.view(n_sel, 3),
                           m2=None if ss is None else ss.view(n_sel, 3), n_frames=n_total, n_local=n_local,
-                          block=(b0, b1), extras={"exact": True, "merge_root": root, "merge_order": merge_order})
+                          block=(b0, b1), average=None if average is None else average.view(n_sel, 3), rmsd=rmsd,
+                          transforms=xf_last, transforms_sweep1=xf_first,
+                          extras={"exact": True, "merge_root": root, "merge_order": merge_order})
 
 
 class CapturedPipeline:

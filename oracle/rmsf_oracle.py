@@ -63,17 +63,44 @@ def center_of_mass(pos: np.ndarray, masses: np.ndarray | None = None) -> np.ndar
 # qcprot (RMSF.py:48)
 
 
+def _seq_sum(terms: np.ndarray) -> float:
+    """terms[0] + terms[1] + ... added one at a time from 0.0, as a C loop
+    ``G += term`` does (np.cumsum accumulates sequentially; ndarray.sum()
+    would sum pairwise)."""
+    return float(np.cumsum(terms)[-1]) if len(terms) else 0.0
+
+
 def inner_product(ref: np.ndarray, conf: np.ndarray, weights=None):
     """qcprot InnerProduct(A, conf, ref, N, weights): A[a][b] = sum w conf_a ref_b,
-    E0 = (sum w |conf|^2 + sum w |ref|^2) / 2.  Returns (A[9] list, E0)."""
+    E0 = (G1 + G2) * 0.5.  Returns (A[9] list, E0).
+
+    Summation order of the published qcprot loop (Theobald's qcprot.c
+    ``InnerProduct``, which MDAnalysis.lib.qcprot restates in Cython --
+    upstream, not vendored or installed here, so unverified in this
+    container): ONE pass over the atoms i = 0..N-1, every accumulator updated
+    per atom in turn --
+        x1 = w conf_x (y1, z1 alike)        (x1 = conf_x without weights)
+        G1 += x1 conf_x + y1 conf_y + z1 conf_z
+        G2 += w (ref_x^2 + ref_y^2 + ref_z^2)   (without the w factor unweighted)
+        A[3a + b] += (a1 ref_b)
+    each right-hand side evaluated left to right and rounded per operation
+    (no contraction), then added to the running sum.  The axis-0 reduction
+    of an [N, 3, 3] product array is sequential in numpy, so A follows that
+    order; G1/G2's per-atom terms are summed by ``_seq_sum``."""
     conf = np.asarray(conf, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)
-    w = np.ones(len(conf)) if weights is None else np.asarray(weights, dtype=np.float64)
-    wc = conf * w[:, None]
+    if weights is None:
+        wc = conf
+        g1 = (conf[:, 0] * conf[:, 0] + conf[:, 1] * conf[:, 1]) + conf[:, 2] * conf[:, 2]
+        g2 = (ref[:, 0] * ref[:, 0] + ref[:, 1] * ref[:, 1]) + ref[:, 2] * ref[:, 2]
+    else:
+        w = np.asarray(weights, dtype=np.float64)
+        wc = conf * w[:, None]
+        g1 = (wc[:, 0] * conf[:, 0] + wc[:, 1] * conf[:, 1]) + wc[:, 2] * conf[:, 2]
+        g2 = w * ((ref[:, 0] * ref[:, 0] + ref[:, 1] * ref[:, 1]) + ref[:, 2] * ref[:, 2])
     A = (wc[:, :, None] * ref[:, None, :]).sum(axis=0).reshape(9)
-    G1 = float((wc * conf).sum())
-    G2 = float((w[:, None] * ref * ref).sum())
-    return [float(v) for v in A], 0.5 * (G1 + G2)
+    G1, G2 = _seq_sum(g1), _seq_sum(g2)
+    return [float(v) for v in A], (G1 + G2) * 0.5
 
 
 def _div(a: float, b: float) -> float:

@@ -43,8 +43,10 @@ readings: the f64 one (keys without suffix) and the float32 one (``_avg32``:
 the average cast to float32 before lines 116-118).
 
 Output: tests/golden/reference_exec.npz (inputs as generator parameters, the
-reference's outputs).  Run from the repo root:
-    python tests/golden/make_reference_vectors.py
+reference's outputs) and tests/golden/reference_literal.npz (RMSF.py's own
+input shape -- 47,681 atoms, 214 CA, 10 frames under ``mpirun -n 2`` -- and
+the same at 2 and 4 frames).  Run from the repo root:
+    python tests/golden/make_reference_vectors.py [literal]
 """
 from __future__ import annotations
 
@@ -266,6 +268,44 @@ def main():
     print("wrote", OUT)
 
 
+# RMSF.py's literal input shape (RMSF.py:34,56: GRO/XTC = adk_oplsaa, 47,681
+# atoms, 214 CA, 10 frames, run as ``mpirun -n 2``: 5 frames per rank --
+# upstream facts) on synthetic frames, and the same shape at
+# 2 and 4 frames: the few-frame end where one f32 rounding flip of an aligned
+# coordinate weighs most (|x - mean| ulp / (N RMSF)).
+OUT_LITERAL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_literal.npz")
+LITERAL = dict(seed=61, n_atoms=47_681, n_sel=214, frames=(2, 4, 10), sizes=(1, 2), sel_seed=62, motion_seed=63)
+
+
+def main_literal():
+    from make_golden import motion_table
+
+    fns, code = load_reference()
+    L = LITERAL
+    sel = np.sort(np.random.default_rng(L["sel_seed"]).choice(L["n_atoms"], L["n_sel"], replace=False))
+    ca = np.full(len(sel), 12.011)  # CA masses (every selected atom a carbon, as for the reference's selection)
+    out = dict(seed=L["seed"], n_atoms=L["n_atoms"], sel=sel, masses=ca, frames=np.array(L["frames"]),
+               sizes=np.array(L["sizes"]))
+    nmax = max(L["frames"])
+    motion = motion_table(L["motion_seed"], nmax)
+    out["motion"] = motion
+    traj_all = SY.frames(L["seed"], L["n_atoms"], 0, nmax, motion)
+    for nf in L["frames"]:
+        traj = traj_all[:nf]  # the first nf frames of one trajectory
+        for P in L["sizes"]:
+            r = run_reference(fns, code, traj, sel, ca, P)
+            for k in ("rmsf", "mean", "m2", "average"):
+                out[f"{k}_F{nf}_P{P}"] = r[k]
+            out[f"blocks_F{nf}_P{P}"] = r["blocks"]
+            print(f"literal shape, {nf} frames, P={P}: blocks={r['blocks'].tolist()} rmsf[:3]={r['rmsf'][:3]}")
+    np.savez_compressed(OUT_LITERAL, **out)
+    print("wrote", OUT_LITERAL)
+
+
 if __name__ == "__main__":
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    main()
+    if sys.argv[1:] == ["literal"]:
+        main_literal()
+    else:
+        main()
+        main_literal()

@@ -79,13 +79,18 @@ def test_rmsf_exact_single_rank(kind, run_kw, batch):
     np.testing.assert_allclose(d.rmsf, r.rmsf, rtol=0, atol=1e-12)
 
 
-def test_rmsf_exact_rejects_alignment_and_splits():
+def test_rmsf_exact_rejects_splits_and_unaligned_records():
+    """exact=True runs the sequential kernels (aligned runs included since
+    round 6, tests/test_gpu_exact_aligned.py): no split grid, and no
+    per-frame records without an alignment."""
     from rmsf_amd import RMSF
     traj = SY.frames(1, 10, 0, 5)
-    with pytest.raises(NotImplementedError):
-        RMSF(traj, align="frame0", exact=True).run()
     with pytest.raises(ValueError):
         RMSF(traj, exact=True, n_splits=2).run()
+    with pytest.raises(ValueError):
+        RMSF(traj, exact=True, collect_rmsd=True).run()
+    r = RMSF(traj, align="frame0", exact=True).run().results
+    _same(r.rmsf, O.rmsf_script(traj, None, None, size=1, align="frame0")["rmsf"], "frame0 exact")
 
 
 def _exact_worker(rank, size, init, n_frames, root, q):

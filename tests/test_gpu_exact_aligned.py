@@ -1,0 +1,239 @@
+"""GPU tier: ``exact=True`` on the ALIGNED path -- RMSF.py:80-146 with the
+reference's own summation orders, bit for bit.
+
+rmsf_reference_setup_sequential (RMSF.py:84-85 / 111 + 117-118),
+rmsf_superpose_sequential (RMSF.py:94-97 / 127-131 + get_rotation_matrix,
+one lane per frame: the COM and qcprot's InnerProduct atom by atom) and
+rmsf_accumulate_sequential (RMSF.py:99-103 / 133-138, one lane per atom,
+frames in order) reproduce each statement's own rounding, so every
+comparison here is ``assert_array_equal`` on float64 bit patterns against
+  * tests/golden/reference_literal.npz -- RMSF.py's own statements executed
+    at its literal input shape (47,681 atoms, 214 CA, 10 frames; also 2 and
+    4 frames), P = 1 and 2 (two gloo ranks sharing the GPU);
+  * the oracle's restatement (rmsf_script) on other shapes, selections,
+    masses, frame subsets, batch splits and sources.
+The default (frame-parallel) aligned path is checked at the literal shape
+against the north star's 1e-6 A, and its margin printed."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, PKG, ROOT
+from oracle import rmsf_oracle as O
+from oracle import synth as SY
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-6
+
+
+def _bits(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64)).view(np.uint64)
+
+
+def _same(got, want, what):
+    np.testing.assert_array_equal(_bits(got), _bits(want), err_msg=what)
+
+
+@pytest.fixture(scope="module")
+def lit():
+    return np.load(os.path.join(GOLDEN, "reference_literal.npz"))
+
+
+@pytest.fixture(scope="module")
+def lit_traj(lit):
+    return SY.frames(int(lit["seed"]), int(lit["n_atoms"]), 0, int(lit["frames"].max()), lit["motion"])
+
+
+@pytest.mark.parametrize("where", ["host", "device"])
+@pytest.mark.parametrize("nf", [2, 4, 10])
+def test_literal_shape_exact_bit_for_bit(lit, lit_traj, nf, where):
+    """RMSF.py's input shape, one rank: exact=True equals the reference's
+    statements bit for bit -- RMSF, mean, sumsquares and the average."""
+    from rmsf_amd import RMSF
+    t = lit_traj[:nf]
+    x = torch.tensor(t, device="cuda") if where == "device" else t
+    r = RMSF(x, select=lit["sel"], masses=lit["masses"], align="average", exact=True).run().results
+    for k, got in (("rmsf", r.rmsf), ("mean", r.mean), ("m2", r.sumsquares), ("average", r.average)):
+        _same(got, lit[f"{k}_F{nf}_P1"], f"{k}, {nf} frames")
+
+
+@pytest.mark.parametrize("nf", [2, 4, 10])
+def test_literal_shape_default_path_margin(lit, lit_traj, nf):
+    """The default (frame-parallel) aligned path at RMSF.py's shape: within
+    1e-6 A of the reference statements (P = 1 and P = 2 blocks agree with
+    each other in the vectors to the last bit or nearly)."""
+    from rmsf_amd import RMSF
+    t = torch.tensor(lit_traj[:nf], device="cuda")
+    r = RMSF(t, select=lit["sel"], masses=lit["masses"], align="average").run().results
+    d = np.abs(r.rmsf - lit[f"rmsf_F{nf}_P1"]).max()
+    da = np.abs(r.average - lit[f"average_F{nf}_P1"]).max()
+    print(f"\nliteral shape, {nf} frames: default path max |dRMSF| {d:.3e} A, max |daverage| {da:.3e} A")
+    assert d < TOL and da < TOL
+
+
+def _lit_worker(rank, size, init, q, nf):
+    sys.path[:0] = [ROOT, PKG]
+    import torch
+    import torch.distributed as dist
+
+    from conftest import init_gloo
+    init_gloo(init, rank, size)
+    try:
+        from rmsf_amd import RMSF, parallel
+        from rmsf_amd.engine import Engine
+        from rmsf_amd.sources import DeviceSource
+        from rmsf_amd.synth import generate
+        lit = np.load(os.path.join(GOLDEN, "reference_literal.npz"))
+        eng = Engine(torch.device("cuda", 0))
+        b0, b1 = parallel.blocks(nf, size)[rank]
+        shard = generate(eng, int(lit["n_atoms"]), b0, max(b1 - b0, 1), seed=int(lit["seed"]),
+                         motion=lit["motion"])[: b1 - b0]
+        src = DeviceSource(shard, lit["sel"], offset=b0, n_traj=nf)
+        r = RMSF(src, masses=lit["masses"], align="average", exact=True).run().results
+        q.put((rank, r.rmsf, r.mean, r.sumsquares, r.average))
+    except Exception as e:  # surface the failure to the parent
+        q.put((rank, repr(e), None, None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nf", [2, 10])
+def test_literal_shape_exact_two_ranks(lit, nf):
+    """``mpirun -n 2`` at RMSF.py's shape: two ranks (gloo, sharing the GPU),
+    each holding only its RMSF.py:65-69 block; frame 0's owner computes the
+    first reference, sweep 1's sums meet in rank order (RMSF.py:110 -- any
+    order for two ranks), the partials in comm.reduce's order: every rank's
+    result equals the reference statements' P = 2 run bit for bit."""
+    from conftest import spawn_ranks
+    out = spawn_ranks(_lit_worker, 2, lambda r, init, q: (r, 2, init, q, nf), timeout=150)
+    for rank, rmsf, mean, m2, avg in out:
+        assert mean is not None, rmsf
+        _same(rmsf, lit[f"rmsf_F{nf}_P2"], f"rank {rank} rmsf")
+        _same(mean, lit[f"mean_F{nf}_P2"], f"rank {rank} mean")
+        _same(m2, lit[f"m2_F{nf}_P2"], f"rank {rank} sumsquares")
+        _same(avg, lit[f"average_F{nf}_P2"], f"rank {rank} average")
+
+
+# shape, selection, masses, frame subset, batch
+CASES = [
+    dict(n_atoms=600, nf=40, sel="every4", masses=None, align="average", batch=None, run={}),
+    dict(n_atoms=600, nf=40, sel="every4", masses="het", align="frame0", batch=7, run={}),
+    dict(n_atoms=3341, nf=98, sel="random214", masses="ca", align="average", batch=30, run={}),
+    dict(n_atoms=3341, nf=98, sel="random214", masses=None, align="frame0", batch=None,
+         run={"start": 3, "stop": 90, "step": 2}),
+    dict(n_atoms=2000, nf=5, sel="all", masses=None, align="average", batch=2, run={}),
+    dict(n_atoms=20000, nf=12, sel="all", masses="het", align="average", batch=None, run={}),
+    dict(n_atoms=50000, nf=3, sel="every3", masses=None, align="frame0", batch=None, run={}),
+    dict(n_atoms=700, nf=33, sel="all", masses=None, align="average", batch=None, run={"frames": [0, 4, 5, 17, 30]}),
+    dict(n_atoms=300, nf=1, sel="all", masses=None, align="average", batch=None, run={}),
+]
+
+
+def _case(c):
+    from rmsf_amd.synth import motion_table
+    n = c["n_atoms"]
+    traj = SY.frames(7, n, 0, c["nf"], motion_table(8, c["nf"]))
+    sel = {"all": np.arange(n), "every4": np.arange(1, n, 4), "every3": np.arange(0, n, 3),
+           "random214": np.sort(np.random.default_rng(9).choice(n, 214, replace=False))}[c["sel"]]
+    masses = {None: None, "ca": np.full(len(sel), 12.011),
+              "het": np.random.default_rng(10).uniform(1.0, 16.0, len(sel))}[c["masses"]]
+    return traj, sel, masses
+
+
+@pytest.mark.parametrize("where", ["host", "device"])
+@pytest.mark.parametrize("ci", range(len(CASES)))
+def test_exact_aligned_vs_oracle(ci, where):
+    from rmsf_amd import RMSF
+    c = CASES[ci]
+    traj, sel, masses = _case(c)
+    x = torch.tensor(traj, device="cuda") if where == "device" else traj
+    r = RMSF(x, select=sel, masses=masses, align=c["align"], exact=True, batch_frames=c["batch"],
+             collect_rmsd=True).run(**c["run"]).results
+    run = c["run"]
+    if "frames" in run:
+        # ref_frame is a TRAJECTORY frame (RMSF.py:63,83): prepend it so the
+        # oracle's traj[0] is that frame, then run over the listed frames
+        sub = traj[run["frames"]]
+        want = O.rmsf_script(np.concatenate([traj[:1], sub]), sel, masses, size=1, align=c["align"], start=1)
+    else:
+        want = O.rmsf_script(traj, sel, masses, size=1, align=c["align"], start=run.get("start"),
+                             stop=run.get("stop"), step=run.get("step"))
+    _same(r.rmsf, want["rmsf"], "rmsf")
+    _same(r.mean, want["mean"], "mean")
+    _same(r.sumsquares, want["m2"], "sumsquares")
+    if c["align"] == "average":
+        _same(r.average, want["average"], "average")
+
+
+@pytest.mark.parametrize("align", ["frame0", "average"])
+def test_exact_transforms_and_rmsd(align):
+    """The per-frame records of the last sweep: rotation, mobile COM and the
+    QCP rmsd equal the oracle's CalcRMSDRotationalMatrix on the same frame
+    against the same reference, bit for bit."""
+    from rmsf_amd import RMSF
+    from rmsf_amd.synth import motion_table
+    n, nf = 900, 17
+    traj = SY.frames(3, n, 0, nf, motion_table(4, nf))
+    sel = np.arange(0, n, 2)
+    m = np.random.default_rng(5).uniform(1.0, 16.0, len(sel))
+    r = RMSF(torch.tensor(traj, device="cuda"), select=sel, masses=m, align=align, exact=True,
+             collect_transforms=True, collect_rmsd=True).run().results
+    if align == "frame0":
+        ref_com, ref_c = O.centred_reference(traj[0][sel], m)
+    else:
+        avg = O.rmsf_script(traj, sel, m, size=1, align="average")["average"]
+        ref_com, ref_c = O.centred_reference(avg, m)
+    for f in range(nf):
+        p = traj[f][sel]
+        com = O.center_of_mass(p, m)
+        rot = np.zeros(9)
+        rmsd = O.CalcRMSDRotationalMatrix(ref_c, p.astype(np.float64) - com, len(sel), rot, None)
+        _same(r.transforms[f, :9], rot, f"rotation, frame {f}")
+        _same(r.transforms[f, 9:12], com, f"COM, frame {f}")
+        _same(r.transforms[f, 12], rmsd, f"rmsd, frame {f}")
+        _same(r.rmsd[f], rmsd, f"results.rmsd, frame {f}")
+
+
+def test_sequential_sum_batches_and_gather():
+    """rmsf_accumulate_sequential (SUM, aligned) continues k across batches
+    and reads a gathered selection: the sweep-1 sums equal RMSF.py:103's
+    frame-order sum (oracle rank_sweep1) bit for bit."""
+    from rmsf_amd.engine import Engine
+    from rmsf_amd.synth import generate, motion_table
+    from rmsf_amd._lib import RMSF_MODE_SUM, RMSF_XFORM_DOUBLES
+    eng = Engine()
+    n, nf = 5000, 23
+    mt = motion_table(6, nf)
+    dev = generate(eng, n, 0, nf, seed=12, motion=mt)
+    traj = dev.cpu().numpy()
+    sel = np.sort(np.random.default_rng(1).choice(n, 777, replace=False))
+    sd = eng.sel_tensor(sel)
+    mtot = float(len(sel))
+    _, ref, info = eng.reference_setup_seq(len(sel), mtot, frame_ptr=dev.data_ptr(), sel=sd)
+    xf = eng.empty(nf, RMSF_XFORM_DOUBLES)
+    eng.superpose_seq(dev.data_ptr(), 3 * n, nf, len(sel), sd, None, mtot, ref, info, xf)
+    s = eng.zeros(3 * len(sel))
+    for f0, f1 in ((0, 5), (5, 6), (6, nf)):
+        eng.accumulate_seq(dev.data_ptr() + 4 * 3 * n * f0, 3 * n, f1 - f0, len(sel), sd, xf[f0:f1], info,
+                           RMSF_MODE_SUM, f0, s, None)
+    torch.cuda.synchronize()
+    ref_com, ref_c = O.centred_reference(traj[0][sel])
+    _same(ref.cpu().numpy().reshape(-1), ref_c.reshape(-1), "reference")
+    want = O.rank_sweep1(traj, sel, None, 0, nf, ref_c, ref_com)
+    _same(s.cpu().numpy(), want.reshape(-1), "sweep-1 sums")
+
+
+def test_default_and_exact_agree():
+    """The frame-parallel aligned path and the exact one agree far inside
+    the tolerance on a many-frame run (where a flip weighs ulp/N)."""
+    from rmsf_amd import RMSF
+    from rmsf_amd.synth import motion_table
+    n, nf = 4000, 300
+    traj = torch.tensor(SY.frames(21, n, 0, nf, motion_table(22, nf)), device="cuda")
+    sel = np.arange(0, n, 7)
+    a = RMSF(traj, select=sel, align="average").run().results
+    b = RMSF(traj, select=sel, align="average", exact=True).run().results
+    assert np.abs(a.rmsf - b.rmsf).max() < 1e-9

@@ -113,6 +113,29 @@ def test_uniform_default_vs_ca_masses(ref, traj):
     assert np.abs(r["rmsf"] - ref["rmsf_ca_P1"]).max() < 1e-7
 
 
+@pytest.fixture(scope="module")
+def lit():
+    return np.load(os.path.join(GOLDEN, "reference_literal.npz"))
+
+
+@pytest.fixture(scope="module")
+def lit_traj(lit):
+    return SY.frames(int(lit["seed"]), int(lit["n_atoms"]), 0, int(lit["frames"].max()), lit["motion"])
+
+
+def test_oracle_bitwise_vs_reference_literal_shape(lit, lit_traj):
+    """RMSF.py's own input shape (47,681 atoms, 214 CA, 10 frames, P = 1 and
+    2 as ``mpirun -n 2``) and the same at 2 and 4 frames: the restatement
+    equals the reference statements bit for bit (rmsf, mean, sumsquares and
+    the sweep-1 average)."""
+    for nf in lit["frames"]:
+        for P in lit["sizes"]:
+            r = O.rmsf_script(lit_traj[:nf], lit["sel"], lit["masses"], size=int(P), align="average")
+            for k in ("rmsf", "mean", "m2", "average"):
+                np.testing.assert_array_equal(r[k], lit[f"{k}_F{nf}_P{P}"], err_msg=f"{k}, {nf} frames, P={P}")
+            assert [[b.start, b.stop] for b in O.block_ranges(int(nf), int(P))] == lit[f"blocks_F{nf}_P{P}"].tolist()
+
+
 # -- GPU tier ------------------------------------------------------------------
 
 @pytest.mark.gpu
