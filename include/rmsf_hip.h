@@ -114,6 +114,23 @@ int rmsf_superpose(const float *d_xyz, int64_t frame_stride, int64_t n_frames,
                    const double *d_refinfo, double *d_xform, void *d_work,
                    size_t work_bytes, void *stream);
 
+/* rmsf_superpose over a gathered selection (d_sel != NULL, rows) that also
+ * COMPACTS it: every frame's selected rows, as the covariance pass stages
+ * them, go out to d_dense_out[f][n_sel][3] (f32, an exact copy), so the
+ * passes after it -- the accumulate of this sweep, and with the whole block
+ * kept resident every pass of RMSF.py's second sweep -- read n_sel dense
+ * rows (d_sel = NULL, frame_stride = 3 n_sel) instead of gathering them
+ * again from the full frames.  Same records, same bits as rmsf_superpose;
+ * the gathered read touches every 128-B line that holds a selected atom,
+ * so at CA-like densities (1 in 10 and sparser) each avoided gather saves
+ * several times the selected bytes ("Sparse selections"). */
+int rmsf_superpose_compact(const float *d_xyz, int64_t frame_stride,
+                           int64_t n_frames, int64_t n_sel, const int32_t *d_sel,
+                           const double *d_masses, const double *d_ref,
+                           const double *d_refinfo, double *d_xform,
+                           void *d_work, size_t work_bytes, float *d_dense_out,
+                           void *stream);
+
 /* The same for frames stored as coordinate planes (SoA): atom a's x, y and
  * z of frame f at d_xyz + f*frame_stride + a (or d_sel[a]) + {0, 1, 2} *
  * plane_stride floats (frame_stride >= 3*plane_stride).  Same workspace,
@@ -668,7 +685,12 @@ int rmsf_ctx_set_staging(rmsf_ctx *ctx, int64_t batch_frames, int n_slots,
  * rmsf_ctx_kernel_time() synchronises and returns, for one kernel family,
  * the number of launches, their summed duration (ms) and the atom-frames
  * they processed (x 12 B = algorithmic bytes), then clears
- * that family's record.                                                      */
+ * that family's record.  Note: a push recorded for atom slabs
+ * (rmsf_multi_push_frames with merge_slabs > 1) is run whole before the
+ * timings are read, so reading them between that push and
+ * rmsf_multi_chan_merge_root makes the merge take its non-overlapped form
+ * (same bits; only the slab overlap is lost).  Read timings after the
+ * merge to keep the overlap.                                                 */
 #define RMSF_TIME_ACCUMULATE 0 /* rmsf_accumulate_balanced (RMSF.py:99-103,133-138) */
 #define RMSF_TIME_SUPERPOSE 1  /* rmsf_superpose (RMSF.py:94-97 + qcprot, :43-51)  */
 /* the cross-context merge, per context: from its packed moments to its
@@ -700,6 +722,19 @@ int rmsf_set_reference_frame(rmsf_ctx *ctx, const float *xyz,
 /* Reference = the context's sweep-1 average sum/n (RMSF.py:111-118);
  * RMSF_EEMPTY when no frame was summed.                                      */
 int rmsf_set_reference_average(rmsf_ctx *ctx);
+
+/* exact=True for the context (RMSF.py:80-146 with the reference's own
+ * summation orders, the sequential entry points above): with on != 0 the
+ * reference setters run rmsf_reference_setup_sequential, RMSF_PUSH_ALIGN_SUM
+ * / RMSF_PUSH_ALIGN_WELFORD run rmsf_superpose_sequential +
+ * rmsf_accumulate_sequential (RMSF_PUSH_WELFORD the sequential Welford, as
+ * RMSF_PUSH_EXACT), and rmsf_multi_allreduce_sum over contexts of this
+ * process adds the sums in rank order.  mass_total = numpy's masses.sum()
+ * of the selection (pairwise; n_sel for unit masses), the centre of mass's
+ * divisor.  Set it before the reference (an earlier reference is refused by
+ * the aligned pushes); merge the Welford states with
+ * rmsf_multi_chan_merge_exact.                                              */
+int rmsf_ctx_set_exact(rmsf_ctx *ctx, int on, double mass_total);
 
 /* Push n_frames float32 frames of n_atoms atoms (frame_stride floats apart,
  * 0 = 3*n_atoms; a multiple of it implements `step`).  is_device_ptr != 0:

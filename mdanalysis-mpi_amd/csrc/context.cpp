@@ -330,6 +330,12 @@ struct rmsf_ctx {
   hipStream_t comm_stream = nullptr;  // the slab merge's RCCL calls (beside the next slab)
   std::vector<hipEvent_t> ev_pack, ev_done;
   hipEvent_t ev_sent = nullptr;  // the exact merge: this context's state is ready to be read by a peer
+  hipEvent_t ev_pulled = nullptr;  // ... and a peer's copy of it (on this context's stream) has completed
+  // exact=True for aligned pushes (rmsf_ctx_set_exact): references, pushes and
+  // the sweep-1 sum exchange in the reference's own summation orders
+  bool exact = false;
+  double mass_total = 0.0;  // numpy's masses.sum() (pairwise), the COM divisor
+  bool ref_exact = false;   // the current reference record came from the sequential setup
   Worker *worker = nullptr;
 
   const int32_t *d_sel() const { return h_sel.empty() ? nullptr : static_cast<const int32_t *>(sel.p); }
@@ -462,12 +468,65 @@ int flush_fold(rmsf_ctx *c) {
                             c->pend.welford ? r.parts1.d() : nullptr, c->stream);
 }
 
+// exact mode, aligned or summing pushes: RMSF.py:94-103 / 127-138 with the
+// reference's summation orders -- rmsf_superpose_sequential for the frames'
+// records, rmsf_accumulate_sequential continuing the running state at k = n
+int process_exact(rmsf_ctx *c, const float *d_xyz, int64_t stride, int64_t n_frames, const int32_t *d_sel, int mode) {
+  const bool aligned = mode == RMSF_PUSH_ALIGN_SUM || mode == RMSF_PUSH_ALIGN_WELFORD;
+  const bool welford = mode == RMSF_PUSH_ALIGN_WELFORD;
+  const double *xf = nullptr;
+  if (aligned) {
+    if (!c->ref_set) return fail(RMSF_EINVAL, "rmsf_push: aligned mode before a reference was set");
+    if (!c->ref_exact)
+      return fail(RMSF_EINVAL, "rmsf_push: exact mode needs its reference set after rmsf_ctx_set_exact "
+                               "(the sequential setup's record)");
+    CX_OK(c->xform.ensure(sizeof(double) * RMSF_XFORM_DOUBLES * (size_t)n_frames, c->stream));
+    CX_OK(timed(c, RMSF_TIME_SUPERPOSE, c->n_sel * n_frames, [&] {
+      return rmsf_superpose_sequential(d_xyz, stride, n_frames, c->n_sel, d_sel, c->d_masses(), c->mass_total,
+                                       c->ref.d(), c->refinfo.d(), c->xform.d(), c->stream);
+    }));
+    xf = c->xform.d();
+    if (welford && c->collect_rmsd) {
+      const size_t need = sizeof(double) * (size_t)(c->n_rmsd + n_frames);
+      CX_OK(c->rmsd.ensure(need > c->rmsd.bytes ? std::max(need, 2 * c->rmsd.bytes) : need, c->stream, true));
+      CX_HIP(hipMemcpy2DAsync(c->rmsd.d() + c->n_rmsd, sizeof(double), c->xform.d() + 12,
+                              sizeof(double) * RMSF_XFORM_DOUBLES, sizeof(double), (size_t)n_frames,
+                              hipMemcpyDeviceToDevice, c->stream));
+      c->n_rmsd += n_frames;
+    }
+  }
+  Running &r = welford ? c->wel : c->sum;
+  const size_t row = sizeof(double) * c->n_coord;
+  CX_OK(r.parts0.ensure(row, c->stream, true));
+  if (welford) {
+    CX_OK(r.parts1.ensure(row, c->stream, true));
+    const size_t wb = rmsf_welford_sequential_workspace_bytes(n_frames);
+    CX_OK(c->seqwork.ensure(std::max<size_t>(wb, 16), c->stream));
+  }
+  CX_OK(timed(c, RMSF_TIME_ACCUMULATE, c->n_sel * n_frames, [&] {
+    return rmsf_accumulate_sequential(d_xyz, stride, n_frames, c->n_sel, d_sel, xf, aligned ? c->refinfo.d() : nullptr,
+                                      welford ? RMSF_MODE_WELFORD : RMSF_MODE_SUM, r.n, r.parts0.d(),
+                                      welford ? r.parts1.d() : nullptr, welford ? c->seqwork.p : nullptr,
+                                      welford ? c->seqwork.bytes : 0, c->stream);
+  }));
+  r.n += n_frames;
+  r.stale = false;
+  if (welford) {
+    c->wel_aligned = aligned;
+    c->rmsf_valid = false;
+    c->merged_away = false;
+  }
+  return RMSF_OK;
+}
+
 // one launch group over n_frames device frames: [superpose] + accumulate; its
 // fold is deferred (flush_fold / the merge's fused fold + pack)
 int process(rmsf_ctx *c, const float *d_xyz, int64_t stride, int64_t n_frames, const int32_t *d_sel, int mode) {
   const bool aligned = mode == RMSF_PUSH_ALIGN_SUM || mode == RMSF_PUSH_ALIGN_WELFORD;
   const bool welford = mode == RMSF_PUSH_WELFORD || mode == RMSF_PUSH_ALIGN_WELFORD;
   CX_OK(flush_fold(c));  // the workspace is about to be rewritten
+  if (c->exact && mode == RMSF_PUSH_WELFORD) mode = RMSF_PUSH_EXACT;  // the sequential Welford
+  if (c->exact && mode != RMSF_PUSH_EXACT) return process_exact(c, d_xyz, stride, n_frames, d_sel, mode);
   if (mode == RMSF_PUSH_EXACT) {
     // RMSF.py:137-138 as written, continuing the running state at k = n (a
     // reset state has n = 0: the kernel starts from zeros); the recurrence
@@ -1128,7 +1187,10 @@ void enable_peer(int dev, int peer) {
   if (hipDeviceEnablePeerAccess(peer, 0) != hipSuccess) (void)hipGetLastError();  // already enabled: fine
 }
 
-// d's stream copies s's Welford state (mean, M2) into d->xb after s's queued work
+// d's stream copies s's Welford state (mean, M2) into d->xb after s's queued
+// work; s's stream then waits for that copy, so nothing s does next (a reset,
+// a push, its destruction's drain) can overwrite or free the state while the
+// peer copy is in flight -- rmsf_ctx_synchronize(s) then covers the read too
 int pull_state(rmsf_ctx *d, rmsf_ctx *s, int64_t nc) {
   enable_peer(d->dev, s->dev);
   {
@@ -1136,12 +1198,18 @@ int pull_state(rmsf_ctx *d, rmsf_ctx *s, int64_t nc) {
     CX_OK(ensure_event(&s->ev_sent));
     CX_HIP(hipEventRecord(s->ev_sent, s->stream));
   }
-  DeviceScope dd(d->dev);
-  CX_OK(d->xb.ensure(sizeof(double) * 2 * nc, d->stream));
-  CX_HIP(hipStreamWaitEvent(d->stream, s->ev_sent, 0));
-  const size_t row = sizeof(double) * nc;
-  CX_HIP(hipMemcpyPeerAsync(d->xb.p, d->dev, s->wel.parts0.p, s->dev, row, d->stream));
-  CX_HIP(hipMemcpyPeerAsync(d->xb.d() + nc, d->dev, s->wel.parts1.p, s->dev, row, d->stream));
+  {
+    DeviceScope dd(d->dev);
+    CX_OK(d->xb.ensure(sizeof(double) * 2 * nc, d->stream));
+    CX_HIP(hipStreamWaitEvent(d->stream, s->ev_sent, 0));
+    const size_t row = sizeof(double) * nc;
+    CX_HIP(hipMemcpyPeerAsync(d->xb.p, d->dev, s->wel.parts0.p, s->dev, row, d->stream));
+    CX_HIP(hipMemcpyPeerAsync(d->xb.d() + nc, d->dev, s->wel.parts1.p, s->dev, row, d->stream));
+    CX_OK(ensure_event(&d->ev_pulled));
+    CX_HIP(hipEventRecord(d->ev_pulled, d->stream));
+  }
+  DeviceScope ds(s->dev);
+  CX_HIP(hipStreamWaitEvent(s->stream, d->ev_pulled, 0));  // the wait binds this record (reuse is safe)
   return RMSF_OK;
 }
 
@@ -1291,6 +1359,7 @@ RMSF_EXPORT int rmsf_ctx_destroy(rmsf_ctx *c) {
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->ev_main) (void)hipEventDestroy(c->ev_main);
     if (c->ev_sent) (void)hipEventDestroy(c->ev_sent);
+    if (c->ev_pulled) (void)hipEventDestroy(c->ev_pulled);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;  // DevBufs free on the context's device
   }
@@ -1418,6 +1487,7 @@ RMSF_EXPORT int rmsf_set_reference(rmsf_ctx *c, const double *h_ref, const doubl
   CX_HIP(hipMemcpyAsync(c->refinfo.p, info, sizeof(info), hipMemcpyHostToDevice, c->stream));
   CX_HIP(hipStreamSynchronize(c->stream));  // the host sources are the caller's / on this stack
   c->ref_set = true;
+  c->ref_exact = true;  // G_ref above is qcprot's per-atom order already
   return digest_reference(c);
 }
 
@@ -1433,8 +1503,14 @@ RMSF_EXPORT int rmsf_set_reference_frame(rmsf_ctx *c, const float *xyz, int is_d
     CX_HIP(hipStreamSynchronize(c->stream));
     d = static_cast<const float *>(c->frame.p);
   }
-  CX_OK(rmsf_reference_setup(d, nullptr, c->n_sel, c->d_sel(), c->d_masses(), c->ref.d(), c->refinfo.d(), c->stream));
+  if (c->exact)
+    CX_OK(rmsf_reference_setup_sequential(d, nullptr, 1.0, c->n_sel, c->d_sel(), c->d_masses(), c->mass_total,
+                                          nullptr, c->ref.d(), c->refinfo.d(), c->stream));
+  else
+    CX_OK(rmsf_reference_setup(d, nullptr, c->n_sel, c->d_sel(), c->d_masses(), c->ref.d(), c->refinfo.d(),
+                               c->stream));
   c->ref_set = true;
+  c->ref_exact = c->exact;
   return digest_reference(c);
 }
 
@@ -1444,10 +1520,25 @@ RMSF_EXPORT int rmsf_set_reference_average(rmsf_ctx *c) {
   DeviceScope ds(c->dev);
   CX_OK(settle(c));
   CX_OK(c->avg.ensure(sizeof(double) * c->n_coord, c->stream));
-  CX_OK(rmsf_reference_setup_mean(c->sum.parts0.d(), (double)c->sum.n, c->n_sel, c->d_masses(), c->avg.d(),
-                                  c->ref.d(), c->refinfo.d(), c->stream));
+  if (c->exact)
+    CX_OK(rmsf_reference_setup_sequential(nullptr, c->sum.parts0.d(), (double)c->sum.n, c->n_sel, nullptr,
+                                          c->d_masses(), c->mass_total, c->avg.d(), c->ref.d(), c->refinfo.d(),
+                                          c->stream));
+  else
+    CX_OK(rmsf_reference_setup_mean(c->sum.parts0.d(), (double)c->sum.n, c->n_sel, c->d_masses(), c->avg.d(),
+                                    c->ref.d(), c->refinfo.d(), c->stream));
   c->ref_set = true;
+  c->ref_exact = c->exact;
   return digest_reference(c);
+}
+
+RMSF_EXPORT int rmsf_ctx_set_exact(rmsf_ctx *c, int on, double mass_total) {
+  CX_OK(check_ctx(c, "rmsf_ctx_set_exact"));
+  if (on && !(mass_total > 0.0)) return fail(RMSF_EINVAL, "rmsf_ctx_set_exact: mass_total must be > 0");
+  c->exact = on != 0;
+  c->mass_total = on ? mass_total : 0.0;
+  c->ref_exact = false;  // a reference set before does not carry the sequential record's bits
+  return RMSF_OK;
 }
 
 RMSF_EXPORT int rmsf_push_frames(rmsf_ctx *c, const float *xyz, int64_t n_frames, int64_t stride, int mode,
@@ -1759,7 +1850,14 @@ RMSF_EXPORT int rmsf_multi_init_all(rmsf_ctx **cs, int n) {
 
 RMSF_EXPORT int rmsf_multi_allreduce_sum(rmsf_ctx **cs, int n) {
   Reduce red;
-  CX_OK(multi_reduce(cs, n, "rmsf_multi_allreduce_sum", &red));
+  int kind = 0;
+  CX_OK(multi_reduce(cs, n, "rmsf_multi_allreduce_sum", &red, &kind));
+  bool exact = true;
+  for (int i = 0; i < n; ++i) exact = exact && cs[i]->exact;
+  // exact contexts of this process: RMSF.py:110's sums added in rank order,
+  // ((s_0 + s_1) + s_2) + ... (local_reduce), not in RCCL's ring order --
+  // the same bits as any order for two ranks, this build's order beyond
+  if (exact && kind == 1 && whole_group_here(cs, n)) red = local_reduce(cs, n);
   return exchange_sum(cs, n, red, whole_group_here(cs, n));
 }
 

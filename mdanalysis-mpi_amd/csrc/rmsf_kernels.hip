@@ -1262,7 +1262,7 @@ template <bool GATHER, bool MASSES, bool VEC4, int WPE = 1, bool PLANES = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_frame_stats(
     const float *__restrict__ xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
     const int32_t *__restrict__ sel, const double *__restrict__ masses, const double *__restrict__ ref,
-    StatsPlan pl, double *__restrict__ part, int64_t ps = 0) {
+    StatsPlan pl, double *__restrict__ part, int64_t ps = 0, float *__restrict__ dense = nullptr) {
   __shared__ __attribute__((aligned(16))) float tile[kStatsLds];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1329,7 +1329,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         }
       }
     };
-    auto lstore = [&]() {
+    auto lstore = [&](int64_t t0) {
       if (VEC4) {
 #pragma unroll
         for (int k = 0; k < kNPre; ++k) {
@@ -1346,6 +1346,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
           d[0] = pel[3 * k];
           d[1] = pel[3 * k + 1];
           d[2] = pel[3 * k + 2];
+          // compaction (rmsf_superpose_compact): every (frame, selected atom)
+          // is staged exactly once over the grid, so its gathered row goes
+          // out once too, to the dense [frame][n_sel][3] copy the later
+          // passes read instead of re-gathering (an exact copy: same bits)
+          if (GATHER && !PLANES && dense != nullptr) {
+            const int64_t a = t0 + j;
+            if (a < a_end && f0 + row <= last) {
+              float *o = dense + (f0 + row) * 3 * n_sel + 3 * a;
+              o[0] = pel[3 * k];
+              o[1] = pel[3 * k + 1];
+              o[2] = pel[3 * k + 2];
+            }
+          }
         }
       }
     };
@@ -1394,7 +1407,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     gload(a_beg);
     for (int64_t t0 = a_beg; t0 < a_end; t0 += kTA) {
       __syncthreads();
-      lstore();
+      lstore(t0);
       __syncthreads();
       if (t0 + kTA < a_end) gload(t0 + kTA);
       const f32x4 *my = reinterpret_cast<const f32x4 *>(tile + lane * kPitch + (PLANES && VEC4 ? 0 : w * 3 * kAPW));
@@ -2246,7 +2259,7 @@ namespace {
 // coordinate-plane stride of SoA frames (PLANES kernels)
 int superpose_impl(const char *who, const float *d_xyz, int64_t fstride, int64_t ps, int64_t n_frames, int64_t n_sel,
                    const int32_t *d_sel, const double *d_masses, const double *d_ref, const double *d_refinfo,
-                   double *d_xform, void *d_work, size_t work_bytes, hipStream_t s) {
+                   double *d_xform, void *d_work, size_t work_bytes, hipStream_t s, float *d_dense = nullptr) {
   if (n_frames == 0) return RMSF_OK;
   const bool planes = ps > 0;
   if (!d_xyz || !d_ref || !d_refinfo || !d_xform || !d_work || n_sel < 1 || n_frames < 0 ||
@@ -2263,7 +2276,7 @@ int superpose_impl(const char *who, const float *d_xyz, int64_t fstride, int64_t
   auto stats = [&](auto P) {
     constexpr bool PL = decltype(P)::value;
 #define ST_LAUNCH(G, M, V) \
-  hipLaunchKernelGGL((k_frame_stats<G, M, V, 1, PL>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, plan, part, ps)
+  hipLaunchKernelGGL((k_frame_stats<G, M, V, 1, PL>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, plan, part, ps, d_dense)
     if (g && m) ST_LAUNCH(true, true, false);
     else if (g) ST_LAUNCH(true, false, false);
     else if (m && vec4) ST_LAUNCH(false, true, true);
@@ -2302,6 +2315,15 @@ RMSF_EXPORT int rmsf_superpose(const float *d_xyz, int64_t fstride, int64_t n_fr
                                void *stream) {
   return superpose_impl("rmsf_superpose", d_xyz, fstride, 0, n_frames, n_sel, d_sel, d_masses, d_ref, d_refinfo,
                         d_xform, d_work, work_bytes, S(stream));
+}
+
+RMSF_EXPORT int rmsf_superpose_compact(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
+                                       const int32_t *d_sel, const double *d_masses, const double *d_ref,
+                                       const double *d_refinfo, double *d_xform, void *d_work, size_t work_bytes,
+                                       float *d_dense_out, void *stream) {
+  if (!d_sel || !d_dense_out) return fail(RMSF_EINVAL, "rmsf_superpose_compact: needs a selection and an output");
+  return superpose_impl("rmsf_superpose_compact", d_xyz, fstride, 0, n_frames, n_sel, d_sel, d_masses, d_ref,
+                        d_refinfo, d_xform, d_work, work_bytes, S(stream), d_dense_out);
 }
 
 RMSF_EXPORT int rmsf_superpose_planes(const float *d_xyz, int64_t fstride, int64_t pstride, int64_t n_frames,

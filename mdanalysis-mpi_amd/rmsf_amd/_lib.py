@@ -59,6 +59,7 @@ SIGNATURES = {
     "rmsf_superpose_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "rmsf_superpose": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, P, P, P, c_size_t, P]),
     "rmsf_superpose_planes": (c_int, [P, c_int64, c_int64, c_int64, c_int64, P, P, P, P, P, P, c_size_t, P]),
+    "rmsf_superpose_compact": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, P, P, P, c_size_t, P, P]),
     "rmsf_accumulate_splits": (c_int, [c_int64, c_int64, c_int]),
     "rmsf_accumulate": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, c_int, c_int, P, P, P]),
     "rmsf_split_count": (c_int64, [c_int64, c_int, c_int]),
@@ -130,6 +131,7 @@ SIGNATURES = {
     "rmsf_ctx_reset": (c_int, [P, c_int]),
     "rmsf_ctx_set_timing": (c_int, [P, c_int]),
     "rmsf_ctx_collect_rmsd": (c_int, [P, c_int]),
+    "rmsf_ctx_set_exact": (c_int, [P, c_int, c_double]),
     "rmsf_get_rmsd": (c_int, [P, POINTER(c_int64), P, c_int64]),
     "rmsf_ctx_kernel_time": (c_int, [P, c_int, POINTER(c_int64), POINTER(c_double), POINTER(c_double)]),
     "rmsf_set_reference": (c_int, [P, P, P]),

@@ -160,6 +160,15 @@ class Context:
             call("rmsf_get_rmsd", self._h, ctypes.byref(n), out.ctypes.data, out.size)
         return out
 
+    def set_exact(self, on: bool = True, masses=None) -> None:
+        """exact=True (rmsf_ctx_set_exact): references, aligned pushes and
+        the sweep-1 sum exchange in RMSF.py's own summation orders.  The
+        centre of mass divides by numpy's ``masses.sum()`` of the selection
+        (``masses``: the context's, default unit masses -> n_sel).  Call it
+        before setting the reference."""
+        mt = float(np.ascontiguousarray(masses, dtype=np.float64).sum()) if masses is not None else float(self.n_sel)
+        call("rmsf_ctx_set_exact", self._h, 1 if on else 0, mt)
+
     def reset(self, welford: bool = True, sum: bool = True) -> None:  # noqa: A002
         call("rmsf_ctx_reset", self._h, (1 if welford else 0) | (2 if sum else 0))
 

@@ -360,7 +360,7 @@ def _exact_merge(ctxs, root: int, order: str) -> dict:
 
 def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int = 0, start=None, stop=None,
               step=None, batch_frames: int | None = None, frames=None, collect_rmsd: bool = False,
-              layout: str = "fac", merge_root: int | None = None, exact: bool = False,
+              layout: str = "fac", merge_root: int | None = None, exact: bool | None = None,
               merge_order: str = "mpi4py") -> dict:
     """RMSF.py's computation over the devices ``gpus`` from one process.
     Returns the ``results`` fields (rmsf, mean, sumsquares, n_frames, ...;
@@ -368,15 +368,17 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
     frame-list order, the by-product RMSF.py:48 discards).  ``merge_root``:
     the final merge is a reduce to that device index (RMSF.py:143's shape)
     and the results are read from it; None = an all-reduce, read from
-    device index 0 (the same numbers).  ``exact`` (align=None): every
-    device runs RMSF.py:137-138's recurrence over its block (RMSF_PUSH_EXACT)
-    and the blocks are reduced by second_order_moments in ``merge_order``
-    (RMSF.py:143's comm.reduce: "mpi4py", its default binomial tree, or
-    "rank"), device to device: the script's arithmetic bit for bit."""
+    device index 0 (the same numbers).  ``exact``: every device runs
+    RMSF.py's statements over its block in the reference's summation orders
+    (rmsf_ctx_set_exact: the sequential references, superposition and
+    accumulate; align=None: RMSF.py:137-138's recurrence, RMSF_PUSH_EXACT),
+    the sweep-1 sums meet in rank order, and the blocks are reduced by
+    second_order_moments in ``merge_order`` (RMSF.py:143's comm.reduce:
+    "mpi4py", its default binomial tree -- restated from mpi4py's published
+    source, unverified here -- or "rank"), device to device: the script's
+    arithmetic bit for bit."""
     from ._lib import merge_order as _order
     _order(merge_order)
-    if exact and align is not None:
-        raise NotImplementedError("exact=True covers align=None (RMSF.py:120-146 on an aligned trajectory)")
     if align not in (None, "frame0", "average"):
         raise ValueError(f"align must be one of (None, 'frame0', 'average'), got {align!r}")
     if parallel.world()[1] > 1:
@@ -393,6 +395,9 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
     fl = FrameList(src.n_traj, start, stop, step, frames=frames)
     if len(fl) == 0:
         raise RmsfEmptyError(-4, "RMSF.run", "no frames selected")
+    if exact is None:  # the pipeline's default: exact for few-frame aligned runs
+        from .pipeline import auto_exact
+        exact = auto_exact(align, len(fl))
     if align is not None and not 0 <= ref_frame < src.n_traj:
         raise IndexError(f"ref_frame {ref_frame} outside the trajectory ({src.n_traj} frames)")
     if masses is None and align is not None and isinstance(src, _AtomGroupFrames):
@@ -421,6 +426,9 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
     else:
         ctxs = [Context(src.n_atoms, sel=src.sel, masses=masses, device=d) for d in devs]
     try:
+        if exact and align is not None:
+            for c in ctxs:
+                c.set_exact(True, masses)
         if len(set(devs)) == len(devs) and len(devs) > 1:
             Context.init_all(ctxs)  # ncclCommInitAll: one communicator per device
         if collect_rmsd:
@@ -473,7 +481,7 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
         # rmsf_multi_push_frames call (every context's launches from its own
         # host thread; from 1M atoms the unaligned sweep runs in atom slabs
         # beside the merge's collectives)
-        whole = (isinstance(src, _DeviceShards) and not staged
+        whole = (isinstance(src, _DeviceShards) and not staged and not exact
                  and all(len(runs) <= 1 and all(r.step == 1 for r in runs) for runs in blocks))
 
         def multi_push(mode):
@@ -499,7 +507,9 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
         if collect_rmsd:
             for c in ctxs:  # the last sweep's rmsd only, as the pipeline reports it
                 c.collect_rmsd(True)
-        last = PUSH_EXACT if exact else (PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD)
+        last = PUSH_WELFORD if align is None else PUSH_ALIGN_WELFORD
+        if exact and align is None:
+            last = PUSH_EXACT
         if whole:
             multi_push(last)
         else:
@@ -507,6 +517,8 @@ def run_multi(inp, gpus, *, select=None, align=None, masses=None, ref_frame: int
         if exact:
             out.update(_exact_merge(ctxs, merge_root or 0, merge_order),
                        blocks=[(int(b0), int(b1)) for b0, b1 in spans], devices=devs, merge_order=merge_order)
+            if collect_rmsd:
+                out["rmsd"] = np.concatenate([c.rmsd() for c in ctxs])
             return out
         Context.multi_chan_merge(ctxs, root=merge_root)
         home = ctxs[merge_root or 0]

@@ -25,7 +25,7 @@ from . import parallel
 from ._lib import (RMSF_MAX_SPLIT_FRAMES, RMSF_MODE_SUM, RMSF_MODE_WELFORD, RMSF_REFINFO_DOUBLES, RMSF_XFORM_DOUBLES,
                    RmsfEmptyError)
 from .engine import Engine
-from .sources import Batch, DeviceSource, FrameList
+from .sources import Batch, DeviceSource, FrameList, _scattered
 
 ALIGN_MODES = (None, "frame0", "average")
 
@@ -190,15 +190,55 @@ class Superposer:
         nbytes = eng.workspace_bytes(n_sel, max_batch)
         self.work = eng.empty(max(1, (nbytes + 7) // 8))
 
-    def run(self, b: Batch, ref: torch.Tensor, refinfo: torch.Tensor) -> torch.Tensor:
+    def run(self, b: Batch, ref: torch.Tensor, refinfo: torch.Tensor, dense_out: int | None = None) -> torch.Tensor:
         xf = self.xform[: b.n_frames]
         need = self.eng.workspace_bytes(self.n_sel, b.n_frames)
         if need > self.work.numel() * 8:  # stats_plan's bytes are not monotone in the batch size
             self.work = self.eng.empty((need + 7) // 8)
         with _span(self.timer, "superpose", b.n_frames * self.n_sel):
             self.eng.superpose(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, self.masses, ref, refinfo, xf,
-                               self.work, pstride=b.pstride)
+                               self.work, pstride=b.pstride, dense_out=dense_out)
         return xf
+
+
+# Compaction of gathered selections on the aligned path (round 6): a gathered
+# row read costs every 128-B line holding a selected atom, so below this
+# density the superpose pass writes the selected rows out once (an exact
+# copy) and the later passes read them dense ("Sparse
+# selections"; the threshold is measured there)
+COMPACT_MAX_DENSITY = 0.5
+
+
+class _Compactor:
+    """The dense [frames, n_sel, 3] copy of a gathered selection's rows,
+    written by rmsf_superpose_compact as the first pass over each batch reads
+    it.  ``resident``: the whole block fits (at most half the free HBM), so a
+    later sweep (RMSF.py:124) reads it with no gather at all; otherwise the
+    copy is per batch of ``frames`` frames."""
+
+    max_bytes: int | None = None  # None: half the free HBM (tests set a small cap for the per-batch form)
+
+    def __init__(self, eng: Engine, n_sel: int, n_local: int, max_batch: int):
+        self.n_sel = n_sel
+        row = 12 * n_sel
+        budget = self.max_bytes
+        if budget is None:
+            budget = torch.cuda.mem_get_info(eng.device)[0] // 2
+        cap = max(1, budget // row)
+        self.resident = n_local <= cap
+        self.frames = n_local if self.resident else max(1, min(max_batch, cap))
+        self.buf = torch.empty((max(1, self.frames), n_sel, 3), dtype=torch.float32, device=eng.device)
+        self.filled = False
+
+    def ptr(self, k: int) -> int:
+        return self.buf.data_ptr() + 12 * self.n_sel * k
+
+    def dense(self, k: int, n: int) -> Batch:
+        return Batch(self.ptr(k), 3 * self.n_sel, n, None)
+
+    def resident_batches(self, n_local: int, max_batch: int):
+        for k in range(0, n_local, max_batch):
+            yield self.dense(k, min(max_batch, n_local - k))
 
 
 @dataclass
@@ -217,6 +257,32 @@ class PipelineResult:
     transforms: torch.Tensor | None = None
     transforms_sweep1: torch.Tensor | None = None
     extras: dict = field(default_factory=dict)
+
+
+# Below this many frames an aligned run takes the exact path by default.  One
+# f32 rounding flip of an aligned coordinate (the frame-parallel sums round
+# the rotation differently, RMSF.py:99-101) moves that atom's RMSF by
+# |x_k - mean| ulp(x) (1 - 1/N) / (N RMSF) <= ulp(x) / sqrt(N), since
+# |x_k - mean| <= sqrt(N) RMSF; with coordinates below 256 A (ulp <= 1.53e-5 A)
+# that bound is under the north star's 1e-6 A from 234 frames.  Measured:
+# 7 of 1,600 runs of 2-10 frames exceed 1e-6 A on the frame-parallel path
+# (worst 2.98e-6 A), none on the exact one (profiles/r06_workloads/
+# fuzz_fewframes_50seeds.txt); DESIGN section 5.
+AUTO_EXACT_FRAMES = 256
+
+
+def auto_exact(align, n_frames: int, *, n_splits=None, merge_scatter: bool = False, merge_slabs=None) -> bool:
+    """exact=None's choice: the sequential (bit-exact) path for aligned runs
+    of fewer than AUTO_EXACT_FRAMES frames, where the frame-parallel path's
+    rounding could exceed 1e-6 A; not where the caller asked for a
+    frame-parallel-only form (split grid, scatter merge, atom slabs)."""
+    return (align is not None and 0 < n_frames < AUTO_EXACT_FRAMES and not n_splits and not merge_scatter
+            and merge_slabs in (None, 0, 1))
+
+
+def _scattered_block(frames: FrameList, b0: int, b1: int, max_batch: int) -> bool:
+    """The source reads this block as gathered compact batches already."""
+    return _scattered(frames, b0, b1, max_batch)
 
 
 def reference_from_frame(eng: Engine, source, frame: int, n_sel: int, masses, owner: int | None = None,
@@ -356,7 +422,8 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                  ref_owner: int | None = None, block: tuple[int, int] | None = None,
                  timer: KernelTimer | None = None, collect_transforms: bool = False,
                  merge_slabs: int | None = None, merge_root: int | None = None,
-                 merge_scatter: bool = False, exact: bool = False, merge_order: str = "mpi4py") -> PipelineResult:
+                 merge_scatter: bool = False, exact: bool | None = None, merge_order: str = "mpi4py",
+                 compact: bool | None = None) -> PipelineResult:
     """``merge_slabs`` (N > 1, no alignment, HBM-resident block in one batch,
     flat chunk-aligned plan): cut the final sweep into that many atom slabs
     so each slab's cross-rank all-reduce overlaps the next slab's stream;
@@ -380,9 +447,18 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     second_order_moments in RMSF.py:143's comm.reduce order (``merge_order``:
     "mpi4py", mpi4py's default binomial tree, or "rank";
     parallel.global_chan_exact), then RMSF.py:146: results bit-identical to
-    RMSF.py's (on the restated upstream orders)."""
+    RMSF.py's (on the restated upstream orders).
+    ``exact=None`` (default): exact for an aligned run of fewer than
+    AUTO_EXACT_FRAMES frames (auto_exact), the frame-parallel path otherwise.
+    ``compact`` (aligned runs over a gathered selection of HBM-resident
+    rows): the first pass writes the selected rows out dense and the later
+    passes read them (_Compactor); None = below COMPACT_MAX_DENSITY selected
+    atoms per frame atom.  Same bits either way."""
     if align not in ALIGN_MODES:
         raise ValueError(f"align must be one of {ALIGN_MODES}, got {align!r}")
+    if exact is None:
+        exact = auto_exact(align, len(frames), n_splits=n_splits, merge_scatter=merge_scatter,
+                           merge_slabs=merge_slabs)
     if exact:
         if n_splits or merge_scatter or merge_slabs not in (None, 0, 1):
             raise ValueError("exact=True runs the sequential kernels: no n_splits, merge_scatter or merge_slabs")
@@ -427,6 +503,13 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     batches_of = source.raw_batches if planes else source.batches
     if not planes and not n_splits and isinstance(source, DeviceSource) and source.layout == "soa":
         batches_of = source.plane_batches_in_place  # the kernels' plane variants read HBM planes in place
+    gathered = (aligned and not planes and isinstance(source, DeviceSource) and source.layout == "fac"
+                and source.sel_dev is not None and not _scattered_block(frames, b0, b1, max_batch))
+    if compact is None:
+        compact = gathered and n_sel <= COMPACT_MAX_DENSITY * source.n_atoms
+    cmp = _Compactor(eng, n_sel, n_local, max_batch) if (compact and gathered and n_local) else None
+    if cmp is not None and not cmp.resident:
+        max_batch = min(max_batch, cmp.frames)
     sup = Superposer(eng, n_sel, max_batch, m_dev, timer) if aligned else None
     rmsd = eng.empty(n_local) if (aligned and collect_rmsd) else None
     keep = aligned and collect_transforms
@@ -436,10 +519,19 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
 
     def sweep(acc: Accumulator, ref=None, info=None, xf_out=None, pack=None, slabs=None, fin=None):
         done, slabbed = 0, None
-        for b in batches_of(frames, b0, b1, max_batch, eng.stream):
-            xf = None
+        if cmp is not None and cmp.resident and cmp.filled:   # a later sweep: the dense block, no gather
+            batches = cmp.resident_batches(n_local, max_batch)
+        else:
+            batches = batches_of(frames, b0, b1, max_batch, eng.stream)
+        for b in batches:
+            xf, src_b = None, b
             if aligned:
-                xf = sup.run(b, ref, info)
+                if cmp is not None and b.sel is not None:
+                    k = done if cmp.resident else 0
+                    xf = sup.run(b, ref, info, dense_out=cmp.ptr(k))
+                    b = cmp.dense(k, b.n_frames)   # the accumulate reads the dense rows
+                else:
+                    xf = sup.run(b, ref, info)
                 if rmsd is not None:
                     rmsd[done:done + b.n_frames].copy_(xf[:, 12])
                 if xf_out is not None:
@@ -456,7 +548,9 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
             if slabbed is None:
                 acc.add(b, xf, info, pack if last else None, fin if last else None)
             done += b.n_frames
-            b.done()
+            src_b.done()
+        if cmp is not None and cmp.resident:
+            cmp.filled = True
         return slabbed
 
     if align == "average":

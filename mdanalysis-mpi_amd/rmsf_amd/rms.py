@@ -90,15 +90,27 @@ class RMSF:
         rank's ``results.atom_slice``, ``slice_mean`` and
         ``slice_sumsquares`` hold its slice (``mean``/``sumsquares`` are
         None).
-    exact : bool
-        ``align=None`` only: compute RMSF.py:120-146 with the reference's own
-        arithmetic -- each rank's frames through the per-frame Welford of
-        RMSF.py:137-138 in order (rmsf_welford_sequential), the ranks folded
-        by second_order_moments in RMSF.py:143's reduce order
-        (``merge_order``), RMSF.py:146 -- so ``results`` are bit-identical to
-        the script's on the same float32 coordinates (``mean``,
-        ``sumsquares`` and ``rmsf``).  About 1.3x the time of the default
-        frame-parallel path, which agrees with it to ~1e-13.
+    exact : bool | None
+        True: compute RMSF.py with the reference's own arithmetic and
+        summation orders, so ``results`` are bit-identical to the script's
+        on the same float32 coordinates (``mean``, ``sumsquares``, ``rmsf``
+        and, aligned, ``average``, ``rmsd`` and ``transforms``).
+        align=None: RMSF.py:120-146, each rank's frames through the
+        per-frame Welford of RMSF.py:137-138 in order
+        (rmsf_welford_sequential) -- about 1.15x the default path's time on
+        all-atom rows and about 1.0x over large gathered selections
+        (BENCH_r05 ``modes.c2_exact``; INTEGRATION.md).  Aligned:
+        RMSF.py:80-146, the references, every frame's COM and qcprot inner
+        product atom by atom, the sweep-1 sum and Welford frame by frame
+        (the rmsf_*_sequential kernels) -- serial in a frame's atoms, so its
+        cost grows with the selection.  The ranks are
+        folded by second_order_moments in RMSF.py:143's reduce order
+        (``merge_order``), then RMSF.py:146.  False: the frame-parallel
+        path, which agrees to ~1e-13 unaligned and, aligned, to within one
+        f32 rounding flip of an aligned coordinate -- at most ulp(x) /
+        sqrt(n_frames), i.e. < 1e-6 A from ~234 frames.  None (default):
+        exact for aligned runs of fewer than 256 frames
+        (pipeline.AUTO_EXACT_FRAMES), the frame-parallel path otherwise.
     merge_order : "mpi4py" | "rank"
         ``exact=True`` with several ranks or devices: the order in which
         RMSF.py:143's ``comm.reduce(S, op=second_order_moments)`` applies
@@ -106,8 +118,10 @@ class RMSF:
         (``rc.fast_reduce``), a binomial tree -- at 4 ranks
         op(op(S0, S1), op(S2, S3)) -- run point to point as mpi4py runs it;
         "rank": op folded in rank order (``rc.fast_reduce = False``).  The
-        two agree up to 3 ranks and differ in the last bits from 4.  (mpi4py
-        is upstream; its order is restated, not verified, here.)
+        two agree up to 3 ranks and differ in the last bits from 4.  mpi4py
+        is upstream and absent here: its tree is restated from its published
+        source, not verified, so from 4 ranks the bit-for-bit claim rests on
+        that restatement (parity unpinned there).
     gpus : int | list of int, optional
         Drive this many devices (or these device ids) from one process: each
         takes the RMSF.py:65-69 block of its index and the blocks merge over
@@ -122,7 +136,7 @@ class RMSF:
                  device=None, batch_frames: int | None = None, n_splits: int | None = None,
                  collect_rmsd: bool = False, verbose: bool = False, gpus=None,
                  collect_transforms: bool = False, layout: str = "fac", merge_root: int | None = None,
-                 merge_scatter: bool = False, exact: bool = False, merge_order: str = "mpi4py", **kwargs):
+                 merge_scatter: bool = False, exact: bool | None = None, merge_order: str = "mpi4py", **kwargs):
         if layout not in ("fac", "soa"):
             raise ValueError(f"layout must be 'fac' or 'soa', got {layout!r}")
         if layout == "soa" and not (isinstance(atomgroup, np.ndarray) or isinstance(atomgroup, torch.Tensor)):
@@ -131,7 +145,7 @@ class RMSF:
         self.layout = layout
         self.merge_root = merge_root
         self.merge_scatter = bool(merge_scatter)
-        self.exact = bool(exact)
+        self.exact = None if exact is None else bool(exact)
         from ._lib import merge_order as _order
         _order(merge_order)
         self.merge_order = merge_order

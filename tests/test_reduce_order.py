@@ -289,6 +289,42 @@ def test_context_exact_push_and_merge(red, P, root):
             c.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("root", [None, 2])
+def test_context_reuse_right_after_exact_merge(red, root):
+    """ADVICE r5 (write-after-read across streams): the exact merge's peer
+    copies read other contexts' states on the reader's stream; every source
+    context's stream now waits for those copies.  Resetting and pushing new
+    frames into context 0 and a merged-away source straight after the merge
+    (no synchronisation) leaves the receivers' results the script's bits."""
+    from rmsf_amd.context import PUSH_EXACT, Context
+    P = 4
+    traj, sel = _traj(red), red["sel"]
+    ctxs = [Context(traj.shape[1], sel=sel) for _ in range(P)]
+    try:
+        for c, b in zip(ctxs, O.block_ranges(traj.shape[0], P)):
+            if len(b):
+                c.push(traj[b.start:b.stop], PUSH_EXACT)
+        Context.multi_chan_merge_exact(ctxs, root=root)
+        reused = [0, 1] if root is not None else [0]
+        noise = np.ascontiguousarray(traj[::-1][:7] + np.float32(3.0))
+        for i in reused:  # overwrite the states the merge read, at once
+            ctxs[i].reset()
+            ctxs[i].push(noise, PUSH_EXACT)
+        check = [root] if root is not None else [1, 2, 3]
+        for i in check:
+            n, mean, m2 = ctxs[i].partial()
+            assert n == traj.shape[0]
+            _same(mean, red[f"tree_mean_P{P}"], f"context {i} mean")
+            _same(m2, red[f"tree_m2_P{P}"], f"context {i} m2")
+        for i in reused:  # and the reused contexts hold their new frames alone
+            n, _, _ = ctxs[i].partial()
+            assert n == 7
+    finally:
+        for c in ctxs:
+            c.close()
+
+
 @pytest.mark.parametrize("P", [2, 3, 4, 5, 6, 7, 8, 9, 16, 33])
 def test_abi_schedule_drives_oracle_fold(P):
     """The C ABI's schedule (rmsf_chan_reduce_steps), applied on the host
