@@ -84,6 +84,9 @@ def parse(argv=None):
     ap.add_argument("--frames", type=int, default=None,
                     help="trajectory frames (strong) or frames per GPU (weak); default: the workload's")
     ap.add_argument("--frames-per-gpu", type=int, default=None, help="shorthand for --scaling weak --frames F")
+    ap.add_argument("--one-process", action="store_true",
+                    help="the one-process context form (main_single_process) even at --gpus 1: one device "
+                         "context, a one-rank ncclCommInitAll communicator")
     ap.add_argument("--rehearse", action="store_true",
                     help="one-process --gpus N with fewer devices: list device 0 N times (rehearsal)")
     ap.add_argument("--rehearse-transport", choices=["fold", "noop"], default="fold",
@@ -448,7 +451,9 @@ def sparse_selection_modes(eng, a, traj, n_atoms: int, n_total: int) -> dict:
     220) under the two sweeps -- each timed with the selected rows compacted
     by the first pass (the default below COMPACT_MAX_DENSITY) and re-gathered
     by every pass (compact=False), same bits.  Rates and roofline fractions
-    count the SELECTED bytes (12 B per selected atom-frame per sweep)."""
+    count the SELECTED bytes (12 B per selected atom-frame per sweep); the
+    gather reads every 128-B line that holds a selected atom, which at 1 in
+    10 is nearly every line of the frames."""
     import numpy as np
     import torch
 
@@ -481,6 +486,7 @@ def sparse_selection_modes(eng, a, traj, n_atoms: int, n_total: int) -> dict:
             res[compact] = r.rmsf
             ks, s_ms, _ = t.totals("superpose")
             ka, a_ms, _ = t.totals("accumulate")
+            kc, c_ms, _ = t.totals("compact")
             step_ms = dt / a.mode_steps * 1e3
             sel_bytes = B_PER_ATOM_FRAME * n_sel * n_total * sweeps
             key = "compacted" if compact else "regathered"
@@ -488,7 +494,8 @@ def sparse_selection_modes(eng, a, traj, n_atoms: int, n_total: int) -> dict:
                         "selected_gbs": sel_bytes / (step_ms / 1e3) / 1e9,
                         "frac_of_single_read_roofline": sel_bytes / (step_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
                         "superpose_ms_per_step": s_ms / a.mode_steps, "superpose_launches": ks // a.mode_steps,
-                        "accumulate_ms_per_step": a_ms / a.mode_steps, "accumulate_launches": ka // a.mode_steps}
+                        "accumulate_ms_per_step": a_ms / a.mode_steps, "accumulate_launches": ka // a.mode_steps,
+                        "compact_ms_per_step": c_ms / a.mode_steps, "compact_launches": kc // a.mode_steps}
         row["speedup_compacted"] = row["regathered"]["ms_per_step"] / row["compacted"]["ms_per_step"]
         row["same_bits"] = bool(torch.equal(res[True], res[False]))
         if not row["same_bits"]:
@@ -579,8 +586,8 @@ def main_single_process(a, wl, cpu) -> None:
         c = Context(n_atoms, device=d)
         c.set_timing(True)
         ctxs.append(c)
-    if not rehearsal and n > 1:
-        Context.init_all(ctxs)
+    if not rehearsal:
+        Context.init_all(ctxs)  # ncclCommInitAll, also for one device (--one-process): the RCCL merge path
     noop = rehearsal and a.rehearse_transport == "noop"
     if noop:
         Context.multi_set_transport(ctxs, TRANSPORT_NOOP)
@@ -668,7 +675,7 @@ def main():
     launched = "WORLD_SIZE" in os.environ
     if launched and a.gpus != world and not a.backend == "gloo":
         raise SystemExit(f"--gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
-    single_multi = not launched and a.gpus > 1
+    single_multi = not launched and (a.gpus > 1 or a.one_process)
     n_gpus = a.gpus if single_multi else world
     wl = resolve(a, n_gpus)
     n_atoms, n_total = wl["n_atoms"], wl["n_total"]

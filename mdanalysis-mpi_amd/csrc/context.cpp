@@ -349,6 +349,20 @@ int check_ctx(const rmsf_ctx *c, const char *fn) {
   return RMSF_OK;
 }
 
+// Every stream, event and buffer a context owns lives on the context's
+// device.  The creation sites check that this device is current (a missing
+// DeviceScope on a worker thread would otherwise create them on device 0:
+// the bug class of ADVICE r4) -- DevBuf::ensure checks the same against its
+// stream's device.  A one-GPU box never trips these; they guard the
+// multi-device paths that have not run on distinct devices here.
+int on_device(const rmsf_ctx *c, const char *what) {
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess || cur != c->dev)
+    return fail(RMSF_EHIP, std::string("internal: ") + what + " for a device-" + std::to_string(c->dev) +
+                               " context created while device " + std::to_string(cur) + " is current");
+  return RMSF_OK;
+}
+
 // the context stream and its side stream (a shift frame's gather reads a
 // caller's frame there): what a getter waits for before the caller may free
 // what it pushed
@@ -383,6 +397,7 @@ template <class F>
 int timed(rmsf_ctx *c, int which, int64_t atom_frames, F &&launch) {
   if (!c->timing) return launch();
   rmsf_ctx::Span sp{nullptr, nullptr, which, atom_frames, true};
+  if (c->event_pool.size() < 2) CX_OK(on_device(c, "a timing event"));
   auto take = [c](hipEvent_t *e) -> hipError_t {
     if (c->event_pool.empty()) return hipEventCreate(e);
     *e = c->event_pool.back();
@@ -407,6 +422,7 @@ int timed(rmsf_ctx *c, int which, int64_t atom_frames, F &&launch) {
 // as each device's stream sees them.
 int merge_open(rmsf_ctx *c, hipStream_t s) {
   if (!c->timing) return RMSF_OK;
+  if (c->event_pool.size() < 2) CX_OK(on_device(c, "a merge timing event"));
   hipEvent_t a = nullptr, b = nullptr;
   auto take = [c](hipEvent_t *e) -> hipError_t {
     if (c->event_pool.empty()) return hipEventCreate(e);
@@ -611,6 +627,7 @@ int settle(rmsf_ctx *c) {
 
 // order the side stream after everything queued on the context stream so far
 int side_begin(rmsf_ctx *c) {
+  if (!c->side || !c->ev_main) CX_OK(on_device(c, "the side stream / its event"));
   if (!c->side) CX_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
   if (!c->ev_main) CX_HIP(hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming));
   CX_HIP(hipEventRecord(c->ev_main, c->stream));
@@ -629,7 +646,10 @@ int digest_into(rmsf_ctx *c, int which, const void *a, bool words32, int64_t n, 
     CX_HIP(hipHostMalloc(&h, sizeof(unsigned long long), hipHostMallocDefault));
     c->h_dig[which] = static_cast<unsigned long long *>(h);
   }
-  if (!c->ev_dig[which]) CX_HIP(hipEventCreateWithFlags(&c->ev_dig[which], hipEventDisableTiming));
+  if (!c->ev_dig[which]) {
+    CX_OK(on_device(c, "a digest event"));
+    CX_HIP(hipEventCreateWithFlags(&c->ev_dig[which], hipEventDisableTiming));
+  }
   CX_HIP(hipMemsetAsync(out.p, 0, sizeof(unsigned long long), c->side));
   const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (n + n_info + 1023) / 1024));
   auto *o = static_cast<unsigned long long *>(out.p);
@@ -1088,7 +1108,11 @@ int slab_merge(rmsf_ctx **cs, int n, int kind, const Reduce &red, int root) {
     CX_OK(c->accwork.ensure(std::max<size_t>(wb, 16), c->stream));
     CX_OK(c->xa.ensure(sizeof(double) * 2 * nc, c->stream));
     if (rc_l) {
-      if (!c->comm_stream) CX_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+      if (!c->comm_stream) {
+        CX_OK(on_device(c, "the slab merge's stream"));
+        CX_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+      }
+      if (c->ev_pack.size() < ns) CX_OK(on_device(c, "the slab merge's events"));
       while (c->ev_pack.size() < ns) {
         hipEvent_t a = nullptr, b = nullptr;
         CX_HIP(hipEventCreateWithFlags(&a, hipEventDisableTiming));
@@ -1172,8 +1196,11 @@ int slab_merge(rmsf_ctx **cs, int n, int kind, const Reduce &red, int root) {
 // streams concurrently.  The result lands in context 0, then goes to `root`
 // (root >= 0, as mpi4py forwards 0's result to root; the others are left
 // merged_away) or to every context (root = -1).
-int ensure_event(hipEvent_t *e) {
-  if (!*e) CX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+int ensure_event(const rmsf_ctx *c, hipEvent_t *e) {
+  if (!*e) {
+    CX_OK(on_device(c, "an exact-merge event"));
+    CX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
   return RMSF_OK;
 }
 
@@ -1195,7 +1222,7 @@ int pull_state(rmsf_ctx *d, rmsf_ctx *s, int64_t nc) {
   enable_peer(d->dev, s->dev);
   {
     DeviceScope ds(s->dev);
-    CX_OK(ensure_event(&s->ev_sent));
+    CX_OK(ensure_event(s, &s->ev_sent));
     CX_HIP(hipEventRecord(s->ev_sent, s->stream));
   }
   {
@@ -1205,7 +1232,7 @@ int pull_state(rmsf_ctx *d, rmsf_ctx *s, int64_t nc) {
     const size_t row = sizeof(double) * nc;
     CX_HIP(hipMemcpyPeerAsync(d->xb.p, d->dev, s->wel.parts0.p, s->dev, row, d->stream));
     CX_HIP(hipMemcpyPeerAsync(d->xb.d() + nc, d->dev, s->wel.parts1.p, s->dev, row, d->stream));
-    CX_OK(ensure_event(&d->ev_pulled));
+    CX_OK(ensure_event(d, &d->ev_pulled));
     CX_HIP(hipEventRecord(d->ev_pulled, d->stream));
   }
   DeviceScope ds(s->dev);

@@ -338,6 +338,7 @@ __global__ __launch_bounds__(kBlock) void k_accum_atoms(
 // Workspace = header (kSkHdr int64) + parts0[G*P][256*cpl] (+ parts1).
 constexpr int kSkHdr = 16;
 constexpr int64_t kSkMinSeg = 32;  // auto grid: ranges of >= this many frames
+constexpr int64_t kSkMaxSegsPerChunk = 64;  // auto grid: ranges per chunk at most (sk_plan)
 struct SkPlan {
   int64_t lanes, C, nf, T;
   int G, P, cpl, mode;
@@ -1262,7 +1263,7 @@ template <bool GATHER, bool MASSES, bool VEC4, int WPE = 1, bool PLANES = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_frame_stats(
     const float *__restrict__ xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
     const int32_t *__restrict__ sel, const double *__restrict__ masses, const double *__restrict__ ref,
-    StatsPlan pl, double *__restrict__ part, int64_t ps = 0, float *__restrict__ dense = nullptr) {
+    StatsPlan pl, double *__restrict__ part, int64_t ps = 0) {
   __shared__ __attribute__((aligned(16))) float tile[kStatsLds];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1329,7 +1330,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         }
       }
     };
-    auto lstore = [&](int64_t t0) {
+    auto lstore = [&]() {
       if (VEC4) {
 #pragma unroll
         for (int k = 0; k < kNPre; ++k) {
@@ -1346,19 +1347,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
           d[0] = pel[3 * k];
           d[1] = pel[3 * k + 1];
           d[2] = pel[3 * k + 2];
-          // compaction (rmsf_superpose_compact): every (frame, selected atom)
-          // is staged exactly once over the grid, so its gathered row goes
-          // out once too, to the dense [frame][n_sel][3] copy the later
-          // passes read instead of re-gathering (an exact copy: same bits)
-          if (GATHER && !PLANES && dense != nullptr) {
-            const int64_t a = t0 + j;
-            if (a < a_end && f0 + row <= last) {
-              float *o = dense + (f0 + row) * 3 * n_sel + 3 * a;
-              o[0] = pel[3 * k];
-              o[1] = pel[3 * k + 1];
-              o[2] = pel[3 * k + 2];
-            }
-          }
         }
       }
     };
@@ -1407,7 +1395,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     gload(a_beg);
     for (int64_t t0 = a_beg; t0 < a_end; t0 += kTA) {
       __syncthreads();
-      lstore(t0);
+      lstore();
       __syncthreads();
       if (t0 + kTA < a_end) gload(t0 + kTA);
       const f32x4 *my = reinterpret_cast<const f32x4 *>(tile + lane * kPitch + (PLANES && VEC4 ? 0 : w * 3 * kAPW));
@@ -1971,19 +1959,45 @@ __host__ __device__ inline uint64_t skey(uint64_t seed, uint64_t stream, uint64_
   return sm64(sm64(sm64(seed ^ (stream * 0xD1B54A32D192ED03ull)) + i) + j);
 }
 
-// k_gather_frames: compact batch of scattered frames (a run(frames=...) list):
-// dst[k][j] = the selected atom j of frame src + frames[k]*fstride, one float
-// per thread, grid = (coordinate blocks, frames).
+// k_gather_frames: compact batch of frames (a scattered run(frames=...) list,
+// or the dense copy of a sparse selection's rows, pipeline._Compactor):
+// dst[k][j] = the selected atom j of frame src + frames[k]*fstride.  One
+// selected atom per thread and kGatherFrames frames per block row, kGatherU
+// frames' loads in flight: each wave stores 64 contiguous 12-B rows per
+// frame (768 B), and the frame indices arrive by scalar loads.  (Round 5's
+// form -- one float per thread, one block row per frame -- launched 2.4M
+// blocks for 10k atoms x 20k frames.)
+constexpr int kGatherFrames = 16, kGatherU = 4;
 template <bool GATHER>
 __global__ __launch_bounds__(kBlock) void k_gather_frames(const float *__restrict__ src, int64_t fstride,
-                                                          const int64_t *__restrict__ frames, int64_t n_sel,
-                                                          const int32_t *__restrict__ sel, float *__restrict__ dst) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= 3 * n_sel) return;
-  const int64_t k = blockIdx.y;
-  const float *fr = src + frames[k] * fstride;
-  const int64_t a = i / 3, c = i - 3 * a;
-  dst[k * 3 * n_sel + i] = __builtin_nontemporal_load(fr + (GATHER ? 3 * (int64_t)sel[a] + c : i));
+                                                          const int64_t *__restrict__ frames, int64_t n_frames,
+                                                          int64_t n_sel, const int32_t *__restrict__ sel,
+                                                          float *__restrict__ dst) {
+  const int64_t a = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (a >= n_sel) return;
+  const int64_t k0 = (int64_t)blockIdx.y * kGatherFrames;
+  const int64_t k1 = min(n_frames, k0 + kGatherFrames);
+  const int64_t off = 3 * (GATHER ? (int64_t)sel[a] : a);
+  float *__restrict__ o = dst + 3 * a;
+  int64_t k = k0;
+  for (; k + kGatherU <= k1; k += kGatherU) {
+    float v[kGatherU][3];
+#pragma unroll
+    for (int u = 0; u < kGatherU; ++u) {
+      const float *p = src + frames[k + u] * fstride + off;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[u][c] = __builtin_nontemporal_load(p + c);
+    }
+#pragma unroll
+    for (int u = 0; u < kGatherU; ++u)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) o[(k + u) * 3 * n_sel + c] = v[u][c];
+  }
+  for (; k < k1; ++k) {
+    const float *p = src + frames[k] * fstride + off;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) o[k * 3 * n_sel + c] = __builtin_nontemporal_load(p + c);
+  }
 }
 
 // k_gather_planes: the same compact batch from frames stored as coordinate
@@ -2259,7 +2273,7 @@ namespace {
 // coordinate-plane stride of SoA frames (PLANES kernels)
 int superpose_impl(const char *who, const float *d_xyz, int64_t fstride, int64_t ps, int64_t n_frames, int64_t n_sel,
                    const int32_t *d_sel, const double *d_masses, const double *d_ref, const double *d_refinfo,
-                   double *d_xform, void *d_work, size_t work_bytes, hipStream_t s, float *d_dense = nullptr) {
+                   double *d_xform, void *d_work, size_t work_bytes, hipStream_t s) {
   if (n_frames == 0) return RMSF_OK;
   const bool planes = ps > 0;
   if (!d_xyz || !d_ref || !d_refinfo || !d_xform || !d_work || n_sel < 1 || n_frames < 0 ||
@@ -2276,7 +2290,7 @@ int superpose_impl(const char *who, const float *d_xyz, int64_t fstride, int64_t
   auto stats = [&](auto P) {
     constexpr bool PL = decltype(P)::value;
 #define ST_LAUNCH(G, M, V) \
-  hipLaunchKernelGGL((k_frame_stats<G, M, V, 1, PL>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, plan, part, ps, d_dense)
+  hipLaunchKernelGGL((k_frame_stats<G, M, V, 1, PL>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, plan, part, ps)
     if (g && m) ST_LAUNCH(true, true, false);
     else if (g) ST_LAUNCH(true, false, false);
     else if (m && vec4) ST_LAUNCH(false, true, true);
@@ -2315,15 +2329,6 @@ RMSF_EXPORT int rmsf_superpose(const float *d_xyz, int64_t fstride, int64_t n_fr
                                void *stream) {
   return superpose_impl("rmsf_superpose", d_xyz, fstride, 0, n_frames, n_sel, d_sel, d_masses, d_ref, d_refinfo,
                         d_xform, d_work, work_bytes, S(stream));
-}
-
-RMSF_EXPORT int rmsf_superpose_compact(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
-                                       const int32_t *d_sel, const double *d_masses, const double *d_ref,
-                                       const double *d_refinfo, double *d_xform, void *d_work, size_t work_bytes,
-                                       float *d_dense_out, void *stream) {
-  if (!d_sel || !d_dense_out) return fail(RMSF_EINVAL, "rmsf_superpose_compact: needs a selection and an output");
-  return superpose_impl("rmsf_superpose_compact", d_xyz, fstride, 0, n_frames, n_sel, d_sel, d_masses, d_ref,
-                        d_refinfo, d_xform, d_work, work_bytes, S(stream), d_dense_out);
 }
 
 RMSF_EXPORT int rmsf_superpose_planes(const float *d_xyz, int64_t fstride, int64_t pstride, int64_t n_frames,
@@ -2473,6 +2478,15 @@ SkPlan sk_plan(int64_t lanes, int cpl, int64_t nf, int n_groups, int mode, int p
     G = p.C * S;
   } else if (n_groups <= 0) {
     G = std::min<int64_t>(G, std::max<int64_t>(1, p.T / kSkMinSeg));
+    // Few chunks over many frames (a sparse selection: RMSF.py's 214 CA, the
+    // adk density 1 in 220): at most kSkMaxSegsPerChunk ranges per chunk.
+    // The fold walks a chunk's segments one after another (a memory round
+    // trip per kFoldBatch of them), so hundreds of 32-frame segments cost
+    // more than the parallelism they buy.
+    // 64 of 16 / 64 / 256 / unlimited measured at 455 of 100k atoms x 20k
+    // frames (RMSF.py's two sweeps 2.16 -> 0.75 ms; 10k atoms unchanged;
+    // profiles/r06_workloads/sparse_segs.txt)
+    G = std::min<int64_t>(G, std::max<int64_t>(1, p.C * kSkMaxSegsPerChunk));
   }
   G = std::max<int64_t>(1, std::min<int64_t>({G, p.T, (int64_t)INT32_MAX}));
   p.G = (int)G;
@@ -3130,13 +3144,13 @@ RMSF_EXPORT int rmsf_gather_frames(const float *d_src, int64_t fstride, const in
     return fail(RMSF_EINVAL, "rmsf_gather_frames: bad arguments");
   if (n_frames == 0) return RMSF_OK;
   if (n_frames > 65535) return fail(RMSF_EINVAL, "rmsf_gather_frames: at most 65535 frames per call");
-  const dim3 grid((unsigned)grid1(3 * n_sel), (unsigned)n_frames);
+  const dim3 grid((unsigned)grid1(n_sel), (unsigned)((n_frames + kGatherFrames - 1) / kGatherFrames));
   if (d_sel)
-    hipLaunchKernelGGL(k_gather_frames<true>, grid, dim3(kBlock), 0, S(stream), d_src, fstride, d_frames, n_sel, d_sel,
-                       d_dst);
+    hipLaunchKernelGGL(k_gather_frames<true>, grid, dim3(kBlock), 0, S(stream), d_src, fstride, d_frames, n_frames,
+                       n_sel, d_sel, d_dst);
   else
-    hipLaunchKernelGGL(k_gather_frames<false>, grid, dim3(kBlock), 0, S(stream), d_src, fstride, d_frames, n_sel,
-                       d_sel, d_dst);
+    hipLaunchKernelGGL(k_gather_frames<false>, grid, dim3(kBlock), 0, S(stream), d_src, fstride, d_frames, n_frames,
+                       n_sel, d_sel, d_dst);
   return after_launch("k_gather_frames");
 }
 

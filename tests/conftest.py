@@ -15,6 +15,13 @@ for p in (ROOT, PKG):
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# The product's default (exact=None) runs aligned runs of fewer than 256
+# frames through the exact path (pipeline.AUTO_EXACT_FRAMES).  The suite's
+# many small aligned cases were written for the frame-parallel kernels, so
+# they keep testing those (0 = never; inherited by spawned ranks);
+# tests/test_gpu_exact_aligned.py checks the default itself.
+os.environ["RMSF_AUTO_EXACT_FRAMES"] = "0"
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); run with -m gpu")

@@ -93,6 +93,29 @@ def test_bench_batched_launches_roofline_below_peak():
     assert 0 < rf["frac"] < 1.0
 
 
+@pytest.mark.parametrize("align", ["none", "frame0"])
+def test_one_process_form_at_one_gpu_matches_n1_line(align):
+    """Verdict r5 item 5: ``bench.py --gpus 1 --one-process`` runs the
+    one-process context form (main_single_process) on one real device -- a
+    one-rank ncclCommInitAll communicator and the RCCL merge path over it, no
+    peer setup -- and its line agrees with the N = 1 pipeline line: the same
+    RMSF checksum, a roofline below peak, no merge_timing (one device)."""
+    base = [sys.executable, "bench.py", "--gpus", "1", "--n-atoms", "20000", "--frames", "300", "--steps", "3",
+            "--warmup", "1", "--no-cpu-baseline", "--no-modes", "--align", align]
+    lines = {}
+    for form, extra in (("pipeline", []), ("contexts", ["--one-process"])):
+        r = subprocess.run(base + extra, cwd=ROOT, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines[form] = json.loads(r.stdout.strip().splitlines()[-1])
+    p, c = lines["pipeline"], lines["contexts"]
+    assert c["devices"] == [0] and c["rehearsal"] is False and "RCCL" in c["config"]["parallelism"]
+    assert "merge_timing" not in c and "merge_timing" not in p
+    for ln in (p, c):
+        assert ln["n_gpus"] == 1 and 0 < ln["roofline"]["frac"] < 1.0 and ln["sanity"]["ok"]
+    assert c["roofline"]["algorithmic_bytes_per_launch"] == p["roofline"]["algorithmic_bytes_per_launch"]
+    assert abs(c["rmsf_checksum"] - p["rmsf_checksum"]) <= 1e-11 * abs(p["rmsf_checksum"])
+
+
 def test_single_process_refuses_missing_devices():
     import torch
 

@@ -61,17 +61,23 @@ def test_literal_shape_exact_bit_for_bit(lit, lit_traj, nf, where):
 
 
 @pytest.mark.parametrize("nf", [2, 4, 10])
-def test_literal_shape_default_path_margin(lit, lit_traj, nf):
-    """The default (frame-parallel) aligned path at RMSF.py's shape: within
-    1e-6 A of the reference statements (P = 1 and P = 2 blocks agree with
-    each other in the vectors to the last bit or nearly)."""
+def test_literal_shape_default_is_exact(lit, lit_traj, nf, monkeypatch):
+    """The product default (exact=None) at RMSF.py's shape: an aligned run of
+    fewer than AUTO_EXACT_FRAMES frames takes the exact path -- the
+    reference statements' bits.  The frame-parallel path (exact=False) is
+    within one f32 rounding flip of an aligned coordinate: printed, and
+    bounded by ulp(x)/sqrt(N) (<= 1.53e-5 A / sqrt(N) below 256 A)."""
     from rmsf_amd import RMSF
+    monkeypatch.delenv("RMSF_AUTO_EXACT_FRAMES", raising=False)  # the product default
     t = torch.tensor(lit_traj[:nf], device="cuda")
     r = RMSF(t, select=lit["sel"], masses=lit["masses"], align="average").run().results
-    d = np.abs(r.rmsf - lit[f"rmsf_F{nf}_P1"]).max()
-    da = np.abs(r.average - lit[f"average_F{nf}_P1"]).max()
-    print(f"\nliteral shape, {nf} frames: default path max |dRMSF| {d:.3e} A, max |daverage| {da:.3e} A")
-    assert d < TOL and da < TOL
+    for k, got in (("rmsf", r.rmsf), ("mean", r.mean), ("m2", r.sumsquares), ("average", r.average)):
+        _same(got, lit[f"{k}_F{nf}_P1"], f"default, {k}, {nf} frames")
+    f = RMSF(t, select=lit["sel"], masses=lit["masses"], align="average", exact=False).run().results
+    d = np.abs(f.rmsf - lit[f"rmsf_F{nf}_P1"]).max()
+    da = np.abs(f.average - lit[f"average_F{nf}_P1"]).max()
+    print(f"\nliteral shape, {nf} frames: frame-parallel max |dRMSF| {d:.3e} A, max |daverage| {da:.3e} A")
+    assert d <= 3 * 1.53e-5 / np.sqrt(nf) and da <= 1.53e-5
 
 
 def _lit_worker(rank, size, init, q, nf):
@@ -252,7 +258,7 @@ def test_compacted_sparse_selection_same_bits(align, resident, monkeypatch):
     from rmsf_amd import pipeline as PL
     from rmsf_amd.synth import motion_table
     if not resident:
-        monkeypatch.setattr(PL._Compactor, "max_bytes", 12 * 300 * 17)  # 17 frames of the selection
+        monkeypatch.setattr(PL._Compactor, "max_bytes", 12 * 300 * 30)  # 30 frames: per 23-frame batch
     n, nf = 3000, 50
     traj = torch.tensor(SY.frames(41, n, 0, nf, motion_table(42, nf)), device="cuda")
     sel = np.arange(3, n, 10)
@@ -269,7 +275,7 @@ def test_compacted_sparse_selection_same_bits(align, resident, monkeypatch):
         if align == "average":
             out[compact]["average"] = res.average.cpu().numpy()
     # and the RMSF class picks compaction by itself at this density (1 in 10)
-    r = RMSF(traj, select=sel, masses=m, align=align).run().results
+    r = RMSF(traj, select=sel, masses=m, align=align, batch_frames=23).run().results
     _same(r.rmsf, out[True]["rmsf"], "RMSF class")
     for k, v in out[False].items():
         _same(out[True][k], v, k)

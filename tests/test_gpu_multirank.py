@@ -393,7 +393,9 @@ def _scatter_worker(rank, size, init, q, n_atoms, n_frames, align):
         shard = generate(eng, n_atoms, b0, b1 - b0, seed=15, motion=mt)
         src = DeviceSource(shard, offset=b0, n_traj=n_frames)
         fl = FrameList(n_frames)
-        every = run_pipeline(eng, src, fl, align=align, ref_owner=0)
+        # the frame-parallel all-reduce merge (exact=False: a few-frame aligned
+        # run would default to the exact path, whose merge is another form)
+        every = run_pipeline(eng, src, fl, align=align, ref_owner=0, exact=False)
         sc = run_pipeline(eng, src, fl, align=align, ref_owner=0, merge_root=0, merge_scatter=True)
         torch.cuda.synchronize()
         a0, a1 = sc.extras["atom_slice"]
