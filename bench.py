@@ -486,7 +486,6 @@ def sparse_selection_modes(eng, a, traj, n_atoms: int, n_total: int) -> dict:
             res[compact] = r.rmsf
             ks, s_ms, _ = t.totals("superpose")
             ka, a_ms, _ = t.totals("accumulate")
-            kc, c_ms, _ = t.totals("compact")
             step_ms = dt / a.mode_steps * 1e3
             sel_bytes = B_PER_ATOM_FRAME * n_sel * n_total * sweeps
             key = "compacted" if compact else "regathered"
@@ -494,8 +493,7 @@ def sparse_selection_modes(eng, a, traj, n_atoms: int, n_total: int) -> dict:
                         "selected_gbs": sel_bytes / (step_ms / 1e3) / 1e9,
                         "frac_of_single_read_roofline": sel_bytes / (step_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
                         "superpose_ms_per_step": s_ms / a.mode_steps, "superpose_launches": ks // a.mode_steps,
-                        "accumulate_ms_per_step": a_ms / a.mode_steps, "accumulate_launches": ka // a.mode_steps,
-                        "compact_ms_per_step": c_ms / a.mode_steps, "compact_launches": kc // a.mode_steps}
+                        "accumulate_ms_per_step": a_ms / a.mode_steps, "accumulate_launches": ka // a.mode_steps}
         row["speedup_compacted"] = row["regathered"]["ms_per_step"] / row["compacted"]["ms_per_step"]
         row["same_bits"] = bool(torch.equal(res[True], res[False]))
         if not row["same_bits"]:

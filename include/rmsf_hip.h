@@ -114,6 +114,24 @@ int rmsf_superpose(const float *d_xyz, int64_t frame_stride, int64_t n_frames,
                    const double *d_refinfo, double *d_xform, void *d_work,
                    size_t work_bytes, void *stream);
 
+/* rmsf_superpose over a gathered selection (d_sel != NULL, rows) that also
+ * COMPACTS it: every frame's selected rows, as the covariance pass stages
+ * them, go out to d_dense_out + f * dense_stride as [n_sel][3] (f32, an exact
+ * copy; dense_stride >= 3 n_sel floats, 0 = 3 n_sel), so the passes after it
+ * -- the accumulate of this sweep, and with the whole block kept resident
+ * every pass of RMSF.py's second sweep -- read n_sel dense rows (d_sel =
+ * NULL, frame_stride = dense_stride) instead of gathering them again from
+ * the full frames.  Same records, same bits as rmsf_superpose.  A gathered
+ * row read costs every 128-B line holding a selected atom -- at CA-like
+ * densities (1 in 10) nearly all of the frame -- so each avoided gather saves
+ * up to ~10x the selected bytes ("Sparse selections").   */
+int rmsf_superpose_compact(const float *d_xyz, int64_t frame_stride,
+                           int64_t n_frames, int64_t n_sel, const int32_t *d_sel,
+                           const double *d_masses, const double *d_ref,
+                           const double *d_refinfo, double *d_xform,
+                           void *d_work, size_t work_bytes, float *d_dense_out,
+                           int64_t dense_stride, void *stream);
+
 /* The same for frames stored as coordinate planes (SoA): atom a's x, y and
  * z of frame f at d_xyz + f*frame_stride + a (or d_sel[a]) + {0, 1, 2} *
  * plane_stride floats (frame_stride >= 3*plane_stride).  Same workspace,

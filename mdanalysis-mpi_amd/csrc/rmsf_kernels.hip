@@ -1263,7 +1263,8 @@ template <bool GATHER, bool MASSES, bool VEC4, int WPE = 1, bool PLANES = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_frame_stats(
     const float *__restrict__ xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
     const int32_t *__restrict__ sel, const double *__restrict__ masses, const double *__restrict__ ref,
-    StatsPlan pl, double *__restrict__ part, int64_t ps = 0) {
+    StatsPlan pl, double *__restrict__ part, int64_t ps = 0, float *__restrict__ dense = nullptr,
+    int64_t dpitch = 0) {
   __shared__ __attribute__((aligned(16))) float tile[kStatsLds];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1350,6 +1351,37 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         }
       }
     };
+    // Compaction (rmsf_superpose_compact): every (frame, selected atom) is
+    // staged exactly once over the grid, so the staged tile goes out once
+    // too, to the dense copy the later passes read instead of re-gathering
+    // (an exact copy: same bits).  From LDS, after the next tile's loads
+    // are issued: a frame's 32 atoms are 384 contiguous bytes of the copy,
+    // written as 24 float4.  Writing the copy here beats a stand-alone gather
+    // before a dense covariance pass: C3 at 10k of 100k atoms 1.23x against
+    // 1.12-1.15x, RMSF.py's two sweeps 2.15x against 1.94-1.98x (ratios to
+    // re-gathering on the same box, profiles/r06_workloads/).
+    auto dense_out = [&](int64_t t0) {
+      const int64_t na = min((int64_t)kTA, a_end - t0);  // atoms in this tile (uniform)
+      const bool vec = na == kTA && (dpitch & 3) == 0 && (reinterpret_cast<uintptr_t>(dense) & 15) == 0;
+      if (vec) {
+#pragma unroll
+        for (int k = 0; k < kNPre; ++k) {
+          const int idx = threadIdx.x + k * kBlock;
+          const int row = idx / kRow4, col = idx % kRow4;
+          if (f0 + row <= last) {
+            const f32x4 v = *reinterpret_cast<const f32x4 *>(tile + row * kPitch + 4 * col);
+            __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(dense + (f0 + row) * dpitch + 3 * t0) + col);
+          }
+        }
+      } else {
+        const int nfl = 3 * (int)na;
+        for (int idx = threadIdx.x; idx < kTF * 3 * kTA; idx += kBlock) {
+          const int row = idx / (3 * kTA), e = idx - row * (3 * kTA);
+          if (e < nfl && f0 + row <= last)
+            __builtin_nontemporal_store(tile[row * kPitch + e], dense + (f0 + row) * dpitch + 3 * t0 + e);
+        }
+      }
+    };
     // one 4-atom group of this wave's slab (atoms a4..a4+3, a wave-uniform index)
     auto group = [&](const f32x4 *my, int gi, int64_t a4, int n_at) {
       float c[12];
@@ -1398,6 +1430,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       lstore();
       __syncthreads();
       if (t0 + kTA < a_end) gload(t0 + kTA);
+      if (GATHER && !PLANES && dense != nullptr) dense_out(t0);
       const f32x4 *my = reinterpret_cast<const f32x4 *>(tile + lane * kPitch + (PLANES && VEC4 ? 0 : w * 3 * kAPW));
       const int64_t ab = t0 + w * kAPW;  // first atom of this wave's slab (uniform)
       if (t0 + kTA <= a_end) {           // a whole tile: no per-atom checks
@@ -1961,43 +1994,22 @@ __host__ __device__ inline uint64_t skey(uint64_t seed, uint64_t stream, uint64_
 
 // k_gather_frames: compact batch of frames (a scattered run(frames=...) list,
 // or the dense copy of a sparse selection's rows, pipeline._Compactor):
-// dst[k][j] = the selected atom j of frame src + frames[k]*fstride.  One
-// selected atom per thread and kGatherFrames frames per block row, kGatherU
-// frames' loads in flight: each wave stores 64 contiguous 12-B rows per
-// frame (768 B), and the frame indices arrive by scalar loads.  (Round 5's
-// form -- one float per thread, one block row per frame -- launched 2.4M
-// blocks for 10k atoms x 20k frames.)
-constexpr int kGatherFrames = 16, kGatherU = 4;
+// dst[k][j] = the selected atom j of frame src + frames[k]*fstride, one float
+// per thread, grid = (coordinate blocks, frames).  Round 6 A/B at 10k, 455 and
+// 50k of 100k atoms x 20k frames (profiles/r06_workloads/ab_gather.txt):
+// this form is the fastest at CA-like densities -- one atom per thread with
+// three strided stores is 3-12 % slower there (13 % faster at 1 in 2, where
+// compaction does not run), 16 frames per block row 12 % slower.
 template <bool GATHER>
 __global__ __launch_bounds__(kBlock) void k_gather_frames(const float *__restrict__ src, int64_t fstride,
-                                                          const int64_t *__restrict__ frames, int64_t n_frames,
-                                                          int64_t n_sel, const int32_t *__restrict__ sel,
-                                                          float *__restrict__ dst) {
-  const int64_t a = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (a >= n_sel) return;
-  const int64_t k0 = (int64_t)blockIdx.y * kGatherFrames;
-  const int64_t k1 = min(n_frames, k0 + kGatherFrames);
-  const int64_t off = 3 * (GATHER ? (int64_t)sel[a] : a);
-  float *__restrict__ o = dst + 3 * a;
-  int64_t k = k0;
-  for (; k + kGatherU <= k1; k += kGatherU) {
-    float v[kGatherU][3];
-#pragma unroll
-    for (int u = 0; u < kGatherU; ++u) {
-      const float *p = src + frames[k + u] * fstride + off;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) v[u][c] = __builtin_nontemporal_load(p + c);
-    }
-#pragma unroll
-    for (int u = 0; u < kGatherU; ++u)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) o[(k + u) * 3 * n_sel + c] = v[u][c];
-  }
-  for (; k < k1; ++k) {
-    const float *p = src + frames[k] * fstride + off;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) o[k * 3 * n_sel + c] = __builtin_nontemporal_load(p + c);
-  }
+                                                          const int64_t *__restrict__ frames, int64_t n_sel,
+                                                          const int32_t *__restrict__ sel, float *__restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= 3 * n_sel) return;
+  const int64_t k = blockIdx.y;
+  const float *fr = src + frames[k] * fstride;
+  const int64_t a = i / 3, c = i - 3 * a;
+  dst[k * 3 * n_sel + i] = __builtin_nontemporal_load(fr + (GATHER ? 3 * (int64_t)sel[a] + c : i));
 }
 
 // k_gather_planes: the same compact batch from frames stored as coordinate
@@ -2273,7 +2285,8 @@ namespace {
 // coordinate-plane stride of SoA frames (PLANES kernels)
 int superpose_impl(const char *who, const float *d_xyz, int64_t fstride, int64_t ps, int64_t n_frames, int64_t n_sel,
                    const int32_t *d_sel, const double *d_masses, const double *d_ref, const double *d_refinfo,
-                   double *d_xform, void *d_work, size_t work_bytes, hipStream_t s) {
+                   double *d_xform, void *d_work, size_t work_bytes, hipStream_t s, float *d_dense = nullptr,
+                   int64_t dense_pitch = 0) {
   if (n_frames == 0) return RMSF_OK;
   const bool planes = ps > 0;
   if (!d_xyz || !d_ref || !d_refinfo || !d_xform || !d_work || n_sel < 1 || n_frames < 0 ||
@@ -2290,7 +2303,7 @@ int superpose_impl(const char *who, const float *d_xyz, int64_t fstride, int64_t
   auto stats = [&](auto P) {
     constexpr bool PL = decltype(P)::value;
 #define ST_LAUNCH(G, M, V) \
-  hipLaunchKernelGGL((k_frame_stats<G, M, V, 1, PL>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, plan, part, ps)
+  hipLaunchKernelGGL((k_frame_stats<G, M, V, 1, PL>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, plan, part, ps, d_dense, dense_pitch)
     if (g && m) ST_LAUNCH(true, true, false);
     else if (g) ST_LAUNCH(true, false, false);
     else if (m && vec4) ST_LAUNCH(false, true, true);
@@ -2329,6 +2342,17 @@ RMSF_EXPORT int rmsf_superpose(const float *d_xyz, int64_t fstride, int64_t n_fr
                                void *stream) {
   return superpose_impl("rmsf_superpose", d_xyz, fstride, 0, n_frames, n_sel, d_sel, d_masses, d_ref, d_refinfo,
                         d_xform, d_work, work_bytes, S(stream));
+}
+
+RMSF_EXPORT int rmsf_superpose_compact(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
+                                       const int32_t *d_sel, const double *d_masses, const double *d_ref,
+                                       const double *d_refinfo, double *d_xform, void *d_work, size_t work_bytes,
+                                       float *d_dense_out, int64_t dense_stride, void *stream) {
+  if (!d_sel || !d_dense_out) return fail(RMSF_EINVAL, "rmsf_superpose_compact: needs a selection and an output");
+  if (dense_stride == 0) dense_stride = 3 * n_sel;
+  if (dense_stride < 3 * n_sel) return fail(RMSF_EINVAL, "rmsf_superpose_compact: dense_stride < 3 n_sel");
+  return superpose_impl("rmsf_superpose_compact", d_xyz, fstride, 0, n_frames, n_sel, d_sel, d_masses, d_ref,
+                        d_refinfo, d_xform, d_work, work_bytes, S(stream), d_dense_out, dense_stride);
 }
 
 RMSF_EXPORT int rmsf_superpose_planes(const float *d_xyz, int64_t fstride, int64_t pstride, int64_t n_frames,
@@ -3144,13 +3168,13 @@ RMSF_EXPORT int rmsf_gather_frames(const float *d_src, int64_t fstride, const in
     return fail(RMSF_EINVAL, "rmsf_gather_frames: bad arguments");
   if (n_frames == 0) return RMSF_OK;
   if (n_frames > 65535) return fail(RMSF_EINVAL, "rmsf_gather_frames: at most 65535 frames per call");
-  const dim3 grid((unsigned)grid1(n_sel), (unsigned)((n_frames + kGatherFrames - 1) / kGatherFrames));
+  const dim3 grid((unsigned)grid1(3 * n_sel), (unsigned)n_frames);
   if (d_sel)
-    hipLaunchKernelGGL(k_gather_frames<true>, grid, dim3(kBlock), 0, S(stream), d_src, fstride, d_frames, n_frames,
-                       n_sel, d_sel, d_dst);
+    hipLaunchKernelGGL(k_gather_frames<true>, grid, dim3(kBlock), 0, S(stream), d_src, fstride, d_frames, n_sel, d_sel,
+                       d_dst);
   else
-    hipLaunchKernelGGL(k_gather_frames<false>, grid, dim3(kBlock), 0, S(stream), d_src, fstride, d_frames, n_frames,
-                       n_sel, d_sel, d_dst);
+    hipLaunchKernelGGL(k_gather_frames<false>, grid, dim3(kBlock), 0, S(stream), d_src, fstride, d_frames, n_sel,
+                       d_sel, d_dst);
   return after_launch("k_gather_frames");
 }
 

@@ -59,6 +59,7 @@ SIGNATURES = {
     "rmsf_superpose_workspace_bytes": (c_size_t, [c_int64, c_int64]),
     "rmsf_superpose": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, P, P, P, c_size_t, P]),
     "rmsf_superpose_planes": (c_int, [P, c_int64, c_int64, c_int64, c_int64, P, P, P, P, P, P, c_size_t, P]),
+    "rmsf_superpose_compact": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, P, P, P, c_size_t, P, c_int64, P]),
     "rmsf_accumulate_splits": (c_int, [c_int64, c_int64, c_int]),
     "rmsf_accumulate": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, c_int, c_int, P, P, P]),
     "rmsf_split_count": (c_int64, [c_int64, c_int, c_int]),

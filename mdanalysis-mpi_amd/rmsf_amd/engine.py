@@ -87,9 +87,18 @@ class Engine:
         return int(self.lib.rmsf_superpose_workspace_bytes(n_sel, n_frames))
 
     def superpose(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, sel, masses, ref, refinfo,
-                  xform: torch.Tensor, work: torch.Tensor, pstride: int = 0) -> None:
+                  xform: torch.Tensor, work: torch.Tensor, pstride: int = 0, dense_out: int | None = None,
+                  dense_stride: int = 0) -> None:
         """RMSF.py:94-97,127-131 + get_rotation_matrix (RMSF.py:43-51): per-frame COM + QCP.
-        ``pstride`` > 0: frames stored as coordinate planes (rmsf_superpose_planes)."""
+        ``pstride`` > 0: frames stored as coordinate planes (rmsf_superpose_planes).
+        ``dense_out`` (a gathered ``sel``): also write the selected rows to
+        that device address, frame f's [n_sel, 3] at f * ``dense_stride``
+        floats (0 = 3 n_sel; rmsf_superpose_compact)."""
+        if dense_out is not None:
+            call("rmsf_superpose_compact", xyz_ptr, fstride, n_frames, n_sel, _ptr(sel), _ptr(masses),
+                 ref.data_ptr(), refinfo.data_ptr(), xform.data_ptr(), work.data_ptr(),
+                 work.numel() * work.element_size(), dense_out, dense_stride, self.stream)
+            return
         if pstride:
             call("rmsf_superpose_planes", xyz_ptr, fstride, pstride, n_frames, n_sel, _ptr(sel), _ptr(masses),
                  ref.data_ptr(), refinfo.data_ptr(), xform.data_ptr(), work.data_ptr(),

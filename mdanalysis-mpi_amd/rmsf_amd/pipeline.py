@@ -191,41 +191,38 @@ class Superposer:
         nbytes = eng.workspace_bytes(n_sel, max_batch)
         self.work = eng.empty(max(1, (nbytes + 7) // 8))
 
-    def run(self, b: Batch, ref: torch.Tensor, refinfo: torch.Tensor) -> torch.Tensor:
+    def run(self, b: Batch, ref: torch.Tensor, refinfo: torch.Tensor, dense_out: int | None = None) -> torch.Tensor:
         xf = self.xform[: b.n_frames]
         need = self.eng.workspace_bytes(self.n_sel, b.n_frames)
         if need > self.work.numel() * 8:  # stats_plan's bytes are not monotone in the batch size
             self.work = self.eng.empty((need + 7) // 8)
         with _span(self.timer, "superpose", b.n_frames * self.n_sel):
             self.eng.superpose(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, self.masses, ref, refinfo, xf,
-                               self.work, pstride=b.pstride)
+                               self.work, pstride=b.pstride, dense_out=dense_out)
         return xf
 
 
 # Compaction of gathered selections on the aligned path (round 6): a gathered
 # row read costs every 128-B line holding a selected atom, so below this
-# density the selected rows are copied out dense once (rmsf_gather_frames: an
-# exact copy) and every pass reads them dense ("Sparse
-# selections")
+# density the first pass over each frame writes its selected rows out once
+# (an exact copy) and the later passes read them dense (DESIGN section 4,
+# "Sparse selections")
 COMPACT_MAX_DENSITY = 0.5
 
 
 class _Compactor:
-    """The dense [frames, n_sel, 3] copy of a gathered selection's rows
-    (rmsf_gather_frames), read by the superposition and accumulate passes in
-    place of the full frames.  ``resident``: the whole block fits (at most
-    half the free HBM), so a later sweep (RMSF.py:124) reads it again with no
-    gather at all; otherwise the copy is per batch.  A dense batch shorter
-    than the pipeline's would change the batching (and the fold's bits), so
-    then it is not used (``usable``).  Measured at 10k of 100k atoms x 20k
-    frames: the gather alone 4.41 ms, against 5.56 ms for writing the copy
-    from the covariance pass's LDS tiles (not adopted,
-    profiles/r06_workloads/ab_compact.txt)."""
+    """The dense [frames, n_sel, 3] copy of a gathered selection's rows,
+    written by the covariance pass as it stages them
+    (rmsf_superpose_compact) and read by the accumulate and, ``resident``
+    (the whole block fits in half the free HBM), by every pass of a later
+    sweep (RMSF.py:124) with no gather at all; otherwise per batch.  A dense
+    batch shorter than the pipeline's would change the batching (and the
+    fold's bits), so then it is not used (``usable``)."""
 
     max_bytes: int | None = None  # None: half the free HBM (tests set a small cap for the per-batch form)
 
-    def __init__(self, eng: Engine, n_sel: int, n_local: int, max_batch: int, timer=None):
-        self.eng, self.n_sel, self.timer = eng, n_sel, timer
+    def __init__(self, eng: Engine, n_sel: int, n_local: int, max_batch: int):
+        self.n_sel = n_sel
         row = 12 * n_sel
         budget = self.max_bytes
         if budget is None:
@@ -234,25 +231,16 @@ class _Compactor:
         self.resident = n_local <= cap
         self.frames = n_local if self.resident else max(1, min(max_batch, cap))
         self.usable = self.resident or self.frames >= max_batch
-        self.buf = self.rows = None
+        self.buf = None
         if self.usable:
             self.buf = torch.empty((max(1, self.frames), n_sel, 3), dtype=torch.float32, device=eng.device)
-            self.rows = torch.arange(min(self.frames, max_batch, 65535), dtype=torch.int64, device=eng.device)
         self.filled = False
 
-    def dense(self, k: int, n: int) -> Batch:
-        return Batch(self.buf.data_ptr() + 12 * self.n_sel * k, 3 * self.n_sel, n, None)
+    def ptr(self, k: int) -> int:
+        return self.buf.data_ptr() + 12 * self.n_sel * k
 
-    def gather(self, b: Batch, k: int) -> Batch:
-        """Copy batch ``b``'s selected rows (frames at b.fstride) into rows
-        k.. of the dense copy; returns the dense batch."""
-        step = self.rows.numel()
-        with _span(self.timer, "compact", b.n_frames * self.n_sel):
-            for i in range(0, b.n_frames, step):
-                n = min(step, b.n_frames - i)
-                self.eng.gather_frames(b.ptr + 4 * b.fstride * i, b.fstride, self.rows, n, self.n_sel, b.sel,
-                                       self.buf[k + i:k + i + n])
-        return self.dense(k, b.n_frames)
+    def dense(self, k: int, n: int) -> Batch:
+        return Batch(self.ptr(k), 3 * self.n_sel, n, None)
 
     def resident_batches(self, n_local: int, max_batch: int):
         for k in range(0, n_local, max_batch):
@@ -477,9 +465,9 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     ``exact=None`` (default): exact for an aligned run of fewer than
     AUTO_EXACT_FRAMES frames (auto_exact), the frame-parallel path otherwise.
     ``compact`` (aligned runs over a gathered selection of HBM-resident
-    rows): the selected rows are copied out dense once and every pass reads
-    them (_Compactor); None = below COMPACT_MAX_DENSITY selected atoms per
-    frame atom.  Same bits either way."""
+    rows): the first pass writes the selected rows out dense and the later
+    passes read them (_Compactor); None = below COMPACT_MAX_DENSITY selected
+    atoms per frame atom.  Same bits either way."""
     if align not in ALIGN_MODES:
         raise ValueError(f"align must be one of {ALIGN_MODES}, got {align!r}")
     if exact is None:
@@ -533,7 +521,7 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                 and source.sel_dev is not None and not _scattered_block(frames, b0, b1, max_batch))
     if compact is None:
         compact = gathered and n_sel <= COMPACT_MAX_DENSITY * source.n_atoms
-    cmp = _Compactor(eng, n_sel, n_local, max_batch, timer) if (compact and gathered and n_local) else None
+    cmp = _Compactor(eng, n_sel, n_local, max_batch) if (compact and gathered and n_local) else None
     if cmp is not None and not cmp.usable:
         cmp = None
     sup = Superposer(eng, n_sel, max_batch, m_dev, timer) if aligned else None
@@ -553,8 +541,11 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
             xf, src_b = None, b
             if aligned:
                 if cmp is not None and b.sel is not None:
-                    b = cmp.gather(b, done if cmp.resident else 0)   # the passes read the dense rows
-                xf = sup.run(b, ref, info)
+                    k = done if cmp.resident else 0
+                    xf = sup.run(b, ref, info, dense_out=cmp.ptr(k))
+                    b = cmp.dense(k, b.n_frames)   # the accumulate reads the dense rows
+                else:
+                    xf = sup.run(b, ref, info)
                 if rmsd is not None:
                     rmsd[done:done + b.n_frames].copy_(xf[:, 12])
                 if xf_out is not None:

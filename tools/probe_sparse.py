@@ -41,12 +41,10 @@ for stride, align in ((10, "frame0"), (10, "average"), (220, "average"), (220, "
         res[compact] = r.rmsf
         _, s_ms, _ = t.totals("superpose")
         _, a_ms, _ = t.totals("accumulate")
-        _, c_ms, _ = t.totals("compact")
         sweeps = 2 if align == "average" else 1
         gbs = 12 * len(sel) * nf * sweeps / (dt / 1e3) / 1e9
         print(f"1 in {stride:3d} ({len(sel)} of {n_atoms}) {align:7s} compact={compact!s:5s}: {dt:7.3f} ms/step "
-              f"(compact {c_ms / steps:6.3f}, superpose {s_ms / steps:6.3f}, accumulate {a_ms / steps:6.3f}; "
-              f"selected {gbs:6.0f} GB/s = "
+              f"(superpose {s_ms / steps:6.3f}, accumulate {a_ms / steps:6.3f}; selected {gbs:6.0f} GB/s = "
               f"{gbs / 8000:.3f} of 8 TB/s)", flush=True)
     print(f"   same bits: {bool(torch.equal(res[True], res[False]))}", flush=True)
     del src
