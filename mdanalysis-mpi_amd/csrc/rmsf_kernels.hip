@@ -25,6 +25,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <unordered_map>
 #include <vector>
 
@@ -1259,12 +1260,13 @@ __host__ __device__ inline int64_t st_lo(const StatsPlan &p, int64_t b) { return
 // the same (atom, xyz) tile rows; the VEC4 path stages each tile row as
 // [x(32) | y(32) | z(32)] (three 128-B plane segments per frame, the same
 // 24 float4 per row) and its 4-atom groups read one float4 of each plane.
-template <bool GATHER, bool MASSES, bool VEC4, int WPE = 1, bool PLANES = false>
+template <bool GATHER, bool MASSES, bool VEC4, int WPE = 1, bool PLANES = false, int DENSE = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void k_frame_stats(
     const float *__restrict__ xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
     const int32_t *__restrict__ sel, const double *__restrict__ masses, const double *__restrict__ ref,
     StatsPlan pl, double *__restrict__ part, int64_t ps = 0, float *__restrict__ dense = nullptr,
     int64_t dpitch = 0) {
+  static_assert(DENSE == 0 || (GATHER && !PLANES && !VEC4), "the dense copy is of gathered (frame, atom, xyz) rows");
   __shared__ __attribute__((aligned(16))) float tile[kStatsLds];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1289,6 +1291,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
 
     f32x4 pre[VEC4 ? kNPre : 1];
     float pel[VEC4 ? 1 : 3 * kNEl];
+    // element path: this thread's atom of the tile at t0 (clamped to the
+    // segment's last atom), as its index in the frame rows.  Loaded one tile
+    // ahead and scaled only where gload uses it: scaling it right after the
+    // load would make the wave wait for that load -- and so for every store
+    // issued before it -- at the end of each tile.
+    using EAtom = std::conditional_t<GATHER, int32_t, int64_t>;
+    auto elem_atom = [&](int64_t t0) -> EAtom {
+      const int64_t a = min(t0 + (int64_t)(threadIdx.x % kTA), a_end - 1);
+      if constexpr (GATHER) return sel[a];
+      else return a;
+    };
+    EAtom eatom = VEC4 ? 0 : elem_atom(a_beg);
     auto gload = [&](int64_t t0) {
       if (VEC4) {
 #pragma unroll
@@ -1314,21 +1328,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
           }
         }
       } else {
+        // kBlock % kTA == 0: a thread stages the same atom j of every row it
+        // loads, so one offset serves its kNEl rows.  The offset (the
+        // selection index) was loaded one tile ahead (eatom), and no load is
+        // conditional: past the segment's last atom the thread re-reads that
+        // atom, whose tile slots neither the sums nor the dense copy read.
+        // (The per-row `if (a < a_end)` form compiled to an index load, a
+        // vmcnt(0), the coordinate load and another vmcnt(0) per row: 16
+        // serial round trips per tile.)
+        // (the empty asm pins the first use of the loaded index here, so its
+        // widening is not hoisted to the load)
+        if constexpr (GATHER) asm volatile("" : "+v"(eatom));
+        const int64_t off = (PLANES ? 1 : 3) * (int64_t)eatom;
 #pragma unroll
         for (int k = 0; k < kNEl; ++k) {
-          const int idx = threadIdx.x + k * kBlock;
-          const int row = idx / kTA, j = idx % kTA;
-          const int64_t a = t0 + j;
-          const float *src = xyz + min(f0 + row, last) * fstride;
-          if (a < a_end) {
-            const int64_t off = (PLANES ? 1 : 3) * (GATHER ? (int64_t)sel[a] : a);
-            pel[3 * k] = __builtin_nontemporal_load(src + off);
-            pel[3 * k + 1] = __builtin_nontemporal_load(src + off + cs);
-            pel[3 * k + 2] = __builtin_nontemporal_load(src + off + 2 * cs);
-          } else {
-            pel[3 * k] = pel[3 * k + 1] = pel[3 * k + 2] = 0.f;
-          }
+          const int row = (threadIdx.x + k * kBlock) / kTA;
+          const float *src = xyz + min(f0 + row, last) * fstride + off;
+          pel[3 * k] = __builtin_nontemporal_load(src);
+          pel[3 * k + 1] = __builtin_nontemporal_load(src + cs);
+          pel[3 * k + 2] = __builtin_nontemporal_load(src + 2 * cs);
         }
+        eatom = elem_atom(t0 + kTA);
       }
     };
     auto lstore = [&]() {
@@ -1351,35 +1371,63 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         }
       }
     };
-    // Compaction (rmsf_superpose_compact): every (frame, selected atom) is
-    // staged exactly once over the grid, so the staged tile goes out once
-    // too, to the dense copy the later passes read instead of re-gathering
-    // (an exact copy: same bits).  From LDS, after the next tile's loads
-    // are issued: a frame's 32 atoms are 384 contiguous bytes of the copy,
-    // written as 24 float4.  Writing the copy here beats a stand-alone gather
-    // before a dense covariance pass: C3 at 10k of 100k atoms 1.23x against
-    // 1.12-1.15x, RMSF.py's two sweeps 2.15x against 1.94-1.98x (ratios to
-    // re-gathering on the same box, profiles/r06_workloads/).
-    auto dense_out = [&](int64_t t0) {
-      const int64_t na = min((int64_t)kTA, a_end - t0);  // atoms in this tile (uniform)
-      const bool vec = na == kTA && (dpitch & 3) == 0 && (reinterpret_cast<uintptr_t>(dense) & 15) == 0;
-      if (vec) {
+    // Compaction (rmsf_superpose_compact, DENSE): every (frame, selected
+    // atom) is staged exactly once over the grid, so the staged tile goes
+    // out once too, to the dense copy the later passes read instead of
+    // re-gathering (an exact copy: same bits).  From LDS, after the next
+    // tile's loads are issued: a frame's 32 atoms are 384 contiguous bytes of
+    // the copy.  Writing the copy here beats a stand-alone gather before a
+    // dense covariance pass (ratios to re-gathering on one box,
+    // profiles/r06_workloads/).
+    // dense_whole: a whole tile with a successor, a FIXED number of stores
+    // per thread (DENSE 2: 6 float4; DENSE 1, rows not 16-B aligned: 24
+    // floats; rows past the trajectory rewrite its last row with the same
+    // values, as gload staged them from it).  vmcnt counts loads and stores
+    // in issue order, so with a fixed count after the next tile's loads the
+    // wait for those loads leaves the stores in flight: vmcnt(6), not
+    // vmcnt(0) (SQ_WAIT_ANY 2.2e8 against 1.3e9 cycles re-gathered).  The
+    // copy still costs +1.4-1.8 ms at 10k of 100k atoms x 20k frames, for
+    // 2.43 GB as 3.8e7 64-B writes: instruction-issue waits +1.6e9 cycles
+    // and L1 pending stalls +46 %, i.e. the writes share the vector memory
+    // path with the gather's per-line requests
+    // (profiles/r06_workloads/pmc_dense_store.txt).
+    auto dense_whole = [&](int64_t t0) {
+      if constexpr (DENSE == 2) {
+        f32x4 v[kNPre];
 #pragma unroll
         for (int k = 0; k < kNPre; ++k) {
           const int idx = threadIdx.x + k * kBlock;
-          const int row = idx / kRow4, col = idx % kRow4;
-          if (f0 + row <= last) {
-            const f32x4 v = *reinterpret_cast<const f32x4 *>(tile + row * kPitch + 4 * col);
-            __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(dense + (f0 + row) * dpitch + 3 * t0) + col);
-          }
+          v[k] = *reinterpret_cast<const f32x4 *>(tile + (idx / kRow4) * kPitch + 4 * (idx % kRow4));
+        }
+#pragma unroll
+        for (int k = 0; k < kNPre; ++k) {
+          const int idx = threadIdx.x + k * kBlock;
+          const int64_t fr = min(f0 + idx / kRow4, last);
+          __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4 *>(dense + fr * dpitch + 3 * t0) + idx % kRow4);
         }
       } else {
-        const int nfl = 3 * (int)na;
-        for (int idx = threadIdx.x; idx < kTF * 3 * kTA; idx += kBlock) {
-          const int row = idx / (3 * kTA), e = idx - row * (3 * kTA);
-          if (e < nfl && f0 + row <= last)
-            __builtin_nontemporal_store(tile[row * kPitch + e], dense + (f0 + row) * dpitch + 3 * t0 + e);
+        constexpr int kN = kTF * 3 * kTA / kBlock;
+        float v[kN];
+#pragma unroll
+        for (int k = 0; k < kN; ++k) {
+          const int idx = threadIdx.x + k * kBlock;
+          v[k] = tile[(idx / (3 * kTA)) * kPitch + idx % (3 * kTA)];
         }
+#pragma unroll
+        for (int k = 0; k < kN; ++k) {
+          const int idx = threadIdx.x + k * kBlock;
+          const int64_t fr = min(f0 + idx / (3 * kTA), last);
+          __builtin_nontemporal_store(v[k], dense + fr * dpitch + 3 * t0 + idx % (3 * kTA));
+        }
+      }
+    };
+    // the segment's last tile, whole or not
+    auto dense_last = [&](int64_t t0) {
+      const int nfl = 3 * (int)min((int64_t)kTA, a_end - t0);
+      for (int idx = threadIdx.x; idx < kTF * 3 * kTA; idx += kBlock) {
+        const int row = idx / (3 * kTA), e = idx - row * (3 * kTA);
+        if (e < nfl && f0 + row <= last)
+          __builtin_nontemporal_store(tile[row * kPitch + e], dense + (f0 + row) * dpitch + 3 * t0 + e);
       }
     };
     // one 4-atom group of this wave's slab (atoms a4..a4+3, a wave-uniform index)
@@ -1424,25 +1472,45 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
       }
     };
 
-    gload(a_beg);
-    for (int64_t t0 = a_beg; t0 < a_end; t0 += kTA) {
+    const f32x4 *my = reinterpret_cast<const f32x4 *>(tile + lane * kPitch + (PLANES && VEC4 ? 0 : w * 3 * kAPW));
+    // The segment's last tile is peeled, so the next tile's loads in the
+    // loop are unconditional.  (Behind an `if (t0 + kTA < a_end)` the
+    // element path's loaded values met the loop-carried ones in a phi, and
+    // the copies resolving it waited for the loads right after issuing
+    // them: no load was in flight across the tile's sums.)  With DENSE the
+    // first tile is peeled too, so both edges into the loop carry the same
+    // loads-then-stores sequence and the wait at its top can count them.
+    auto step = [&](int64_t t0) {  // a whole tile with a successor
       __syncthreads();
       lstore();
       __syncthreads();
-      if (t0 + kTA < a_end) gload(t0 + kTA);
-      if (GATHER && !PLANES && dense != nullptr) dense_out(t0);
-      const f32x4 *my = reinterpret_cast<const f32x4 *>(tile + lane * kPitch + (PLANES && VEC4 ? 0 : w * 3 * kAPW));
+      gload(t0 + kTA);
+      if constexpr (DENSE != 0) dense_whole(t0);
       const int64_t ab = t0 + w * kAPW;  // first atom of this wave's slab (uniform)
-      if (t0 + kTA <= a_end) {           // a whole tile: no per-atom checks
 #pragma unroll 1
-        for (int gi = 0; gi < kAPW / 4; ++gi) group(my, gi, ab + 4 * gi, 4);
-      } else {
+      for (int gi = 0; gi < kAPW / 4; ++gi) group(my, gi, ab + 4 * gi, 4);
+    };
+    gload(a_beg);
+    int64_t t0 = a_beg;
+    if constexpr (DENSE != 0) {
+      if (t0 + kTA < a_end) {  // the loop is entered from the peeled tile only
+        step(t0);
+        for (t0 += kTA; t0 + kTA < a_end; t0 += kTA) step(t0);
+      }
+    } else {
+      for (; t0 + kTA < a_end; t0 += kTA) step(t0);
+    }
+    {  // the last tile, whole or not
+      __syncthreads();
+      lstore();
+      __syncthreads();
+      if constexpr (DENSE != 0) dense_last(t0);
+      const int64_t ab = t0 + w * kAPW;
 #pragma unroll 1
-        for (int gi = 0; gi < kAPW / 4; ++gi) {
-          const int64_t a4 = ab + 4 * gi;
-          if (a4 >= a_end) break;  // uniform
-          group(my, gi, a4, (int)min((int64_t)4, a_end - a4));
-        }
+      for (int gi = 0; gi < kAPW / 4; ++gi) {
+        const int64_t a4 = ab + 4 * gi;
+        if (a4 >= a_end) break;  // uniform
+        group(my, gi, a4, (int)min((int64_t)4, a_end - a4));
       }
     }
     // the 4 waves' sums meet in LDS (the tile buffer is free after this
@@ -2303,14 +2371,25 @@ int superpose_impl(const char *who, const float *d_xyz, int64_t fstride, int64_t
   auto stats = [&](auto P) {
     constexpr bool PL = decltype(P)::value;
 #define ST_LAUNCH(G, M, V) \
-  hipLaunchKernelGGL((k_frame_stats<G, M, V, 1, PL>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, plan, part, ps, d_dense, dense_pitch)
-    if (g && m) ST_LAUNCH(true, true, false);
+  hipLaunchKernelGGL((k_frame_stats<G, M, V, 1, PL>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, plan, part, ps)
+#define ST_DENSE(M, D) \
+  hipLaunchKernelGGL((k_frame_stats<true, M, false, 1, false, D>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, plan, part, ps, d_dense, dense_pitch)
+    if (d_dense) {
+      if constexpr (!PL) {
+        const bool dv = dense_pitch % 4 == 0 && reinterpret_cast<uintptr_t>(d_dense) % 16 == 0;
+        if (m && dv) ST_DENSE(true, 2);
+        else if (m) ST_DENSE(true, 1);
+        else if (dv) ST_DENSE(false, 2);
+        else ST_DENSE(false, 1);
+      }
+    } else if (g && m) ST_LAUNCH(true, true, false);
     else if (g) ST_LAUNCH(true, false, false);
     else if (m && vec4) ST_LAUNCH(false, true, true);
     else if (m) ST_LAUNCH(false, true, false);
     else if (vec4) ST_LAUNCH(false, false, true);
     else ST_LAUNCH(false, false, false);
 #undef ST_LAUNCH
+#undef ST_DENSE
   };
   if (planes) stats(std::true_type{});
   else stats(std::false_type{});

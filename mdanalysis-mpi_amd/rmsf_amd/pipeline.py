@@ -191,14 +191,15 @@ class Superposer:
         nbytes = eng.workspace_bytes(n_sel, max_batch)
         self.work = eng.empty(max(1, (nbytes + 7) // 8))
 
-    def run(self, b: Batch, ref: torch.Tensor, refinfo: torch.Tensor, dense_out: int | None = None) -> torch.Tensor:
+    def run(self, b: Batch, ref: torch.Tensor, refinfo: torch.Tensor, dense_out: int | None = None,
+            dense_stride: int = 0) -> torch.Tensor:
         xf = self.xform[: b.n_frames]
         need = self.eng.workspace_bytes(self.n_sel, b.n_frames)
         if need > self.work.numel() * 8:  # stats_plan's bytes are not monotone in the batch size
             self.work = self.eng.empty((need + 7) // 8)
         with _span(self.timer, "superpose", b.n_frames * self.n_sel):
             self.eng.superpose(b.ptr, b.fstride, b.n_frames, self.n_sel, b.sel, self.masses, ref, refinfo, xf,
-                               self.work, pstride=b.pstride, dense_out=dense_out)
+                               self.work, pstride=b.pstride, dense_out=dense_out, dense_stride=dense_stride)
         return xf
 
 
@@ -211,7 +212,8 @@ COMPACT_MAX_DENSITY = 0.5
 
 
 class _Compactor:
-    """The dense [frames, n_sel, 3] copy of a gathered selection's rows,
+    """The dense [frames, pitch] copy (rows of n_sel x 3 floats, padded to
+    16 B) of a gathered selection's rows,
     written by the covariance pass as it stages them
     (rmsf_superpose_compact) and read by the accumulate and, ``resident``
     (the whole block fits in half the free HBM), by every pass of a later
@@ -223,7 +225,11 @@ class _Compactor:
 
     def __init__(self, eng: Engine, n_sel: int, n_local: int, max_batch: int):
         self.n_sel = n_sel
-        row = 12 * n_sel
+        # rows padded to 16 B: the copy is written as float4 (a fixed store
+        # count per tile, rmsf_kernels.hip k_frame_stats DENSE 2) and the
+        # dense passes stage it as float4 (VEC4); the pad is never read
+        self.pitch = (3 * n_sel + 3) // 4 * 4
+        row = 4 * self.pitch
         budget = self.max_bytes
         if budget is None:
             budget = torch.cuda.mem_get_info(eng.device)[0] // 2
@@ -233,14 +239,14 @@ class _Compactor:
         self.usable = self.resident or self.frames >= max_batch
         self.buf = None
         if self.usable:
-            self.buf = torch.empty((max(1, self.frames), n_sel, 3), dtype=torch.float32, device=eng.device)
+            self.buf = torch.empty((max(1, self.frames), self.pitch), dtype=torch.float32, device=eng.device)
         self.filled = False
 
     def ptr(self, k: int) -> int:
-        return self.buf.data_ptr() + 12 * self.n_sel * k
+        return self.buf.data_ptr() + 4 * self.pitch * k
 
     def dense(self, k: int, n: int) -> Batch:
-        return Batch(self.ptr(k), 3 * self.n_sel, n, None)
+        return Batch(self.ptr(k), self.pitch, n, None)
 
     def resident_batches(self, n_local: int, max_batch: int):
         for k in range(0, n_local, max_batch):
@@ -542,7 +548,7 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
             if aligned:
                 if cmp is not None and b.sel is not None:
                     k = done if cmp.resident else 0
-                    xf = sup.run(b, ref, info, dense_out=cmp.ptr(k))
+                    xf = sup.run(b, ref, info, dense_out=cmp.ptr(k), dense_stride=cmp.pitch)
                     b = cmp.dense(k, b.n_frames)   # the accumulate reads the dense rows
                 else:
                     xf = sup.run(b, ref, info)

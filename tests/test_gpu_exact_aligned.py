@@ -245,9 +245,10 @@ def test_default_and_exact_agree():
     assert np.abs(a.rmsf - b.rmsf).max() < 1e-9
 
 
+@pytest.mark.parametrize("shape", [(3000, 50, 3, 10), (6000, 150, 1, 13)])
 @pytest.mark.parametrize("resident", [True, False])
 @pytest.mark.parametrize("align", ["frame0", "average"])
-def test_compacted_sparse_selection_same_bits(align, resident, monkeypatch):
+def test_compacted_sparse_selection_same_bits(align, resident, shape, monkeypatch):
     """Round 6 (verdict item 2): over a sparse gathered selection the aligned
     path writes the selected rows out once (rmsf_superpose_compact) and the
     later passes read them dense.  A gather is an exact copy and the dense
@@ -257,11 +258,11 @@ def test_compacted_sparse_selection_same_bits(align, resident, monkeypatch):
     from rmsf_amd import RMSF
     from rmsf_amd import pipeline as PL
     from rmsf_amd.synth import motion_table
+    n, nf, first, stride = shape  # 300 atoms (rows of 900 floats), 462 (1,386 -> padded to 1,388)
+    sel = np.arange(first, n, stride)
     if not resident:
-        monkeypatch.setattr(PL._Compactor, "max_bytes", 12 * 300 * 30)  # 30 frames: per 23-frame batch
-    n, nf = 3000, 50
+        monkeypatch.setattr(PL._Compactor, "max_bytes", (3 * len(sel) + 3) // 4 * 4 * 4 * 30)  # 30 padded rows
     traj = torch.tensor(SY.frames(41, n, 0, nf, motion_table(42, nf)), device="cuda")
-    sel = np.arange(3, n, 10)
     m = np.random.default_rng(43).uniform(1.0, 16.0, len(sel))
     from rmsf_amd.engine import Engine
     from rmsf_amd.sources import DeviceSource, FrameList
@@ -281,6 +282,48 @@ def test_compacted_sparse_selection_same_bits(align, resident, monkeypatch):
         _same(out[True][k], v, k)
     want = O.rmsf_script(traj.cpu().numpy(), sel, m, size=1, align=align)
     np.testing.assert_allclose(out[True]["rmsf"], want["rmsf"], rtol=0, atol=TOL)
+
+
+@pytest.mark.parametrize("masses", [False, True])
+@pytest.mark.parametrize("pitch", ["packed", "padded", "odd"])
+@pytest.mark.parametrize("shape", [(2000, 64, 0, 10), (5000, 131, 2, 11), (700, 7, 5, 3)])
+def test_superpose_compact_kernel(shape, pitch, masses):
+    """rmsf_superpose_compact at the kernel level: the transform records are
+    bit-identical to rmsf_superpose's over the same gathered rows, every
+    copied row equals the selected coordinates, and nothing outside the
+    rows is written (the pad of a padded pitch, the frame past the last).
+    Whole tiles with a successor take the fixed-count store loop, float4 for
+    a 16-B pitch ("padded", and "packed" when 3 n_sel is a multiple of 4) or
+    single floats ("odd"), and frames past the trajectory in a 64-frame
+    group rewrite its last row; the last tile of a segment takes the
+    general form."""
+    from rmsf_amd._lib import RMSF_XFORM_DOUBLES
+    from rmsf_amd.engine import Engine
+    from rmsf_amd.synth import motion_table
+    n, nf, first, stride = shape
+    eng = Engine()
+    traj = torch.tensor(SY.frames(51, n, 0, nf, motion_table(52, nf)), device="cuda")
+    sel_h = np.arange(first, n, stride)
+    ns = len(sel_h)
+    sel = eng.sel_tensor(sel_h)
+    m = None
+    if masses:
+        m = torch.tensor(np.random.default_rng(53).uniform(1.0, 16.0, ns), device="cuda")
+    dstride = {"packed": 3 * ns, "padded": (3 * ns + 3) // 4 * 4, "odd": 3 * ns + 5}[pitch]
+    ref, info = eng.reference_setup(ns, frame_ptr=traj.data_ptr(), sel=sel, masses=m)
+    work = eng.empty((eng.workspace_bytes(ns, nf) + 7) // 8)
+    xf0 = eng.empty(nf, RMSF_XFORM_DOUBLES)
+    xf1 = eng.empty(nf, RMSF_XFORM_DOUBLES)
+    dense = torch.full((nf + 1, dstride), float("nan"), dtype=torch.float32, device="cuda")
+    eng.superpose(traj.data_ptr(), 3 * n, nf, ns, sel, m, ref, info, xf0, work)
+    eng.superpose(traj.data_ptr(), 3 * n, nf, ns, sel, m, ref, info, xf1, work, dense_out=dense.data_ptr(),
+                  dense_stride=dstride)
+    torch.cuda.synchronize()
+    _same(xf1.cpu().numpy(), xf0.cpu().numpy(), "records")
+    d = dense.cpu().numpy()
+    want = traj.cpu().numpy()[:, sel_h].reshape(nf, 3 * ns)
+    np.testing.assert_array_equal(d[:nf, :3 * ns].view(np.uint32), want.view(np.uint32))
+    assert np.isnan(d[:nf, 3 * ns:]).all() and np.isnan(d[nf]).all()
 
 
 @pytest.mark.parametrize("P", [1, 2])
