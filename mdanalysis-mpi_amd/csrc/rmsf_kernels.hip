@@ -679,12 +679,97 @@ __global__ __launch_bounds__(kBlock) void k_welford_seq_atoms(const float *__res
 // aligned coordinate now and then -- a cost of |x - mean| ulp / (N RMSF)
 // that only a few-frame run can push past 1e-6 A.
 //
-// k_ref_seq: the centred reference, one workgroup.  x = frame[sel[a]]
-// (f32 -> f64) or avg[a] / div (RMSF.py:111, written to avg_out too);
-// com_c = (sum_a x_ac m_a, atom by atom) / mass_total (RMSF.py:84/117);
-// ref = x - com (RMSF.py:85/118); the record [0..15]: com, sum r, G2 =
-// sum_a ((r0 r0 + r1 r1) + r2 r2) in qcprot's per-atom order (the G2 of
-// every InnerProduct call against this reference), mass_total, n_sel.
+// wave_seq_sum: s = ((t_0 + t_1) + t_2) + ... over atoms 0..n-1, the
+// reference's order, by one wave.  Its 64 lanes form the terms of a block
+// of kSeqBlk atoms at once (lane i: atoms a0 + i + 64 j -- coalesced loads,
+// elementwise terms with the same roundings as the serial statement), park
+// them in the wave's LDS slice, and one serial chain adds them in order
+// (broadcast reads); the next block's loads are issued before the chain
+// runs.  The adds are the only serial work: ~2 instructions per atom.  (The
+// first round-6 form walked every chain in one lane per frame: ~500 cycles
+// per atom, 24 ms for one sweep's superposition of 100k atoms x 100 frames;
+// profiles/r06_workloads/probe_exact_aligned.txt.)  load(a) issues atom a's
+// loads (a clamped to the last atom: every block issues the same count),
+// term(raw, a) forms t_a.  lds: kSeqBlk doubles private to the wave.
+constexpr int kSeqK = 4;              // atoms per lane per block
+constexpr int kSeqBlk = 64 * kSeqK;   // atoms per block
+template <class Load, class Term>
+__device__ __forceinline__ double wave_seq_sum(int64_t n, double *lds, Load load, Term term) {
+  using Raw = decltype(load(int64_t(0)));
+  const int lane = threadIdx.x & 63;
+  Raw va[kSeqK], vb[kSeqK];
+  double s = 0.0;
+  auto fill = [&](Raw(&v)[kSeqK], int64_t a0) {
+#pragma unroll
+    for (int j = 0; j < kSeqK; ++j) v[j] = load(min(a0 + lane + 64 * j, n - 1));
+    __builtin_amdgcn_sched_barrier(0);  // issued before the chain below
+  };
+  auto run = [&](const Raw(&v)[kSeqK], int64_t a0) {
+#pragma unroll
+    for (int j = 0; j < kSeqK; ++j) lds[lane + 64 * j] = term(v[j], a0 + lane + 64 * j);
+    __builtin_amdgcn_wave_barrier();  // one wave: its LDS operations complete in order
+    const int cnt = (int)min((int64_t)kSeqBlk, n - a0);
+    if (cnt == kSeqBlk) {  // the next 16 terms' reads in flight while 16 are added
+      constexpr int G = 16;
+      double ta[G], tb[G];
+      auto rd = [&](double(&t)[G], int i0) {
+#pragma unroll
+        for (int k = 0; k < G; ++k) t[k] = lds[i0 + k];
+      };
+      auto add = [&](const double(&t)[G]) {
+#pragma unroll
+        for (int k = 0; k < G; ++k) s = s + t[k];
+      };
+      rd(ta, 0);
+#pragma unroll
+      for (int i0 = 0; i0 < kSeqBlk; i0 += 2 * G) {
+        rd(tb, i0 + G);
+        add(ta);
+        if (i0 + 2 * G < kSeqBlk) rd(ta, i0 + 2 * G);
+        add(tb);
+      }
+    } else {
+      for (int i = 0; i < cnt; ++i) s = s + lds[i];
+    }
+    __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next block
+  };
+  fill(va, 0);
+  int64_t a0 = 0;
+  for (; a0 + 2 * kSeqBlk < n; a0 += 2 * kSeqBlk) {
+    fill(vb, a0 + kSeqBlk);
+    run(va, a0);
+    fill(va, a0 + 2 * kSeqBlk);
+    run(vb, a0 + kSeqBlk);
+  }
+  fill(vb, a0 + kSeqBlk);
+  run(va, a0);
+  if (a0 + kSeqBlk < n) run(vb, a0 + kSeqBlk);
+  return s;
+}
+
+struct SeqF1D {  // a coordinate and an f64 factor (mass / reference)
+  float x;
+  double d;
+};
+struct SeqF3 {
+  float x, y, z;
+};
+struct SeqD1D {
+  double x, d;
+};
+struct SeqD3 {
+  double x, y, z;
+};
+
+// k_ref_seq: the centred reference, one workgroup of four waves.
+//   1. x = frame[sel[a]] (f32 -> f64) or avg[a] / div (RMSF.py:111, also to
+//      avg_out) into ref, all threads;
+//   2. com_c = (sum_a x_ac m_a, atom by atom) / mass_total (RMSF.py:84/117),
+//      wave c's chain;
+//   3. ref = x - com in place (RMSF.py:85/118), all threads;
+//   4. the record [0..15]: com, sum r (waves 0-2), G2 = sum_a ((r0 r0 + r1
+//      r1) + r2 r2) in qcprot's per-atom order (wave 3; the G2 of every
+//      InnerProduct call against this reference), mass_total, n_sel.
 template <bool FROM_F32, bool GATHER, bool MASSES>
 __global__ __launch_bounds__(kBlock) void k_ref_seq(const float *__restrict__ frame, const double *__restrict__ avg,
                                                     double div, int64_t n_sel, const int32_t *__restrict__ sel,
@@ -692,106 +777,130 @@ __global__ __launch_bounds__(kBlock) void k_ref_seq(const float *__restrict__ fr
                                                     double *__restrict__ avg_out, double *__restrict__ ref,
                                                     double *__restrict__ info) {
   __shared__ double com[3];
-  auto load = [&](int64_t a, int c) -> double {
-    if (FROM_F32) return (double)frame[3 * (GATHER ? (int64_t)sel[a] : a) + c];
-    return avg[3 * a + c] / div;
-  };
-  if (!FROM_F32 && avg_out)
-    for (int64_t j = threadIdx.x; j < 3 * n_sel; j += kBlock) avg_out[j] = avg[j] / div;
-  if (threadIdx.x < 3) {  // three independent chains, one per axis
-    const int c = threadIdx.x;
-    double s = 0.0;
-#pragma unroll 4
-    for (int64_t a = 0; a < n_sel; ++a) s = s + load(a, c) * (MASSES ? masses[a] : 1.0);
-    com[c] = s / mass_total;
+  __shared__ double slice[kBlock / 64][kSeqBlk];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool lead = (threadIdx.x & 63) == 0;
+  for (int64_t a = threadIdx.x; a < n_sel; a += kBlock) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      double x;
+      if (FROM_F32) {
+        x = (double)frame[3 * (GATHER ? (int64_t)sel[a] : a) + c];
+      } else {
+        x = avg[3 * a + c] / div;
+        if (avg_out) avg_out[3 * a + c] = x;
+      }
+      ref[3 * a + c] = x;
+    }
+  }
+  __syncthreads();
+  if (w < 3) {  // three independent chains, one per axis
+    const int c = w;
+    const double s = wave_seq_sum(
+        n_sel, slice[w], [&](int64_t a) { return SeqD1D{ref[3 * a + c], MASSES ? masses[a] : 1.0}; },
+        [&](const SeqD1D &v, int64_t) { return v.x * v.d; });
+    if (lead) com[c] = s / mass_total;
   }
   __syncthreads();
   const double c0 = com[0], c1 = com[1], c2 = com[2];
   for (int64_t a = threadIdx.x; a < n_sel; a += kBlock) {
-    ref[3 * a] = load(a, 0) - c0;
-    ref[3 * a + 1] = load(a, 1) - c1;
-    ref[3 * a + 2] = load(a, 2) - c2;
+    ref[3 * a] = ref[3 * a] - c0;
+    ref[3 * a + 1] = ref[3 * a + 1] - c1;
+    ref[3 * a + 2] = ref[3 * a + 2] - c2;
   }
-  if (threadIdx.x == 0) {  // the same r recomputed (same bits), summed in order
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, g = 0.0;
-#pragma unroll 4
-    for (int64_t a = 0; a < n_sel; ++a) {
-      const double r0 = load(a, 0) - c0, r1 = load(a, 1) - c1, r2 = load(a, 2) - c2;
-      s0 = s0 + r0;
-      s1 = s1 + r1;
-      s2 = s2 + r2;
-      g = g + (r0 * r0 + r1 * r1 + r2 * r2);
+  __syncthreads();
+  if (w < 3) {  // the sums of r, in order
+    const int c = w;
+    const double s = wave_seq_sum(
+        n_sel, slice[w], [&](int64_t a) { return ref[3 * a + c]; }, [&](double r, int64_t) { return r; });
+    if (lead) info[3 + c] = s;
+  } else {
+    const double g = wave_seq_sum(
+        n_sel, slice[w], [&](int64_t a) { return SeqD3{ref[3 * a], ref[3 * a + 1], ref[3 * a + 2]}; },
+        [&](const SeqD3 &r, int64_t) { return r.x * r.x + r.y * r.y + r.z * r.z; });
+    if (lead) {
+      info[0] = c0;
+      info[1] = c1;
+      info[2] = c2;
+      info[6] = g;
+      info[7] = mass_total;
+      info[8] = (double)n_sel;
+      for (int j = 9; j < 16; ++j) info[j] = 0.0;
     }
-    info[0] = c0;
-    info[1] = c1;
-    info[2] = c2;
-    info[3] = s0;
-    info[4] = s1;
-    info[5] = s2;
-    info[6] = g;
-    info[7] = mass_total;
-    info[8] = (double)n_sel;
-    for (int j = 9; j < 16; ++j) info[j] = 0.0;
   }
 }
 
-// k_superpose_seq: one lane per frame -- the frame's mobile COM (RMSF.py:94
-// / 127, atom by atom), its centred coordinates f64(x) - com (RMSF.py:95 /
-// 128), qcprot's InnerProduct loop against the reference (A, G1; G2 from the
-// record), E0 = (G1 + G2) * 0.5 and the QCP solve (RMSF.py:43-51) -> the
-// transform record.  The atom index is wave-uniform, so the selection, the
-// masses and the reference rows arrive by scalar loads; each lane walks its
-// own frame (frames are independent chains, atoms are not).
+// The per-frame superposition of exact=True (RMSF.py:94-97 / 127-131 +
+// get_rotation_matrix, RMSF.py:43-51), one wave per (frame, chain):
+//   k_seq_com: the frame's mobile COM (RMSF.py:94 / 127), atom by atom, chain
+//     c the axis c; written to the record's [9..11];
+//   k_seq_ip: qcprot's InnerProduct loop against the reference, chain j < 9
+//     A[j] = sum_a x1_a[j/3] r_a[j%3], chain 9 G1 = sum_a ((x1 x1 + y1 y1) +
+//     z1 z1), x1 = f64(x) - com (RMSF.py:95 / 128); A parked in the record's
+//     [0..8], G1 in [13];
+//   k_seq_qcp: E0 = (G1 + G2) * 0.5 and the QCP solve -> R in [0..8], rmsd in
+//     [12], [13..15] zero.
 template <bool GATHER, bool MASSES>
-__global__ __launch_bounds__(64) void k_superpose_seq(const float *__restrict__ xyz, int64_t fstride,
-                                                      int64_t n_frames, int64_t n_sel,
-                                                      const int32_t *__restrict__ sel,
-                                                      const double *__restrict__ masses, double mass_total,
-                                                      const double *__restrict__ ref,
-                                                      const double *__restrict__ refinfo,
-                                                      double *__restrict__ xform) {
+__global__ __launch_bounds__(64) void k_seq_com(const float *__restrict__ xyz, int64_t fstride, int64_t n_sel,
+                                                const int32_t *__restrict__ sel, const double *__restrict__ masses,
+                                                double mass_total, double *__restrict__ xform) {
+  __shared__ double slice[kSeqBlk];
+  const int64_t f = blockIdx.x;
+  const int c = blockIdx.y;
+  const float *__restrict__ fr = xyz + f * fstride + c;
+  const double s = wave_seq_sum(
+      n_sel, slice,
+      [&](int64_t a) { return SeqF1D{fr[3 * (GATHER ? (int64_t)sel[a] : a)], MASSES ? masses[a] : 1.0}; },
+      [&](const SeqF1D &v, int64_t) { return (double)v.x * v.d; });
+  if (threadIdx.x == 0) xform[f * kXform + 9 + c] = s / mass_total;
+}
+
+template <bool GATHER>
+__global__ __launch_bounds__(64) void k_seq_ip(const float *__restrict__ xyz, int64_t fstride, int64_t n_sel,
+                                               const int32_t *__restrict__ sel, const double *__restrict__ ref,
+                                               double *__restrict__ xform) {
+  __shared__ double slice[kSeqBlk];
+  const int64_t f = blockIdx.x;
+  const int j = blockIdx.y;
+  const float *__restrict__ fr = xyz + f * fstride;
+  const double *t = xform + f * kXform;
+  auto row = [&](int64_t a) -> int64_t { return 3 * (GATHER ? (int64_t)sel[a] : a); };
+  double s;
+  if (j < 9) {
+    const int ax = j / 3, rb = j % 3;
+    const double cx = t[9 + ax];
+    s = wave_seq_sum(
+        n_sel, slice, [&](int64_t a) { return SeqF1D{fr[row(a) + ax], ref[3 * a + rb]}; },
+        [&](const SeqF1D &v, int64_t) { return ((double)v.x - cx) * v.d; });
+  } else {
+    const double c0 = t[9], c1 = t[10], c2 = t[11];
+    s = wave_seq_sum(
+        n_sel, slice,
+        [&](int64_t a) {
+          const float *p = fr + row(a);
+          return SeqF3{p[0], p[1], p[2]};
+        },
+        [&](const SeqF3 &v, int64_t) {
+          const double x1 = (double)v.x - c0, y1 = (double)v.y - c1, z1 = (double)v.z - c2;
+          return x1 * x1 + y1 * y1 + z1 * z1;
+        });
+  }
+  if (threadIdx.x == 0) xform[f * kXform + (j < 9 ? j : 13)] = s;
+}
+
+__global__ __launch_bounds__(64) void k_seq_qcp(int64_t n_frames, int64_t n_sel, const double *__restrict__ refinfo,
+                                                double *__restrict__ xform) {
   const int64_t f = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (f >= n_frames) return;
-  const float *__restrict__ fr = xyz + f * fstride;
-  double c0 = 0.0, c1 = 0.0, c2 = 0.0;
-#pragma unroll 4
-  for (int64_t a = 0; a < n_sel; ++a) {
-    const float *p = fr + 3 * (GATHER ? (int64_t)sel[a] : a);
-    const double m = MASSES ? masses[a] : 1.0;
-    c0 = c0 + (double)p[0] * m;
-    c1 = c1 + (double)p[1] * m;
-    c2 = c2 + (double)p[2] * m;
-  }
-  c0 = c0 / mass_total;
-  c1 = c1 / mass_total;
-  c2 = c2 / mass_total;
-  double A[9] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, G1 = 0.0;
-#pragma unroll 2
-  for (int64_t a = 0; a < n_sel; ++a) {
-    const float *p = fr + 3 * (GATHER ? (int64_t)sel[a] : a);
-    const double x1 = (double)p[0] - c0, y1 = (double)p[1] - c1, z1 = (double)p[2] - c2;
-    const double *r = ref + 3 * a;
-    const double x2 = r[0], y2 = r[1], z2 = r[2];
-    G1 = G1 + (x1 * x1 + y1 * y1 + z1 * z1);
-    A[0] = A[0] + x1 * x2;
-    A[1] = A[1] + x1 * y2;
-    A[2] = A[2] + x1 * z2;
-    A[3] = A[3] + y1 * x2;
-    A[4] = A[4] + y1 * y2;
-    A[5] = A[5] + y1 * z2;
-    A[6] = A[6] + z1 * x2;
-    A[7] = A[7] + z1 * y2;
-    A[8] = A[8] + z1 * z2;
-  }
-  const double E0 = (G1 + refinfo[6]) * 0.5;
+  double *t = xform + f * kXform;
+  double A[9];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) A[j] = t[j];
+  const double E0 = (t[13] + refinfo[6]) * 0.5;
   double rot[9], rmsd;
   qcp_solve(A, E0, (double)n_sel, rot, &rmsd);
-  double *t = xform + f * kXform;
 #pragma unroll
   for (int j = 0; j < 9; ++j) t[j] = rot[j];
-  t[9] = c0;
-  t[10] = c1;
-  t[11] = c2;
   t[12] = rmsd;
   t[13] = t[14] = t[15] = 0.0;
 }
@@ -3141,18 +3250,25 @@ RMSF_EXPORT int rmsf_superpose_sequential(const float *d_xyz, int64_t fstride, i
   if (!d_xyz || !d_ref || !d_refinfo || !d_xform || n_sel < 1 || n_frames < 0 || fstride < (d_sel ? 3 : 3 * n_sel))
     return fail(RMSF_EINVAL, "rmsf_superpose_sequential: bad arguments");
   if (n_frames == 0) return RMSF_OK;
-  const dim3 grid((unsigned)((n_frames + 63) / 64));
+  const unsigned fb = (unsigned)((n_frames + 63) / 64);
   hipStream_t s = S(stream);
   const bool g = d_sel != nullptr, m = d_masses != nullptr;
-#define SEQSUP(G, M)                                                                                          \
-  hipLaunchKernelGGL((k_superpose_seq<G, M>), grid, dim3(64), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, \
-                     mass_total, d_ref, d_refinfo, d_xform)
-  if (g && m) SEQSUP(true, true);
-  else if (g) SEQSUP(true, false);
-  else if (m) SEQSUP(false, true);
-  else SEQSUP(false, false);
-#undef SEQSUP
-  return after_launch("k_superpose_seq");
+  const dim3 gc((unsigned)n_frames, 3), gi((unsigned)n_frames, 10);
+#define SEQCOM(G, M) \
+  hipLaunchKernelGGL((k_seq_com<G, M>), gc, dim3(64), 0, s, d_xyz, fstride, n_sel, d_sel, d_masses, mass_total, d_xform)
+  if (g && m) SEQCOM(true, true);
+  else if (g) SEQCOM(true, false);
+  else if (m) SEQCOM(false, true);
+  else SEQCOM(false, false);
+#undef SEQCOM
+  if (int rc = after_launch("k_seq_com")) return rc;
+  if (g)
+    hipLaunchKernelGGL((k_seq_ip<true>), gi, dim3(64), 0, s, d_xyz, fstride, n_sel, d_sel, d_ref, d_xform);
+  else
+    hipLaunchKernelGGL((k_seq_ip<false>), gi, dim3(64), 0, s, d_xyz, fstride, n_sel, d_sel, d_ref, d_xform);
+  if (int rc = after_launch("k_seq_ip")) return rc;
+  hipLaunchKernelGGL(k_seq_qcp, dim3(fb), dim3(64), 0, s, n_frames, n_sel, d_refinfo, d_xform);
+  return after_launch("k_seq_qcp");
 }
 
 RMSF_EXPORT int rmsf_accumulate_sequential(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
