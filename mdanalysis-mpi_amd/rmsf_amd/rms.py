@@ -102,8 +102,11 @@ class RMSF:
         (BENCH_r05 ``modes.c2_exact``; INTEGRATION.md).  Aligned:
         RMSF.py:80-146, the references, every frame's COM and qcprot inner
         product atom by atom, the sweep-1 sum and Welford frame by frame
-        (the rmsf_*_sequential kernels) -- serial in a frame's atoms, so its
-        cost grows with the selection.  The ranks are
+        (the rmsf_*_sequential kernels) -- each sum an in-order add chain
+        over the atoms, so its cost grows with the selection, not the
+        frames: faster than the default at RMSF.py's 214 atoms, 2.6-5.2 ms
+        against 0.17-0.30 ms at 100k atoms x 100 frames (DESIGN section 5,
+        "Few frames").  The ranks are
         folded by second_order_moments in RMSF.py:143's reduce order
         (``merge_order``), then RMSF.py:146.  False: the frame-parallel
         path, which agrees to ~1e-13 unaligned and, aligned, to within one
