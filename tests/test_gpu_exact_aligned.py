@@ -174,6 +174,28 @@ def test_exact_aligned_vs_oracle(ci, where):
         _same(r.average, want["average"], "average")
 
 
+@pytest.mark.parametrize("gathered", [False, True])
+@pytest.mark.parametrize("n_sel", [2, 3, 63, 64, 65, 255, 256, 257, 511, 512, 513, 769])
+def test_exact_aligned_block_edges(n_sel, gathered):
+    """The serial sums run 256 atoms per block in one wave (wave_seq_sum:
+    whole blocks, a two-block loop, a partial last block); selections on
+    either side of every block edge equal the oracle bit for bit."""
+    from rmsf_amd import RMSF
+    from rmsf_amd.synth import motion_table
+    nf = 6
+    n_atoms = 3 * n_sel + 1 if gathered else n_sel
+    traj = SY.frames(61, n_atoms, 0, nf, motion_table(62, nf))
+    sel = np.arange(1, n_atoms, 3)[:n_sel] if gathered else np.arange(n_sel)
+    m = np.random.default_rng(63).uniform(1.0, 16.0, n_sel)
+    for align in ("frame0", "average"):
+        r = RMSF(torch.tensor(traj, device="cuda"), select=sel, masses=m, align=align, exact=True).run().results
+        want = O.rmsf_script(traj, sel, m, size=1, align=align)
+        _same(r.rmsf, want["rmsf"], f"rmsf {align}")
+        _same(r.mean, want["mean"], f"mean {align}")
+        if align == "average":
+            _same(r.average, want["average"], "average")
+
+
 @pytest.mark.parametrize("align", ["frame0", "average"])
 def test_exact_transforms_and_rmsd(align):
     """The per-frame records of the last sweep: rotation, mobile COM and the
