@@ -242,7 +242,7 @@ def c1_latency(eng, no_cpu: bool) -> dict:
     import numpy as np
     import torch
 
-    from rmsf_amd.pipeline import CapturedPipeline, run_pipeline
+    from rmsf_amd.pipeline import CapturedPipeline, auto_exact, run_pipeline
     from rmsf_amd.sources import DeviceSource, FrameList
     from rmsf_amd.synth import generate, motion_table
 
@@ -271,8 +271,21 @@ def c1_latency(eng, no_cpu: bool) -> dict:
     torch.cuda.synchronize()
     graph_ms = (time.perf_counter() - t0) / reps * 1e3
     same = bool(torch.equal(cap.result.rmsf, res.rmsf))
+    # the default above is the exact path (aligned, under AUTO_EXACT_FRAMES
+    # frames); the frame-parallel path beside it
+    for _ in range(5):
+        run_pipeline(eng, src, fl, align="average", exact=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fp = run_pipeline(eng, src, fl, align="average", exact=False)
+    torch.cuda.synchronize()
+    fp_ms = (time.perf_counter() - t0) / reps * 1e3
     out = {"workload": "C1 shape: 3341 atoms, 214 selected, 98 frames, RMSF.py two-sweep",
+           "default_path": "exact" if auto_exact("average", nf) else "frame-parallel",
            "gpu_ms_eager": gpu_ms, "gpu_ms_hipgraph": graph_ms, "hipgraph_bitwise_equal": same,
+           "gpu_ms_eager_frame_parallel": fp_ms,
+           "max_abs_diff_frame_parallel_A": float((fp.rmsf - res.rmsf).abs().max()),
            "sanity": sanity(eng, res.rmsf, nf, seed=11, atoms=sel)}
     if not no_cpu:
         from oracle import rmsf_oracle as O
