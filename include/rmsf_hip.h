@@ -410,7 +410,8 @@ int rmsf_welford_sequential(const float *d_xyz, int64_t frame_stride,
  * divided by avg_divisor = n_frames as they are read and written to
  * d_avg_out when non-NULL; d_sel must be NULL): ref_com, d_ref = x - ref_com,
  * and the refinfo record (ref_com, sum r, G2 of qcprot's loop, mass_total,
- * n_sel).  One workgroup; serial in the atoms (~1 ms per 100k atoms).     */
+ * n_sel).  One workgroup: each sum is one wave's in-order add chain (two
+ * chain phases, ~0.6 ms each per 100k atoms).                              */
 int rmsf_reference_setup_sequential(const float *d_frame, const double *d_avg,
                                     double avg_divisor, int64_t n_sel,
                                     const int32_t *d_sel, const double *d_masses,
@@ -418,12 +419,15 @@ int rmsf_reference_setup_sequential(const float *d_frame, const double *d_avg,
                                     double *d_ref, double *d_refinfo,
                                     void *stream);
 /* rmsf_superpose_sequential: RMSF.py:94-97 / 127-131 + get_rotation_matrix
- * for every frame (one lane per frame): mobile COM atom by atom, centred
- * coordinates f64(x) - com, InnerProduct against d_ref (G2 from
- * d_refinfo[6], i.e. a record of rmsf_reference_setup_sequential), QCP ->
- * d_xform[f * RMSF_XFORM_DOUBLES] as rmsf_superpose writes it (COM absolute).
- * Rows only (frame, atom, xyz).  Serial in the atoms of a frame: for large
- * selections this is the exact path's cost.            */
+ * for every frame: mobile COM atom by atom, centred coordinates f64(x) - com,
+ * InnerProduct against d_ref (G2 from d_refinfo[6], i.e. a record of
+ * rmsf_reference_setup_sequential), QCP -> d_xform[f * RMSF_XFORM_DOUBLES]
+ * as rmsf_superpose writes it (COM absolute).  Rows only (frame, atom, xyz).
+ * Three launches: the COM (one wave per frame and axis), the InnerProduct
+ * (one wave per frame and sum: A[0..8], G1) and the QCP (one lane per
+ * frame); d_xform holds the COM and the sums in between.  Each sum is an
+ * in-order add chain over the atoms, so the cost grows with n_sel, not the
+ * frames: ~1.2 ms per 100k atoms ("Few frames").       */
 int rmsf_superpose_sequential(const float *d_xyz, int64_t frame_stride,
                               int64_t n_frames, int64_t n_sel,
                               const int32_t *d_sel, const double *d_masses,

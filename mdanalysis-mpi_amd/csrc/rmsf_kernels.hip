@@ -1499,7 +1499,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     // 2.43 GB as 3.8e7 64-B writes: instruction-issue waits +1.6e9 cycles
     // and L1 pending stalls +46 %, i.e. the writes share the vector memory
     // path with the gather's per-line requests
-    // (profiles/r06_workloads/pmc_dense_store.txt).
+    // (profiles/r06_workloads/pmc_dense_store.txt).  Storing from wave 0
+    // only, or after the tile's sums, costs the same (ab_dense_store_split.txt).
     auto dense_whole = [&](int64_t t0) {
       if constexpr (DENSE == 2) {
         f32x4 v[kNPre];
