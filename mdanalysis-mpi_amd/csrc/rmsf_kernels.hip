@@ -1488,49 +1488,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     // the copy.  Writing the copy here beats a stand-alone gather before a
     // dense covariance pass (ratios to re-gathering on one box,
     // profiles/r06_workloads/).
-    // dense_whole: a whole tile with a successor, a FIXED number of stores
-    // per thread (DENSE 2: 6 float4; DENSE 1, rows not 16-B aligned: 24
-    // floats; rows past the trajectory rewrite its last row with the same
-    // values, as gload staged them from it).  vmcnt counts loads and stores
-    // in issue order, so with a fixed count after the next tile's loads the
-    // wait for those loads leaves the stores in flight: vmcnt(6), not
-    // vmcnt(0) (SQ_WAIT_ANY 2.2e8 against 1.3e9 cycles re-gathered).  The
-    // copy still costs +1.4-1.8 ms at 10k of 100k atoms x 20k frames, for
-    // 2.43 GB as 3.8e7 64-B writes: instruction-issue waits +1.6e9 cycles
-    // and L1 pending stalls +46 %, i.e. the writes share the vector memory
-    // path with the gather's per-line requests
-    // (profiles/r06_workloads/pmc_dense_store.txt).  Storing from wave 0
-    // only, or after the tile's sums, costs the same (ab_dense_store_split.txt).
-    auto dense_whole = [&](int64_t t0) {
-      if constexpr (DENSE == 2) {
-        f32x4 v[kNPre];
-#pragma unroll
-        for (int k = 0; k < kNPre; ++k) {
-          const int idx = threadIdx.x + k * kBlock;
-          v[k] = *reinterpret_cast<const f32x4 *>(tile + (idx / kRow4) * kPitch + 4 * (idx % kRow4));
-        }
-#pragma unroll
-        for (int k = 0; k < kNPre; ++k) {
-          const int idx = threadIdx.x + k * kBlock;
-          const int64_t fr = min(f0 + idx / kRow4, last);
-          __builtin_nontemporal_store(v[k], reinterpret_cast<f32x4 *>(dense + fr * dpitch + 3 * t0) + idx % kRow4);
-        }
-      } else {
-        constexpr int kN = kTF * 3 * kTA / kBlock;
-        float v[kN];
-#pragma unroll
-        for (int k = 0; k < kN; ++k) {
-          const int idx = threadIdx.x + k * kBlock;
-          v[k] = tile[(idx / (3 * kTA)) * kPitch + idx % (3 * kTA)];
-        }
-#pragma unroll
-        for (int k = 0; k < kN; ++k) {
-          const int idx = threadIdx.x + k * kBlock;
-          const int64_t fr = min(f0 + idx / (3 * kTA), last);
-          __builtin_nontemporal_store(v[k], dense + fr * dpitch + 3 * t0 + idx % (3 * kTA));
-        }
-      }
-    };
+    // The copy costs +1.4-1.8 ms at 10k of 100k atoms x 20k frames for its
+    // 2.43 GB (3.8e7 64-B writes) beside the gathered read, where the bytes
+    // alone would take 0.4 ms.  None of the kernel-side levers moved it:
+    // store forms and row pitches, storing before or after the next tile's
+    // loads or after the tile's sums, from one wave or all, keeping the
+    // stores in flight across the next wait (a fixed count per tile), and 2
+    // or 3 waves per SIMD all measured the same
+    // (profiles/r06_workloads/ab_dense_store_split.txt, pmc_dense_store.txt:
+    // instruction-issue waits +1.6e9 cycles and L1 pending stalls +46 %).
     // the segment's last tile, whole or not
     auto dense_last = [&](int64_t t0) {
       const int nfl = 3 * (int)min((int64_t)kTA, a_end - t0);
@@ -1538,6 +1504,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
         const int row = idx / (3 * kTA), e = idx - row * (3 * kTA);
         if (e < nfl && f0 + row <= last)
           __builtin_nontemporal_store(tile[row * kPitch + e], dense + (f0 + row) * dpitch + 3 * t0 + e);
+      }
+    };
+    // DENSE 2: threads 0..239 own one float4 column (t % 24) of rows t / 24 +
+    // 10 k, so a thread's copy addresses are one base plus constant strides:
+    // few registers, and the kernel keeps 3 waves per SIMD (WPE 3) as the
+    // re-gathering kernel does.  (Measured equal to 2 waves per SIMD with
+    // per-row addresses, ab_dense_store_split.txt: the copy's cost is not
+    // occupancy.)  DENSE 1 (a copy pitch not 16-B aligned; only through the
+    // ABI) takes the general loop.
+    auto dense_whole = [&](int64_t t0) {
+      if constexpr (DENSE == 2) {
+        constexpr int kRows = kBlock / kRow4;  // 10 rows per pass
+        if (threadIdx.x < kRows * kRow4) {
+          const int col = threadIdx.x % kRow4, r0 = threadIdx.x / kRow4;
+          const float *src = tile + r0 * kPitch + 4 * col;
+          f32x4 *dst = reinterpret_cast<f32x4 *>(dense + (f0 + r0) * dpitch + 3 * t0) + col;
+          const int64_t step4 = kRows * dpitch / 4;
+#pragma unroll
+          for (int k = 0; k < (kTF + kRows - 1) / kRows; ++k) {
+            const int row = r0 + kRows * k;
+            if (row < kTF && f0 + row <= last)
+              __builtin_nontemporal_store(*reinterpret_cast<const f32x4 *>(src + kRows * kPitch * k), dst + step4 * k);
+          }
+        }
+      } else {
+        dense_last(t0);
       }
     };
     // one 4-atom group of this wave's slab (atoms a4..a4+3, a wave-uniform index)
@@ -1587,9 +1579,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     // loop are unconditional.  (Behind an `if (t0 + kTA < a_end)` the
     // element path's loaded values met the loop-carried ones in a phi, and
     // the copies resolving it waited for the loads right after issuing
-    // them: no load was in flight across the tile's sums.)  With DENSE the
-    // first tile is peeled too, so both edges into the loop carry the same
-    // loads-then-stores sequence and the wait at its top can count them.
+    // them: no load was in flight across the tile's sums.)
     auto step = [&](int64_t t0) {  // a whole tile with a successor
       __syncthreads();
       lstore();
@@ -1602,14 +1592,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     };
     gload(a_beg);
     int64_t t0 = a_beg;
-    if constexpr (DENSE != 0) {
-      if (t0 + kTA < a_end) {  // the loop is entered from the peeled tile only
-        step(t0);
-        for (t0 += kTA; t0 + kTA < a_end; t0 += kTA) step(t0);
-      }
-    } else {
-      for (; t0 + kTA < a_end; t0 += kTA) step(t0);
-    }
+    for (; t0 + kTA < a_end; t0 += kTA) step(t0);
     {  // the last tile, whole or not
       __syncthreads();
       lstore();
@@ -2483,7 +2466,7 @@ int superpose_impl(const char *who, const float *d_xyz, int64_t fstride, int64_t
 #define ST_LAUNCH(G, M, V) \
   hipLaunchKernelGGL((k_frame_stats<G, M, V, 1, PL>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, plan, part, ps)
 #define ST_DENSE(M, D) \
-  hipLaunchKernelGGL((k_frame_stats<true, M, false, 1, false, D>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, plan, part, ps, d_dense, dense_pitch)
+  hipLaunchKernelGGL((k_frame_stats<true, M, false, 3, false, D>), grid, dim3(kBlock), 0, s, d_xyz, fstride, n_frames, n_sel, d_sel, d_masses, d_ref, plan, part, ps, d_dense, dense_pitch)
     if (d_dense) {
       if constexpr (!PL) {
         const bool dv = dense_pitch % 4 == 0 && reinterpret_cast<uintptr_t>(d_dense) % 16 == 0;
