@@ -455,6 +455,16 @@ def c5_xtc_mode(eng, a, n_atoms: int = 250_000, nf: int = 2048) -> dict:
             "accumulate_avg_ms": ms / max(1, k), "xtc_write_s_untimed": t_w, "sanity": chk}
 
 
+# HBM bytes per step of the sparse modes, from the L2's read requests by size
+# and WRITE_SIZE (rocprofv3 --pmc passes of tools/sparse_once.py, round 6;
+# profiles/r06_workloads/pmc_sparse_c4.txt) -- a committed measurement, like
+# the headline's traffic, not a counter of this run
+SPARSE_PMC = {
+    "c3_ca_like": {"regathered_read_gb": 48.14, "compacted_read_gb": 26.63, "compacted_written_gb": 2.43},
+    "average_ca_like": {"regathered_read_gb": 96.24, "compacted_read_gb": 31.80, "compacted_written_gb": 2.43},
+}
+
+
 def sparse_selection_modes(eng, a, traj, n_atoms: int, n_total: int) -> dict:
     """RMSF.py's real workload shape: a sparse selection of the system
     (``select_atoms("protein and name CA")``, RMSF.py:77,126 -- 214 of 47,681
@@ -508,6 +518,14 @@ def sparse_selection_modes(eng, a, traj, n_atoms: int, n_total: int) -> dict:
                         "superpose_ms_per_step": s_ms / a.mode_steps, "superpose_launches": ks // a.mode_steps,
                         "accumulate_ms_per_step": a_ms / a.mode_steps, "accumulate_launches": ka // a.mode_steps}
         row["speedup_compacted"] = row["regathered"]["ms_per_step"] / row["compacted"]["ms_per_step"]
+        if name in SPARSE_PMC:  # bytes moved per selected byte, regathered vs compacted
+            pm = dict(SPARSE_PMC[name])
+            sel_gb = B_PER_ATOM_FRAME * n_sel * n_total * sweeps / 1e9
+            pm["selected_gb"] = sel_gb
+            pm["regathered_over_selected"] = pm["regathered_read_gb"] / sel_gb
+            pm["compacted_over_selected"] = (pm["compacted_read_gb"] + pm["compacted_written_gb"]) / sel_gb
+            pm["source"] = "profiles/r06_workloads/pmc_sparse_c4.txt"
+            row["traffic_pmc"] = pm
         row["same_bits"] = bool(torch.equal(res[True], res[False]))
         if not row["same_bits"]:
             raise SystemExit(f"bench: compacted and re-gathered results differ ({name})")
