@@ -175,7 +175,7 @@ def test_exact_aligned_vs_oracle(ci, where):
 
 
 @pytest.mark.parametrize("gathered", [False, True])
-@pytest.mark.parametrize("n_sel", [2, 3, 63, 64, 65, 255, 256, 257, 511, 512, 513, 769])
+@pytest.mark.parametrize("n_sel", [1, 2, 3, 63, 64, 65, 255, 256, 257, 511, 512, 513, 769])
 def test_exact_aligned_block_edges(n_sel, gathered):
     """The serial sums run 256 atoms per block in one wave (wave_seq_sum:
     whole blocks, a two-block loop, a partial last block); selections on
