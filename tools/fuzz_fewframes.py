@@ -4,13 +4,14 @@ item 1; not product code, not a test).
 Where one f32 rounding flip of an aligned coordinate (RMSF.py:99-101 /
 133-135) weighs most -- 2, 4, 8 and 10 frames -- every (selection shape,
 align mode, frame count) group runs N_SEEDS seeded trajectories through
-  * the default frame-parallel path, RMSF(x, align=...).run(): max |dRMSF|
+  * the frame-parallel path, RMSF(x, align=..., exact=False): max |dRMSF|
     and max |daverage| against the oracle's restatement of RMSF.py;
   * exact=True: must equal the restatement bit for bit (mismatch count).
 The oracle runs in a spawned CPU process pool beside the GPU work.  One
 line per group; the table is committed under profiles/.
 
     python tools/fuzz_fewframes.py [n_seeds] [--quick]
+    FUZZ_FRAMES=256,384,512 python tools/fuzz_fewframes.py 20   (other frame counts)
 """
 import os
 import sys
@@ -28,6 +29,8 @@ SHAPES = [("214 of 47,681 (RMSF.py)", 47_681, 214, "ca"),
           ("20,000 of 100,000", 100_000, 20_000, None),
           ("200,000 of 200,000", 200_000, 200_000, None)]
 FRAMES = (2, 4, 8, 10)
+if os.environ.get("FUZZ_FRAMES"):  # e.g. "256,384,512": the bound's side of AUTO_EXACT_FRAMES
+    FRAMES = tuple(int(x) for x in os.environ["FUZZ_FRAMES"].split(","))
 ALIGNS = ("frame0", "average")
 
 
@@ -78,7 +81,7 @@ def main():
                 for s in range(n_seeds):
                     traj, sel, m = case_inputs(na, ns, ms, nf, s)
                     x = torch.tensor(traj, device="cuda")
-                    d = RMSF(x, select=sel, masses=m, align=align).run().results
+                    d = RMSF(x, select=sel, masses=m, align=align, exact=False).run().results
                     e = RMSF(x, select=sel, masses=m, align=align, exact=True).run().results
                     got.append((d.rmsf, d.get("average"), e.rmsf, e.get("average")))
                     del x
