@@ -434,6 +434,21 @@ int rmsf_superpose_sequential(const float *d_xyz, int64_t frame_stride,
                               double mass_total, const double *d_ref,
                               const double *d_refinfo, double *d_xform,
                               void *stream);
+/* The two halves of rmsf_superpose_sequential, same bits:
+ * rmsf_frame_com_sequential writes every frame's mobile COM (RMSF.py:94 /
+ * 127) to d_xform[f * RMSF_XFORM_DOUBLES + 9..11]; it needs no reference, so
+ * it may run on another stream beside rmsf_reference_setup_sequential.
+ * rmsf_superpose_sequential_from_com then runs the InnerProduct and the QCP
+ * from those COMs (it keeps [9..11] and rewrites the rest of the record).  */
+int rmsf_frame_com_sequential(const float *d_xyz, int64_t frame_stride,
+                              int64_t n_frames, int64_t n_sel,
+                              const int32_t *d_sel, const double *d_masses,
+                              double mass_total, double *d_xform, void *stream);
+int rmsf_superpose_sequential_from_com(const float *d_xyz, int64_t frame_stride,
+                                       int64_t n_frames, int64_t n_sel,
+                                       const int32_t *d_sel, const double *d_ref,
+                                       const double *d_refinfo, double *d_xform,
+                                       void *stream);
 /* rmsf_accumulate_sequential: the frames in order for every selected atom
  * (one lane per atom), k = k0 + f, each frame transformed first when d_xform
  * (+ d_refinfo) is given (RMSF.py:99-101 / 133-135, the same f32-faithful

@@ -326,6 +326,20 @@ class Engine:
         call("rmsf_superpose_sequential", xyz_ptr, fstride, n_frames, n_sel, _ptr(sel), _ptr(masses),
              float(mass_total), ref.data_ptr(), refinfo.data_ptr(), xform.data_ptr(), self.stream)
 
+    def frame_com_seq(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, sel, masses,
+                      mass_total: float, xform: torch.Tensor) -> None:
+        """The first half of superpose_seq: every frame's mobile COM into the
+        records' [9..11] (rmsf_frame_com_sequential); no reference needed."""
+        call("rmsf_frame_com_sequential", xyz_ptr, fstride, n_frames, n_sel, _ptr(sel), _ptr(masses),
+             float(mass_total), xform.data_ptr(), self.stream)
+
+    def superpose_seq_from_com(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, sel,
+                               ref: torch.Tensor, refinfo: torch.Tensor, xform: torch.Tensor) -> None:
+        """The second half: InnerProduct + QCP from the COMs in the records
+        (rmsf_superpose_sequential_from_com)."""
+        call("rmsf_superpose_sequential_from_com", xyz_ptr, fstride, n_frames, n_sel, _ptr(sel), ref.data_ptr(),
+             refinfo.data_ptr(), xform.data_ptr(), self.stream)
+
     def accumulate_seq(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, sel, xform, refinfo,
                        mode: int, k0: int, acc0: torch.Tensor, acc1: torch.Tensor | None,
                        work: torch.Tensor | None = None) -> torch.Tensor | None:

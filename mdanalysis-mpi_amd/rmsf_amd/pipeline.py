@@ -510,7 +510,8 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     max_batch = max(1, min(max_batch, max(1, n_local)))
     m_dev = None
     if masses is not None:
-        m_dev = torch.as_tensor(np.ascontiguousarray(masses, dtype=np.float64)).to(eng.device)
+        m_dev = (masses.dev if isinstance(masses, UploadedMasses)
+                 else torch.as_tensor(np.ascontiguousarray(masses, dtype=np.float64)).to(eng.device))
         if m_dev.numel() != n_sel:
             raise ValueError("masses must have one entry per selected atom")
     aligned = align is not None
@@ -673,6 +674,9 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
                           transforms=xf_last, transforms_sweep1=xf_first)
 
 
+EXACT_OVERLAP_MIN_ATOMS = 16384
+
+
 def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, merge_root,
                merge_order: str = "mpi4py", *, align=None, masses=None, ref_frame: int = 0,
                ref_owner: int | None = None, collect_rmsd: bool = False,
@@ -695,19 +699,49 @@ def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, 
     aligned = align is not None
     m_dev, mass_total = None, float(n_sel)
     if masses is not None:
-        m_np = np.ascontiguousarray(masses, dtype=np.float64)
+        m_np = masses.host if isinstance(masses, UploadedMasses) else np.ascontiguousarray(masses, dtype=np.float64)
         if m_np.size != n_sel:
             raise ValueError("masses must have one entry per selected atom")
         # AtomGroup.center_of_mass divides by weights.sum(): numpy's own
         # (pairwise) sum of the f64 masses -- one host scalar
         mass_total = float(m_np.sum())
-        m_dev = torch.as_tensor(m_np).to(eng.device)
+        m_dev = masses.dev if isinstance(masses, UploadedMasses) else torch.as_tensor(m_np).to(eng.device)
     xf = eng.empty(max_batch, RMSF_XFORM_DOUBLES) if aligned else None
     rmsd = eng.empty(n_local) if (aligned and collect_rmsd) else None
     xf_last = eng.empty(n_local, RMSF_XFORM_DOUBLES) if (aligned and collect_transforms) else None
     xf_first = eng.empty(n_local, RMSF_XFORM_DOUBLES) if (collect_transforms and align == "average") else None
 
-    def sweep(mode, acc0, acc1, ref=None, info=None, xf_out=None):
+    # The frames' COM chains need no reference, so one process runs the
+    # reference's chains (rmsf_reference_setup_sequential) on a side stream
+    # beside the first batch's COM chains: 3 serial chain phases per sweep,
+    # not 4.  (With ranks the reference may come from a collective, and a
+    # host source stages its frames on the current stream; those keep one
+    # stream.)  ``pending`` = the side stream's work the first batch's
+    # InnerProduct waits for.
+    # Below EXACT_OVERLAP_MIN_ATOMS a chain phase is microseconds and the
+    # fork/join costs more than it saves.  The side stream is the engine's,
+    # made once (creating a stream per run cost milliseconds).
+    from .sources import DeviceSource
+    overlap = aligned and size == 1 and isinstance(source, DeviceSource) and n_sel >= EXACT_OVERLAP_MIN_ATOMS
+    main = torch.cuda.current_stream(eng.device)
+    side = None
+    if overlap:
+        side = getattr(eng, "_exact_side_stream", None)
+        if side is None:
+            side = eng._exact_side_stream = torch.cuda.Stream(eng.device)
+
+    def on_side(fn):
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            out = fn()
+        ev = torch.cuda.Event()
+        ev.record(side)
+        for t in out if isinstance(out, tuple) else (out,):
+            if isinstance(t, torch.Tensor):
+                t.record_stream(main)
+        return out, ev
+
+    def sweep(mode, acc0, acc1, ref=None, info=None, xf_out=None, pending=None):
         work, k = None, 0
         for b in source.batches(frames, b0, b1, max_batch, eng.stream):  # rows: (frame, atom, xyz)
             if b.pstride:
@@ -716,7 +750,14 @@ def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, 
             if aligned:
                 x = xf[:b.n_frames]
                 with _span(timer, "superpose", b.n_frames * n_sel):
-                    eng.superpose_seq(b.ptr, b.fstride, b.n_frames, n_sel, b.sel, m_dev, mass_total, ref, info, x)
+                    if pending is None:
+                        eng.superpose_seq(b.ptr, b.fstride, b.n_frames, n_sel, b.sel, m_dev, mass_total, ref, info,
+                                          x)
+                    else:
+                        eng.frame_com_seq(b.ptr, b.fstride, b.n_frames, n_sel, b.sel, m_dev, mass_total, x)
+                        main.wait_event(pending)
+                        pending = None
+                        eng.superpose_seq_from_com(b.ptr, b.fstride, b.n_frames, n_sel, b.sel, ref, info, x)
                 if rmsd is not None:
                     rmsd[k:k + b.n_frames].copy_(x[:, 12])
                 if xf_out is not None:
@@ -730,20 +771,34 @@ def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, 
             k += b.n_frames
             b.done()
 
-    ref = info = average = None
+    ref = info = average = pending = None
     if aligned:   # RMSF.py:80-87
-        ref, info = reference_from_frame(eng, source, ref_frame, n_sel, m_dev, ref_owner, mass_total=mass_total)
+        def ref_frame_setup():
+            return reference_from_frame(eng, source, ref_frame, n_sel, m_dev, ref_owner, mass_total=mass_total)
+        if overlap:
+            (ref, info), pending = on_side(ref_frame_setup)
+        else:
+            ref, info = ref_frame_setup()
     if align == "average":
         total = eng.zeros(3 * n_sel)                            # RMSF.py:89, selection rows
         if n_local:
-            sweep(RMSF_MODE_SUM, total, None, ref, info, xf_first)   # RMSF.py:91-103
+            sweep(RMSF_MODE_SUM, total, None, ref, info, xf_first, pending)   # RMSF.py:91-103
+        elif pending is not None:
+            main.wait_event(pending)
+        pending = None
         parallel.allreduce_sum_ordered_(eng, total)             # RMSF.py:110, rank order
-        # RMSF.py:111 + 113-118
-        average, ref, info = eng.reference_setup_seq(n_sel, mass_total, total=total, n_frames=float(n_total),
-                                                     masses=m_dev)
+
+        def ref_avg_setup():                                    # RMSF.py:111 + 113-118
+            return eng.reference_setup_seq(n_sel, mass_total, total=total, n_frames=float(n_total), masses=m_dev)
+        if overlap:
+            (average, ref, info), pending = on_side(ref_avg_setup)
+        else:
+            average, ref, info = ref_avg_setup()
     mean, ss = eng.zeros(3 * n_sel), eng.zeros(3 * n_sel)       # RMSF.py:120-121
     if n_local:
-        sweep(RMSF_MODE_WELFORD, mean, ss, ref, info, xf_last)  # RMSF.py:123-138
+        sweep(RMSF_MODE_WELFORD, mean, ss, ref, info, xf_last, pending)  # RMSF.py:123-138
+    elif pending is not None:
+        main.wait_event(pending)
     if size > 1:                                                # RMSF.py:141-143, comm.reduce's order
         with _span(timer, "merge"):
             mean, ss = parallel.global_chan_exact(eng, mean, ss, [e - s for s, e in blocks], root, merge_order)
@@ -756,6 +811,19 @@ def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, 
                           block=(b0, b1), average=None if average is None else average.view(n_sel, 3), rmsd=rmsd,
                           transforms=xf_last, transforms_sweep1=xf_first,
                           extras={"exact": True, "merge_root": root, "merge_order": merge_order})
+
+
+class UploadedMasses:
+    """Masses already on the device, with their host copy (for the host
+    scalar mass_total): CapturedPipeline uploads them before capture, since
+    a host-to-device copy cannot be recorded into a graph."""
+
+    def __init__(self, masses, device):
+        self.host = np.ascontiguousarray(masses, dtype=np.float64)
+        self.dev = torch.as_tensor(self.host).to(device)
+
+    def __len__(self) -> int:
+        return self.host.size
 
 
 class CapturedPipeline:
@@ -781,6 +849,8 @@ class CapturedPipeline:
         if kw.get("timer") is not None:
             raise ValueError("a KernelTimer cannot be captured")
         dev = eng.device
+        if kw.get("masses") is not None and not isinstance(kw["masses"], UploadedMasses):
+            kw["masses"] = UploadedMasses(kw["masses"], dev)
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # warm-up outside capture (allocator pools, lazy init)

@@ -196,6 +196,50 @@ def test_exact_aligned_block_edges(n_sel, gathered):
             _same(r.average, want["average"], "average")
 
 
+@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("align", ["frame0", "average"])
+def test_exact_aligned_graph_and_split_superpose(align, overlap, monkeypatch):
+    """The exact aligned run recorded as a hipGraph (CapturedPipeline: its
+    reference chains on a side stream beside the frames' COM chains) replays
+    the eager run bit for bit, and the split superposition
+    (rmsf_frame_com_sequential + rmsf_superpose_sequential_from_com) writes
+    the records of rmsf_superpose_sequential bit for bit."""
+    from rmsf_amd._lib import RMSF_XFORM_DOUBLES
+    from rmsf_amd.engine import Engine
+    from rmsf_amd import pipeline as PL
+    from rmsf_amd.pipeline import CapturedPipeline, run_pipeline
+    from rmsf_amd.sources import DeviceSource, FrameList
+    from rmsf_amd.synth import motion_table
+    if overlap:  # the reference's chains on the side stream at this small size too
+        monkeypatch.setattr(PL, "EXACT_OVERLAP_MIN_ATOMS", 0)
+    n, nf = 3000, 37
+    traj = torch.tensor(SY.frames(71, n, 0, nf, motion_table(72, nf)), device="cuda")
+    sel = np.arange(2, n, 5)
+    m = np.random.default_rng(73).uniform(1.0, 16.0, len(sel))
+    eng = Engine()
+    src, fl = DeviceSource(traj, sel), FrameList(nf)
+    eager = run_pipeline(eng, src, fl, align=align, masses=m, exact=True)
+    cap = CapturedPipeline(eng, src, fl, align=align, masses=m, exact=True)
+    for _ in range(2):
+        r = cap.replay()
+        torch.cuda.synchronize()
+        _same(r.rmsf.cpu().numpy(), eager.rmsf.cpu().numpy(), "graph replay")
+    want = O.rmsf_script(traj.cpu().numpy(), sel, m, size=1, align=align)
+    _same(eager.rmsf.cpu().numpy(), want["rmsf"], "eager vs oracle")
+    ns = len(sel)
+    st = eng.sel_tensor(sel)
+    md = torch.tensor(m, device="cuda")
+    mt = float(np.asarray(m, dtype=np.float64).sum())
+    ref, info = eng.reference_setup(ns, frame_ptr=traj.data_ptr(), sel=st, masses=md)
+    a = eng.empty(nf, RMSF_XFORM_DOUBLES)
+    b = eng.empty(nf, RMSF_XFORM_DOUBLES)
+    eng.superpose_seq(traj.data_ptr(), 3 * n, nf, ns, st, md, mt, ref, info, a)
+    eng.frame_com_seq(traj.data_ptr(), 3 * n, nf, ns, st, md, mt, b)
+    eng.superpose_seq_from_com(traj.data_ptr(), 3 * n, nf, ns, st, ref, info, b)
+    torch.cuda.synchronize()
+    _same(b.cpu().numpy(), a.cpu().numpy(), "split superposition")
+
+
 @pytest.mark.parametrize("align", ["frame0", "average"])
 def test_exact_transforms_and_rmsd(align):
     """The per-frame records of the last sweep: rotation, mobile COM and the
