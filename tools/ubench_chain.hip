@@ -80,6 +80,29 @@ __global__ __launch_bounds__(64) void k_lds1(double *out, int reps, double seed)
   }
 }
 
+// 4. terms held by the lanes, read into the chain by v_readlane (two 32-bit
+// halves per f64) -- no LDS round trip
+__global__ __launch_bounds__(64) void k_readlane(double *out, int reps, double seed) {
+  double t[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) t[j] = seed * (threadIdx.x + 64 * j + 1);
+  double s = 0.0;
+  for (int r = 0; r < reps; ++r) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const unsigned long long u = __builtin_bit_cast(unsigned long long, t[j]);
+      const int lo = (int)(u & 0xffffffffu), hi = (int)(u >> 32);
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const unsigned long long v = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane(hi, i) << 32) |
+                                     (unsigned)__builtin_amdgcn_readlane(lo, i);
+        s = s + __builtin_bit_cast(double, v);
+      }
+    }
+  }
+  if (threadIdx.x == 0) out[0] = s;
+}
+
 int main() {
   double *out;
   hipMalloc(&out, 64);
@@ -89,7 +112,7 @@ int main() {
   int dev = 0, clk = 0;
   hipDeviceGetAttribute(&clk, hipDeviceAttributeClockRate, dev);  // kHz
   const int reps = 20000;
-  for (int which = 0; which < 3; ++which) {
+  for (int which = 0; which < 4; ++which) {
     const long adds = (long)reps * (which == 0 ? 64 : 256);
     for (int it = 0; it < 2; ++it) {
       hipEventRecord(a);
@@ -97,8 +120,10 @@ int main() {
         hipLaunchKernelGGL(k_reg, dim3(1), dim3(64), 0, 0, out, reps, 1.0000001);
       else if (which == 1)
         hipLaunchKernelGGL(k_lds, dim3(1), dim3(64), 0, 0, out, reps / 4, 1.0000001);
-      else
+      else if (which == 2)
         hipLaunchKernelGGL(k_lds1, dim3(1), dim3(64), 0, 0, out, reps / 4, 1.0000001);
+      else
+        hipLaunchKernelGGL(k_readlane, dim3(1), dim3(64), 0, 0, out, reps / 4, 1.0000001);
       hipEventRecord(b);
       hipEventSynchronize(b);
       float ms;
@@ -106,7 +131,7 @@ int main() {
       const long n = which == 0 ? adds : adds / 4;
       if (it)
         std::printf("%s: %ld dependent f64 adds in %.3f ms = %.2f ns per add = %.1f cycles at the %.0f MHz peak clock\n",
-                    which == 0 ? "registers" : which == 1 ? "LDS terms" : "LDS terms, lane 0 only", n, ms, ms * 1e6 / n, ms * 1e6 / n * clk / 1e6,
+                    which == 0 ? "registers" : which == 1 ? "LDS terms" : which == 2 ? "LDS terms, lane 0 only" : "readlane terms", n, ms, ms * 1e6 / n, ms * 1e6 / n * clk / 1e6,
                     clk / 1e3);
     }
   }
