@@ -63,6 +63,8 @@ def main():
     n_seeds = int(sys.argv[1]) if len(sys.argv) > 1 and not sys.argv[1].startswith("-") else 50
     quick = "--quick" in sys.argv
     shapes = SHAPES[:2] if quick else SHAPES
+    if os.environ.get("FUZZ_SHAPES"):  # e.g. "2,3": a subset, to split a long sweep over calls
+        shapes = [SHAPES[int(i)] for i in os.environ["FUZZ_SHAPES"].split(",")]
     workers = min(16, len(os.sched_getaffinity(0)))
     pool = mp.get_context("spawn").Pool(workers)
     print(f"# tools/fuzz_fewframes.py: {n_seeds} seeds per group, oracle on {workers} CPU processes", flush=True)
