@@ -472,7 +472,7 @@ def sparse_selection_modes(eng, a, traj, n_atoms: int, n_total: int) -> dict:
     motion), HBM-resident.  Every 10th atom (CA-like) under
     C3's frame-0 alignment and RMSF.py's two sweeps, and the adk density (1 in
     220) under the two sweeps -- each timed with the selected rows compacted
-    by the first pass (the default below COMPACT_MAX_DENSITY) and re-gathered
+    by the first pass (the default below the compaction densities) and re-gathered
     by every pass (compact=False), same bits.  Rates and roofline fractions
     count the SELECTED bytes (12 B per selected atom-frame per sweep); the
     gather reads every 128-B line that holds a selected atom, which at 1 in

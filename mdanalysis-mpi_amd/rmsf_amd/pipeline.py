@@ -204,11 +204,16 @@ class Superposer:
 
 
 # Compaction of gathered selections on the aligned path (round 6): a gathered
-# row read costs every 128-B line holding a selected atom, so below this
-# density the first pass over each frame writes its selected rows out once
+# row read costs every 128-B line holding a selected atom, so below these
+# densities the first pass over each frame writes its selected rows out once
 # (an exact copy) and the later passes read them dense (DESIGN section 4,
-# "Sparse selections")
-COMPACT_MAX_DENSITY = 0.5
+# "Sparse selections").  The copy's writes beside the gathered read cost
+# more than their bytes, so one sweep (frame-0 alignment: one later pass)
+# only gains below ~1 in 4.5 (C3 at 1 in 4 -2 %, 1 in 6 +11 %, 1 in 2 -28 %),
+# RMSF.py's two sweeps (three later passes) at every density up to 1 in 2
+# (+8 % there, +52 % at 1 in 4; profiles/r06_workloads/probe_density.txt).
+COMPACT_MAX_DENSITY = 0.5           # two sweeps (align="average")
+COMPACT_MAX_DENSITY_ONE_SWEEP = 0.2  # one sweep (align="frame0")
 
 
 class _Compactor:
@@ -472,8 +477,9 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     AUTO_EXACT_FRAMES frames (auto_exact), the frame-parallel path otherwise.
     ``compact`` (aligned runs over a gathered selection of HBM-resident
     rows): the first pass writes the selected rows out dense and the later
-    passes read them (_Compactor); None = below COMPACT_MAX_DENSITY selected
-    atoms per frame atom.  Same bits either way."""
+    passes read them (_Compactor); None = below COMPACT_MAX_DENSITY (two
+    sweeps) or COMPACT_MAX_DENSITY_ONE_SWEEP (one) selected atoms per frame
+    atom.  Same bits either way."""
     if align not in ALIGN_MODES:
         raise ValueError(f"align must be one of {ALIGN_MODES}, got {align!r}")
     if exact is None:
@@ -527,7 +533,8 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     gathered = (aligned and not planes and isinstance(source, DeviceSource) and source.layout == "fac"
                 and source.sel_dev is not None and not _scattered_block(frames, b0, b1, max_batch))
     if compact is None:
-        compact = gathered and n_sel <= COMPACT_MAX_DENSITY * source.n_atoms
+        dmax = COMPACT_MAX_DENSITY if align == "average" else COMPACT_MAX_DENSITY_ONE_SWEEP
+        compact = gathered and n_sel <= dmax * source.n_atoms
     cmp = _Compactor(eng, n_sel, n_local, max_batch) if (compact and gathered and n_local) else None
     if cmp is not None and not cmp.usable:
         cmp = None
