@@ -463,8 +463,8 @@ def run_pipeline(eng: Engine, source, frames: FrameList, *, align=None, masses=N
     "slice_mean", "slice_m2").
     ``exact``: RMSF.py with the reference's own arithmetic and summation
     orders -- align=None: RMSF.py:120-146, each rank's block through the
-    sequential Welford (rmsf_welford_sequential), ~1.15x the balanced path's
-    time; aligned: RMSF.py:80-146, every per-frame COM / inner product atom by
+    sequential Welford (rmsf_welford_sequential), ~1.1-1.15x the balanced
+    path's time; aligned: RMSF.py:80-146, every per-frame COM / inner product atom by
     atom (rmsf_superpose_sequential), the sweep-1 sum and Welford frame by
     frame (rmsf_accumulate_sequential), the Allreduce of RMSF.py:110 in rank
     order and the references of RMSF.py:84-85 / 117-118 in order

@@ -97,9 +97,10 @@ class RMSF:
         and, aligned, ``average``, ``rmsd`` and ``transforms``).
         align=None: RMSF.py:120-146, each rank's frames through the
         per-frame Welford of RMSF.py:137-138 in order
-        (rmsf_welford_sequential) -- about 1.15x the default path's time on
-        all-atom rows and about 1.0x over large gathered selections
-        (BENCH_r05 ``modes.c2_exact``; INTEGRATION.md).  Aligned:
+        (rmsf_welford_sequential) -- about 1.1-1.15x the default path's time
+        on all-atom rows, by box, and about 1.0x over large gathered
+        selections (``modes.c2_exact`` of BENCH_r05 and
+        profiles/r06_final_tree; INTEGRATION.md).  Aligned:
         RMSF.py:80-146, the references, every frame's COM and qcprot inner
         product atom by atom, the sweep-1 sum and Welford frame by frame
         (the rmsf_*_sequential kernels) -- each sum an in-order add chain
