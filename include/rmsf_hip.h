@@ -410,14 +410,30 @@ int rmsf_welford_sequential(const float *d_xyz, int64_t frame_stride,
  * divided by avg_divisor = n_frames as they are read and written to
  * d_avg_out when non-NULL; d_sel must be NULL): ref_com, d_ref = x - ref_com,
  * and the refinfo record (ref_com, sum r, G2 of qcprot's loop, mass_total,
- * n_sel).  One workgroup: each sum is one wave's in-order add chain (two
- * chain phases, ~0.6 ms each per 100k atoms).                              */
+ * n_sel).  Each sum is one wave's in-order add chain (two chain phases,
+ * ~0.2 ms each per 100k atoms); below 16,384 atoms one launch, from there
+ * the fill and the centring as grid-wide launches around the chains.      */
 int rmsf_reference_setup_sequential(const float *d_frame, const double *d_avg,
                                     double avg_divisor, int64_t n_sel,
                                     const int32_t *d_sel, const double *d_masses,
                                     double mass_total, double *d_avg_out,
                                     double *d_ref, double *d_refinfo,
                                     void *stream);
+/* The two halves of rmsf_reference_setup_sequential, same bits and the same
+ * arguments: rmsf_reference_centre_sequential writes d_ref (centred) and
+ * d_refinfo[0..2] (ref_com) -- all an InnerProduct needs;
+ * rmsf_reference_sums_sequential writes the rest of the record from the
+ * centred d_ref (sum r, G2, mass_total, n_sel).  Only the QCP reads G2, so the
+ * sums may run on another stream beside rmsf_inner_product_sequential.    */
+int rmsf_reference_centre_sequential(const float *d_frame, const double *d_avg,
+                                     double avg_divisor, int64_t n_sel,
+                                     const int32_t *d_sel, const double *d_masses,
+                                     double mass_total, double *d_avg_out,
+                                     double *d_ref, double *d_refinfo,
+                                     void *stream);
+int rmsf_reference_sums_sequential(int64_t n_sel, double mass_total,
+                                   const double *d_ref, double *d_refinfo,
+                                   void *stream);
 /* rmsf_superpose_sequential: RMSF.py:94-97 / 127-131 + get_rotation_matrix
  * for every frame: mobile COM atom by atom, centred coordinates f64(x) - com,
  * InnerProduct against d_ref (G2 from d_refinfo[6], i.e. a record of
@@ -427,7 +443,7 @@ int rmsf_reference_setup_sequential(const float *d_frame, const double *d_avg,
  * (one wave per frame and sum: A[0..8], G1) and the QCP (one lane per
  * frame); d_xform holds the COM and the sums in between.  Each sum is an
  * in-order add chain over the atoms, so the cost grows with n_sel, not the
- * frames: ~1.2 ms per 100k atoms ("Few frames").       */
+ * frames: ~0.7 ms per 100k atoms ("Few frames").       */
 int rmsf_superpose_sequential(const float *d_xyz, int64_t frame_stride,
                               int64_t n_frames, int64_t n_sel,
                               const int32_t *d_sel, const double *d_masses,
@@ -439,7 +455,11 @@ int rmsf_superpose_sequential(const float *d_xyz, int64_t frame_stride,
  * 127) to d_xform[f * RMSF_XFORM_DOUBLES + 9..11]; it needs no reference, so
  * it may run on another stream beside rmsf_reference_setup_sequential.
  * rmsf_superpose_sequential_from_com then runs the InnerProduct and the QCP
- * from those COMs (it keeps [9..11] and rewrites the rest of the record).  */
+ * from those COMs (it keeps [9..11] and rewrites the rest of the record).
+ * It is in turn rmsf_inner_product_sequential (A[0..8] and G1 into the
+ * record's [0..8] and [13]; needs the centred d_ref only) followed by
+ * rmsf_superpose_sequential_qcp (E0 = (G1 + d_refinfo[6]) * 0.5 and the QCP:
+ * R in [0..8], rmsd in [12], [13..15] zero).                                */
 int rmsf_frame_com_sequential(const float *d_xyz, int64_t frame_stride,
                               int64_t n_frames, int64_t n_sel,
                               const int32_t *d_sel, const double *d_masses,
@@ -449,6 +469,13 @@ int rmsf_superpose_sequential_from_com(const float *d_xyz, int64_t frame_stride,
                                        const int32_t *d_sel, const double *d_ref,
                                        const double *d_refinfo, double *d_xform,
                                        void *stream);
+int rmsf_inner_product_sequential(const float *d_xyz, int64_t frame_stride,
+                                  int64_t n_frames, int64_t n_sel,
+                                  const int32_t *d_sel, const double *d_ref,
+                                  double *d_xform, void *stream);
+int rmsf_superpose_sequential_qcp(int64_t n_frames, int64_t n_sel,
+                                  const double *d_refinfo, double *d_xform,
+                                  void *stream);
 /* rmsf_accumulate_sequential: the frames in order for every selected atom
  * (one lane per atom), k = k0 + f, each frame transformed first when d_xform
  * (+ d_refinfo) is given (RMSF.py:99-101 / 133-135, the same f32-faithful

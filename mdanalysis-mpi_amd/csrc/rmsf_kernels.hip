@@ -682,54 +682,100 @@ __global__ __launch_bounds__(kBlock) void k_welford_seq_atoms(const float *__res
 // wave_seq_sum: s = ((t_0 + t_1) + t_2) + ... over atoms 0..n-1, the
 // reference's order, by one wave.  Its 64 lanes form the terms of a block
 // of kSeqBlk atoms at once (lane i: atoms a0 + i + 64 j -- coalesced loads,
-// elementwise terms with the same roundings as the serial statement), park
-// them in the wave's LDS slice, and one serial chain adds them in order
-// (broadcast reads); the next block's loads are issued before the chain
-// runs.  The adds are the only serial work: ~2 instructions per atom.  (The
-// first round-6 form walked every chain in one lane per frame: ~500 cycles
-// per atom, 24 ms for one sweep's superposition of 100k atoms x 100 frames;
-// profiles/r06_workloads/probe_exact_aligned.txt.)  load(a) issues atom a's
-// loads (a clamped to the last atom: every block issues the same count),
-// term(raw, a) forms t_a.  lds: kSeqBlk doubles private to the wave.
+// elementwise terms with the same roundings as the serial statement) and
+// park them in the wave's LDS slice; then the chain adds them in order, 32
+// at a time: each lane reads two consecutive terms of the group (lane i of
+// every 16-lane row: terms 2i and 2i + 1, one ds_read_b128), and each add is
+// a v_fmac_f64 of the term broadcast from lane j of the row (DPP
+// row_newbcast:j) times 1.0 -- fma(t, 1.0, s) rounds once, exactly as s + t
+// does, so the bits are the serial sum's (every lane carries the same s).
+// The next block's loads are issued before the chain runs.  The adds are the
+// only serial work, at the dependent f64 add's own floor: 2.05 ns per add,
+// against 4.3-4.6 when every lane read each term by a broadcast LDS read
+// (the LDS's return bandwidth bound that form; tools/ubench_chain2.hip,
+// profiles/r06_workloads/chain2.txt).  (The first round-6 form walked every
+// chain in one lane per frame: ~500 cycles per atom, 24 ms for one sweep's
+// superposition of 100k atoms x 100 frames; a form with four frames' chains
+// per wave, one per row, and the terms in registers lost to load latency:
+// profiles/r06_workloads/probe_exact_aligned.txt.)  Atoms past n enter as
+// +0.0: s is never -0.0 (it starts at +0.0, and x + (-x) is +0.0), so
+// s + 0.0 == s bit for bit and a ragged last group needs no branch.
+// load(a) issues atom a's loads (a clamped to the last atom: every block
+// issues the same count), term(raw, a) forms t_a.  lds: kSeqBlk doubles
+// private to the wave.
 constexpr int kSeqK = 16;             // atoms per lane per block (4 / 8 / 16 measured: 16 ~7 % faster)
 constexpr int kSeqBlk = 64 * kSeqK;   // atoms per block
+// s += the group's 32 terms (lane 0's pair first), in order.  The opening
+// s_nop 1: a DPP read of a VGPR needs 2 wait states after a VALU write, and
+// hipcc pads nothing inside an asm string.  The adds follow each other with
+// none: back to back, each reads the accumulator the previous one wrote
+// (measured: the sum of 2e5 chained adds bit-equal to the plain chain's;
+// 2.05 ns per add, against 3.6 with an s_nop 0 between; ubench_chain2 V5).
+#define RMSF_ROW_FMAC(J)                                                \
+  "v_fmac_f64_dpp %0, %1, %3 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_fmac_f64_dpp %0, %2, %3 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"
+__device__ __forceinline__ double row_add32(double s, const double2 &u, double one) {
+  asm("s_nop 1\n\t" RMSF_ROW_FMAC(0) RMSF_ROW_FMAC(1) RMSF_ROW_FMAC(2) RMSF_ROW_FMAC(3) RMSF_ROW_FMAC(4)
+          RMSF_ROW_FMAC(5) RMSF_ROW_FMAC(6) RMSF_ROW_FMAC(7) RMSF_ROW_FMAC(8) RMSF_ROW_FMAC(9) RMSF_ROW_FMAC(10)
+              RMSF_ROW_FMAC(11) RMSF_ROW_FMAC(12) RMSF_ROW_FMAC(13) RMSF_ROW_FMAC(14) RMSF_ROW_FMAC(15)
+      : "+v"(s)
+      : "v"(u.x), "v"(u.y), "v"(one));
+  return s;
+}
+#undef RMSF_ROW_FMAC
 template <class Load, class Term>
 __device__ __forceinline__ double wave_seq_sum(int64_t n, double *lds, Load load, Term term) {
   using Raw = decltype(load(int64_t(0)));
   const int lane = threadIdx.x & 63;
+  const double one = 1.0;
+  // lane i of a row reads the pair 2i, 2i + 1 of each 32-term group
+  const double2 *pair = reinterpret_cast<const double2 *>(lds) + (lane & 15);
   Raw va[kSeqK], vb[kSeqK];
   double s = 0.0;
+  // whole blocks: unclamped indices, so one base and constant offsets per
+  // lane address the block (no 64-bit index arithmetic per load)
   auto fill = [&](Raw(&v)[kSeqK], int64_t a0) {
+    const int64_t b = a0 + lane;
+    if (a0 + kSeqBlk <= n) {
 #pragma unroll
-    for (int j = 0; j < kSeqK; ++j) v[j] = load(min(a0 + lane + 64 * j, n - 1));
+      for (int j = 0; j < kSeqK; ++j) v[j] = load(b + 64 * j);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kSeqK; ++j) v[j] = load(min(b + 64 * j, n - 1));
+    }
     __builtin_amdgcn_sched_barrier(0);  // issued before the chain below
   };
   auto run = [&](const Raw(&v)[kSeqK], int64_t a0) {
+    const int64_t b = a0 + lane;
+    if (a0 + kSeqBlk <= n) {
 #pragma unroll
-    for (int j = 0; j < kSeqK; ++j) lds[lane + 64 * j] = term(v[j], a0 + lane + 64 * j);
+      for (int j = 0; j < kSeqK; ++j) lds[lane + 64 * j] = term(v[j], b + 64 * j);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kSeqK; ++j) lds[lane + 64 * j] = b + 64 * j < n ? term(v[j], b + 64 * j) : 0.0;
+    }
     __builtin_amdgcn_wave_barrier();  // one wave: its LDS operations complete in order
     const int cnt = (int)min((int64_t)kSeqBlk, n - a0);
-    if (cnt == kSeqBlk) {  // the next 16 terms' reads in flight while 16 are added
-      constexpr int G = 16;
-      double ta[G], tb[G];
-      auto rd = [&](double(&t)[G], int i0) {
+    constexpr int NG = kSeqBlk / 32;
+    if (cnt == kSeqBlk) {  // two groups' reads in flight while one is added
+      double2 u[3];
+      u[0] = pair[0];
+      u[1] = pair[16];
 #pragma unroll
-        for (int k = 0; k < G; ++k) t[k] = lds[i0 + k];
-      };
-      auto add = [&](const double(&t)[G]) {
-#pragma unroll
-        for (int k = 0; k < G; ++k) s = s + t[k];
-      };
-      rd(ta, 0);
-#pragma unroll
-      for (int i0 = 0; i0 < kSeqBlk; i0 += 2 * G) {
-        rd(tb, i0 + G);
-        add(ta);
-        if (i0 + 2 * G < kSeqBlk) rd(ta, i0 + 2 * G);
-        add(tb);
+      for (int g = 0; g < NG; ++g) {
+        if (g + 2 < NG) u[(g + 2) % 3] = pair[16 * (g + 2)];
+        __builtin_amdgcn_sched_barrier(0);
+        s = row_add32(s, u[g % 3], one);
+        __builtin_amdgcn_sched_barrier(0);
       }
-    } else {
-      for (int i = 0; i < cnt; ++i) s = s + lds[i];
+    } else {  // the ragged last block: its groups, the last one padded with +0.0
+      const int ng = (cnt + 31) / 32;
+      double2 u = pair[0];
+      for (int g = 0; g < ng; ++g) {
+        const double2 w = u;
+        if (g + 1 < ng) u = pair[16 * (g + 1)];
+        s = row_add32(s, w, one);
+      }
     }
     __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next block
   };
@@ -761,16 +807,53 @@ struct SeqD3 {
   double x, y, z;
 };
 
-// k_ref_seq: the centred reference, one workgroup of four waves.
+// The centred reference of exact=True (RMSF.py:84-85 / 111 + 117-118) and
+// its record, in parts:
 //   1. x = frame[sel[a]] (f32 -> f64) or avg[a] / div (RMSF.py:111, also to
-//      avg_out) into ref, all threads;
+//      avg_out) into ref;
 //   2. com_c = (sum_a x_ac m_a, atom by atom) / mass_total (RMSF.py:84/117),
-//      wave c's chain;
-//   3. ref = x - com in place (RMSF.py:85/118), all threads;
-//   4. the record [0..15]: com, sum r (waves 0-2), G2 = sum_a ((r0 r0 + r1
+//      wave c's chain, to the record's [0..2];
+//   3. ref = x - com in place (RMSF.py:85/118);
+//   4. the rest of the record: sum r (waves 0-2), G2 = sum_a ((r0 r0 + r1
 //      r1) + r2 r2) in qcprot's per-atom order (wave 3; the G2 of every
 //      InnerProduct call against this reference), mass_total, n_sel.
-template <bool FROM_F32, bool GATHER, bool MASSES>
+// k_ref_seq runs them in one workgroup of four waves (PART kRefAll), or
+// 1-3 (kRefCentre), 2 alone (kRefCom) or 4 alone (kRefSums).  From
+// kRefGridMin atoms, 1 and 3 run as grid-wide launches (k_ref_fill,
+// k_ref_centre_grid) instead: one workgroup streamed them at one CU's rate,
+// ~4 ms of a 1M-atom setup's 8.5 (profiles/r06_workloads/exact_chain_dpp.txt).
+constexpr int kRefAll = 0, kRefCentre = 1, kRefCom = 2, kRefSums = 3;
+constexpr int64_t kRefGridMin = 16384;
+template <bool FROM_F32, bool GATHER>
+__device__ __forceinline__ void ref_fill_atom(int64_t a, const float *__restrict__ frame,
+                                              const double *__restrict__ avg, double div,
+                                              const int32_t *__restrict__ sel, double *__restrict__ avg_out,
+                                              double *__restrict__ ref) {
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    double x;
+    if (FROM_F32) {
+      x = (double)frame[3 * (GATHER ? (int64_t)sel[a] : a) + c];
+    } else {
+      x = avg[3 * a + c] / div;
+      if (avg_out) avg_out[3 * a + c] = x;
+    }
+    ref[3 * a + c] = x;
+  }
+}
+template <bool FROM_F32, bool GATHER>
+__global__ __launch_bounds__(kBlock) void k_ref_fill(const float *__restrict__ frame, const double *__restrict__ avg,
+                                                     double div, int64_t n_sel, const int32_t *__restrict__ sel,
+                                                     double *__restrict__ avg_out, double *__restrict__ ref) {
+  const int64_t a = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (a < n_sel) ref_fill_atom<FROM_F32, GATHER>(a, frame, avg, div, sel, avg_out, ref);
+}
+__global__ __launch_bounds__(kBlock) void k_ref_centre_grid(int64_t n_coord, const double *__restrict__ info,
+                                                            double *__restrict__ ref) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n_coord) ref[i] = ref[i] - info[i % 3];
+}
+template <bool FROM_F32, bool GATHER, bool MASSES, int PART>
 __global__ __launch_bounds__(kBlock) void k_ref_seq(const float *__restrict__ frame, const double *__restrict__ avg,
                                                     double div, int64_t n_sel, const int32_t *__restrict__ sel,
                                                     const double *__restrict__ masses, double mass_total,
@@ -780,35 +863,30 @@ __global__ __launch_bounds__(kBlock) void k_ref_seq(const float *__restrict__ fr
   __shared__ double slice[kBlock / 64][kSeqBlk];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool lead = (threadIdx.x & 63) == 0;
-  for (int64_t a = threadIdx.x; a < n_sel; a += kBlock) {
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      double x;
-      if (FROM_F32) {
-        x = (double)frame[3 * (GATHER ? (int64_t)sel[a] : a) + c];
-      } else {
-        x = avg[3 * a + c] / div;
-        if (avg_out) avg_out[3 * a + c] = x;
-      }
-      ref[3 * a + c] = x;
+  if (PART == kRefAll || PART == kRefCentre) {
+    for (int64_t a = threadIdx.x; a < n_sel; a += kBlock)
+      ref_fill_atom<FROM_F32, GATHER>(a, frame, avg, div, sel, avg_out, ref);
+    __syncthreads();
+  }
+  if (PART != kRefSums) {
+    if (w < 3) {  // three independent chains, one per axis
+      const int c = w;
+      const double s = wave_seq_sum(
+          n_sel, slice[w], [&](int64_t a) { return SeqD1D{ref[3 * a + c], MASSES ? masses[a] : 1.0}; },
+          [&](const SeqD1D &v, int64_t) { return v.x * v.d; });
+      if (lead) info[c] = com[c] = s / mass_total;
     }
+    if (PART == kRefCom) return;
+    __syncthreads();
+    const double c0 = com[0], c1 = com[1], c2 = com[2];
+    for (int64_t a = threadIdx.x; a < n_sel; a += kBlock) {
+      ref[3 * a] = ref[3 * a] - c0;
+      ref[3 * a + 1] = ref[3 * a + 1] - c1;
+      ref[3 * a + 2] = ref[3 * a + 2] - c2;
+    }
+    if (PART == kRefCentre) return;
+    __syncthreads();
   }
-  __syncthreads();
-  if (w < 3) {  // three independent chains, one per axis
-    const int c = w;
-    const double s = wave_seq_sum(
-        n_sel, slice[w], [&](int64_t a) { return SeqD1D{ref[3 * a + c], MASSES ? masses[a] : 1.0}; },
-        [&](const SeqD1D &v, int64_t) { return v.x * v.d; });
-    if (lead) com[c] = s / mass_total;
-  }
-  __syncthreads();
-  const double c0 = com[0], c1 = com[1], c2 = com[2];
-  for (int64_t a = threadIdx.x; a < n_sel; a += kBlock) {
-    ref[3 * a] = ref[3 * a] - c0;
-    ref[3 * a + 1] = ref[3 * a + 1] - c1;
-    ref[3 * a + 2] = ref[3 * a + 2] - c2;
-  }
-  __syncthreads();
   if (w < 3) {  // the sums of r, in order
     const int c = w;
     const double s = wave_seq_sum(
@@ -819,9 +897,6 @@ __global__ __launch_bounds__(kBlock) void k_ref_seq(const float *__restrict__ fr
         n_sel, slice[w], [&](int64_t a) { return SeqD3{ref[3 * a], ref[3 * a + 1], ref[3 * a + 2]}; },
         [&](const SeqD3 &r, int64_t) { return r.x * r.x + r.y * r.y + r.z * r.z; });
     if (lead) {
-      info[0] = c0;
-      info[1] = c1;
-      info[2] = c2;
       info[6] = g;
       info[7] = mass_total;
       info[8] = (double)n_sel;
@@ -3201,18 +3276,22 @@ RMSF_EXPORT int rmsf_welford_sequential(const float *d_xyz, int64_t fstride, int
   return after_launch("k_welford_seq");
 }
 
-RMSF_EXPORT int rmsf_reference_setup_sequential(const float *d_frame, const double *d_avg, double avg_divisor,
-                                                int64_t n_sel, const int32_t *d_sel, const double *d_masses,
-                                                double mass_total, double *d_avg_out, double *d_ref,
-                                                double *d_refinfo, void *stream) {
-  if ((d_frame == nullptr) == (d_avg == nullptr))
-    return fail(RMSF_EINVAL, "rmsf_reference_setup_sequential: exactly one of d_frame / d_avg");
-  if (n_sel < 1 || !d_ref || !d_refinfo || (d_avg && !(avg_divisor > 0.0)) || (d_avg && d_sel))
-    return fail(RMSF_EINVAL, "rmsf_reference_setup_sequential: bad arguments");
+}  // extern "C"
+
+namespace {
+bool ref_seq_args_ok(const float *d_frame, const double *d_avg, double avg_divisor, int64_t n_sel,
+                     const int32_t *d_sel, const double *d_ref, const double *d_refinfo) {
+  return (d_frame == nullptr) != (d_avg == nullptr) && n_sel >= 1 && d_ref && d_refinfo &&
+         !(d_avg && !(avg_divisor > 0.0)) && !(d_avg && d_sel);
+}
+// one k_ref_seq launch of part PART
+template <int PART>
+void ref_seq_launch(const float *d_frame, const double *d_avg, double div, int64_t n_sel, const int32_t *d_sel,
+                    const double *d_masses, double mass_total, double *d_avg_out, double *d_ref, double *d_refinfo,
+                    hipStream_t s) {
   const bool g = d_sel != nullptr, m = d_masses != nullptr;
-  hipStream_t s = S(stream);
-#define SEQREF(F, G, M)                                                                                     \
-  hipLaunchKernelGGL((k_ref_seq<F, G, M>), dim3(1), dim3(kBlock), 0, s, d_frame, d_avg, avg_divisor, n_sel, d_sel, \
+#define SEQREF(F, G, M)                                                                                          \
+  hipLaunchKernelGGL((k_ref_seq<F, G, M, PART>), dim3(1), dim3(kBlock), 0, s, d_frame, d_avg, div, n_sel, d_sel, \
                      d_masses, mass_total, d_avg_out, d_ref, d_refinfo)
   if (d_frame) {
     if (g && m) SEQREF(true, true, true);
@@ -3224,7 +3303,69 @@ RMSF_EXPORT int rmsf_reference_setup_sequential(const float *d_frame, const doub
     else SEQREF(false, false, false);
   }
 #undef SEQREF
+}
+// RMSF.py:84-85 / 111 + 117-118: ref centred, the record's [0..2]
+int ref_centre_seq(const float *d_frame, const double *d_avg, double div, int64_t n_sel, const int32_t *d_sel,
+                   const double *d_masses, double mass_total, double *d_avg_out, double *d_ref, double *d_refinfo,
+                   hipStream_t s) {
+  if (n_sel < kRefGridMin) {
+    ref_seq_launch<kRefCentre>(d_frame, d_avg, div, n_sel, d_sel, d_masses, mass_total, d_avg_out, d_ref, d_refinfo,
+                               s);
+    return after_launch("k_ref_seq");
+  }
+  if (d_frame && d_sel)
+    hipLaunchKernelGGL((k_ref_fill<true, true>), dim3(grid1(n_sel)), dim3(kBlock), 0, s, d_frame, d_avg, div, n_sel,
+                       d_sel, d_avg_out, d_ref);
+  else if (d_frame)
+    hipLaunchKernelGGL((k_ref_fill<true, false>), dim3(grid1(n_sel)), dim3(kBlock), 0, s, d_frame, d_avg, div, n_sel,
+                       d_sel, d_avg_out, d_ref);
+  else
+    hipLaunchKernelGGL((k_ref_fill<false, false>), dim3(grid1(n_sel)), dim3(kBlock), 0, s, d_frame, d_avg, div,
+                       n_sel, d_sel, d_avg_out, d_ref);
+  if (int rc = after_launch("k_ref_fill")) return rc;
+  ref_seq_launch<kRefCom>(d_frame, d_avg, div, n_sel, d_sel, d_masses, mass_total, d_avg_out, d_ref, d_refinfo, s);
+  if (int rc = after_launch("k_ref_seq")) return rc;
+  hipLaunchKernelGGL(k_ref_centre_grid, dim3(grid1(3 * n_sel)), dim3(kBlock), 0, s, 3 * n_sel, d_refinfo, d_ref);
+  return after_launch("k_ref_centre_grid");
+}
+}  // namespace
+
+extern "C" {
+
+RMSF_EXPORT int rmsf_reference_centre_sequential(const float *d_frame, const double *d_avg, double avg_divisor,
+                                                 int64_t n_sel, const int32_t *d_sel, const double *d_masses,
+                                                 double mass_total, double *d_avg_out, double *d_ref,
+                                                 double *d_refinfo, void *stream) {
+  if (!ref_seq_args_ok(d_frame, d_avg, avg_divisor, n_sel, d_sel, d_ref, d_refinfo))
+    return fail(RMSF_EINVAL, "rmsf_reference_centre_sequential: bad arguments (exactly one of d_frame / d_avg)");
+  return ref_centre_seq(d_frame, d_avg, avg_divisor, n_sel, d_sel, d_masses, mass_total, d_avg_out, d_ref, d_refinfo,
+                        S(stream));
+}
+
+RMSF_EXPORT int rmsf_reference_sums_sequential(int64_t n_sel, double mass_total, const double *d_ref,
+                                               double *d_refinfo, void *stream) {
+  if (n_sel < 1 || !d_ref || !d_refinfo) return fail(RMSF_EINVAL, "rmsf_reference_sums_sequential: bad arguments");
+  ref_seq_launch<kRefSums>(nullptr, nullptr, 1.0, n_sel, nullptr, nullptr, mass_total, nullptr,
+                           const_cast<double *>(d_ref), d_refinfo, S(stream));
   return after_launch("k_ref_seq");
+}
+
+RMSF_EXPORT int rmsf_reference_setup_sequential(const float *d_frame, const double *d_avg, double avg_divisor,
+                                                int64_t n_sel, const int32_t *d_sel, const double *d_masses,
+                                                double mass_total, double *d_avg_out, double *d_ref,
+                                                double *d_refinfo, void *stream) {
+  if (!ref_seq_args_ok(d_frame, d_avg, avg_divisor, n_sel, d_sel, d_ref, d_refinfo))
+    return fail(RMSF_EINVAL, "rmsf_reference_setup_sequential: bad arguments (exactly one of d_frame / d_avg)");
+  hipStream_t s = S(stream);
+  if (n_sel < kRefGridMin) {  // one launch
+    ref_seq_launch<kRefAll>(d_frame, d_avg, avg_divisor, n_sel, d_sel, d_masses, mass_total, d_avg_out, d_ref,
+                            d_refinfo, s);
+    return after_launch("k_ref_seq");
+  }
+  if (int rc = ref_centre_seq(d_frame, d_avg, avg_divisor, n_sel, d_sel, d_masses, mass_total, d_avg_out, d_ref,
+                              d_refinfo, s))
+    return rc;
+  return rmsf_reference_sums_sequential(n_sel, mass_total, d_ref, d_refinfo, stream);
 }
 
 RMSF_EXPORT int rmsf_frame_com_sequential(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
@@ -3246,22 +3387,39 @@ RMSF_EXPORT int rmsf_frame_com_sequential(const float *d_xyz, int64_t fstride, i
   return after_launch("k_seq_com");
 }
 
-RMSF_EXPORT int rmsf_superpose_sequential_from_com(const float *d_xyz, int64_t fstride, int64_t n_frames,
-                                                   int64_t n_sel, const int32_t *d_sel, const double *d_ref,
-                                                   const double *d_refinfo, double *d_xform, void *stream) {
-  if (!d_xyz || !d_ref || !d_refinfo || !d_xform || n_sel < 1 || n_frames < 0 || fstride < (d_sel ? 3 : 3 * n_sel))
-    return fail(RMSF_EINVAL, "rmsf_superpose_sequential_from_com: bad arguments");
+RMSF_EXPORT int rmsf_inner_product_sequential(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,
+                                              const int32_t *d_sel, const double *d_ref, double *d_xform,
+                                              void *stream) {
+  if (!d_xyz || !d_ref || !d_xform || n_sel < 1 || n_frames < 0 || fstride < (d_sel ? 3 : 3 * n_sel))
+    return fail(RMSF_EINVAL, "rmsf_inner_product_sequential: bad arguments");
   if (n_frames == 0) return RMSF_OK;
-  const unsigned fb = (unsigned)((n_frames + 63) / 64);
   hipStream_t s = S(stream);
   const dim3 gi((unsigned)n_frames, 10);
   if (d_sel)
     hipLaunchKernelGGL((k_seq_ip<true>), gi, dim3(64), 0, s, d_xyz, fstride, n_sel, d_sel, d_ref, d_xform);
   else
     hipLaunchKernelGGL((k_seq_ip<false>), gi, dim3(64), 0, s, d_xyz, fstride, n_sel, d_sel, d_ref, d_xform);
-  if (int rc = after_launch("k_seq_ip")) return rc;
-  hipLaunchKernelGGL(k_seq_qcp, dim3(fb), dim3(64), 0, s, n_frames, n_sel, d_refinfo, d_xform);
+  return after_launch("k_seq_ip");
+}
+
+RMSF_EXPORT int rmsf_superpose_sequential_qcp(int64_t n_frames, int64_t n_sel, const double *d_refinfo,
+                                              double *d_xform, void *stream) {
+  if (!d_refinfo || !d_xform || n_sel < 1 || n_frames < 0)
+    return fail(RMSF_EINVAL, "rmsf_superpose_sequential_qcp: bad arguments");
+  if (n_frames == 0) return RMSF_OK;
+  const unsigned fb = (unsigned)((n_frames + 63) / 64);
+  hipLaunchKernelGGL(k_seq_qcp, dim3(fb), dim3(64), 0, S(stream), n_frames, n_sel, d_refinfo, d_xform);
   return after_launch("k_seq_qcp");
+}
+
+RMSF_EXPORT int rmsf_superpose_sequential_from_com(const float *d_xyz, int64_t fstride, int64_t n_frames,
+                                                   int64_t n_sel, const int32_t *d_sel, const double *d_ref,
+                                                   const double *d_refinfo, double *d_xform, void *stream) {
+  if (!d_xyz || !d_ref || !d_refinfo || !d_xform || n_sel < 1 || n_frames < 0 || fstride < (d_sel ? 3 : 3 * n_sel))
+    return fail(RMSF_EINVAL, "rmsf_superpose_sequential_from_com: bad arguments");
+  if (int rc = rmsf_inner_product_sequential(d_xyz, fstride, n_frames, n_sel, d_sel, d_ref, d_xform, stream))
+    return rc;
+  return rmsf_superpose_sequential_qcp(n_frames, n_sel, d_refinfo, d_xform, stream);
 }
 
 RMSF_EXPORT int rmsf_superpose_sequential(const float *d_xyz, int64_t fstride, int64_t n_frames, int64_t n_sel,

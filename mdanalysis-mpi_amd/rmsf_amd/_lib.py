@@ -79,7 +79,11 @@ SIGNATURES = {
     "rmsf_finalize": (c_int, [P, c_int64, c_int64, P, P]),
     "rmsf_reference_setup_sequential": (c_int, [P, P, c_double, c_int64, P, P, c_double, P, P, P, P]),
     "rmsf_superpose_sequential": (c_int, [P, c_int64, c_int64, c_int64, P, P, c_double, P, P, P, P]),
+    "rmsf_reference_centre_sequential": (c_int, [P, P, c_double, c_int64, P, P, c_double, P, P, P, P]),
+    "rmsf_reference_sums_sequential": (c_int, [c_int64, c_double, P, P, P]),
     "rmsf_frame_com_sequential": (c_int, [P, c_int64, c_int64, c_int64, P, P, c_double, P, P]),
+    "rmsf_inner_product_sequential": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, P]),
+    "rmsf_superpose_sequential_qcp": (c_int, [c_int64, c_int64, P, P, P]),
     "rmsf_superpose_sequential_from_com": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, P, P]),
     "rmsf_accumulate_sequential": (c_int, [P, c_int64, c_int64, c_int64, P, P, P, c_int, c_int64, P, P, P, c_size_t,
                                            P]),

@@ -306,17 +306,27 @@ class Engine:
     # -- exact=True on the aligned path (the reference's summation orders) ---
     def reference_setup_seq(self, n_sel: int, mass_total: float, *, frame_ptr: int | None = None,
                             sel: torch.Tensor | None = None, total: torch.Tensor | None = None,
-                            n_frames: float = 1.0, masses: torch.Tensor | None = None):
+                            n_frames: float = 1.0, masses: torch.Tensor | None = None, after_centre=None):
         """RMSF.py:84-85 (``frame_ptr``) or RMSF.py:111 + 117-118 (``total``,
         the all-reduced sweep-1 sums, divided by ``n_frames`` as read) with
         the reference's own summation order (rmsf_reference_setup_sequential).
-        Returns (average or None, ref, info)."""
+        ``after_centre``: called between the two halves (the centred
+        reference, then the record's sums; rmsf_reference_centre_sequential /
+        rmsf_reference_sums_sequential, same bits) -- e.g. to record an event
+        an InnerProduct on another stream waits for.  Returns (average or
+        None, ref, info)."""
         ref = self.empty(n_sel, 3)
         info = self.empty(RMSF_REFINFO_DOUBLES)
         avg = self.empty(3 * n_sel) if total is not None else None
-        call("rmsf_reference_setup_sequential", frame_ptr, _ptr(total), float(n_frames), n_sel,
-             _ptr(sel if frame_ptr else None), _ptr(masses), float(mass_total), _ptr(avg), ref.data_ptr(),
-             info.data_ptr(), self.stream)
+        args = (frame_ptr, _ptr(total), float(n_frames), n_sel, _ptr(sel if frame_ptr else None), _ptr(masses),
+                float(mass_total), _ptr(avg), ref.data_ptr(), info.data_ptr(), self.stream)
+        if after_centre is None:
+            call("rmsf_reference_setup_sequential", *args)
+        else:
+            call("rmsf_reference_centre_sequential", *args)
+            after_centre()
+            call("rmsf_reference_sums_sequential", n_sel, float(mass_total), ref.data_ptr(), info.data_ptr(),
+                 self.stream)
         return avg, ref, info
 
     def superpose_seq(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, sel, masses,
@@ -339,6 +349,19 @@ class Engine:
         (rmsf_superpose_sequential_from_com)."""
         call("rmsf_superpose_sequential_from_com", xyz_ptr, fstride, n_frames, n_sel, _ptr(sel), ref.data_ptr(),
              refinfo.data_ptr(), xform.data_ptr(), self.stream)
+
+    def inner_product_seq(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, sel, ref: torch.Tensor,
+                          xform: torch.Tensor) -> None:
+        """superpose_seq_from_com's first part: qcprot's InnerProduct per
+        frame against the centred reference (rmsf_inner_product_sequential;
+        the record's sums need not be ready)."""
+        call("rmsf_inner_product_sequential", xyz_ptr, fstride, n_frames, n_sel, _ptr(sel), ref.data_ptr(),
+             xform.data_ptr(), self.stream)
+
+    def superpose_seq_qcp(self, n_frames: int, n_sel: int, refinfo: torch.Tensor, xform: torch.Tensor) -> None:
+        """Its second part: E0 with the record's G2, and the QCP
+        (rmsf_superpose_sequential_qcp)."""
+        call("rmsf_superpose_sequential_qcp", n_frames, n_sel, refinfo.data_ptr(), xform.data_ptr(), self.stream)
 
     def accumulate_seq(self, xyz_ptr: int, fstride: int, n_frames: int, n_sel: int, sel, xform, refinfo,
                        mode: int, k0: int, acc0: torch.Tensor, acc1: torch.Tensor | None,

@@ -311,7 +311,7 @@ def _scattered_block(frames: FrameList, b0: int, b1: int, max_batch: int) -> boo
 
 
 def reference_from_frame(eng: Engine, source, frame: int, n_sel: int, masses, owner: int | None = None,
-                         mass_total: float | None = None):
+                         mass_total: float | None = None, after_centre=None):
     """RMSF.py:80-87: centred f64 reference of trajectory frame ``frame``.
 
     RMSF.py has every rank re-read that frame from disk.  Here, if every rank
@@ -319,10 +319,12 @@ def reference_from_frame(eng: Engine, source, frame: int, n_sel: int, masses, ow
     otherwise (sharded HBM-resident trajectories) the lowest rank holding it
     computes it and broadcasts 3*n_sel + 16 doubles.  ``mass_total`` given:
     the reference's own summation order (exact=True,
-    rmsf_reference_setup_sequential; numpy's masses.sum())."""
+    rmsf_reference_setup_sequential; numpy's masses.sum()); ``after_centre``
+    as Engine.reference_setup_seq takes it."""
     if mass_total is not None:
         def setup(b):
-            _, r, i = eng.reference_setup_seq(n_sel, mass_total, frame_ptr=b.ptr, sel=b.sel, masses=masses)
+            _, r, i = eng.reference_setup_seq(n_sel, mass_total, frame_ptr=b.ptr, sel=b.sel, masses=masses,
+                                              after_centre=after_centre)
             return r, i
     else:
         def setup(b):
@@ -720,11 +722,13 @@ def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, 
 
     # The frames' COM chains need no reference, so one process runs the
     # reference's chains (rmsf_reference_setup_sequential) on a side stream
-    # beside the first batch's COM chains: 3 serial chain phases per sweep,
-    # not 4.  (With ranks the reference may come from a collective, and a
-    # host source stages its frames on the current stream; those keep one
-    # stream.)  ``pending`` = the side stream's work the first batch's
-    # InnerProduct waits for.
+    # beside the first batch's COM chains, and the reference's sums beside
+    # its InnerProduct (which needs only the centred reference; the QCP needs
+    # the sums' G2): 2 serial chain phases per sweep, not 4.  (With ranks the
+    # reference may come from a collective, and a host source stages its
+    # frames on the current stream; those keep one stream.)  ``pending`` =
+    # the side stream's two events (reference centred, record complete) the
+    # first batch's InnerProduct and QCP wait for.
     # Below EXACT_OVERLAP_MIN_ATOMS a chain phase is microseconds and the
     # fork/join costs more than it saves.  The side stream is the engine's,
     # made once (creating a stream per run cost milliseconds).
@@ -739,14 +743,15 @@ def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, 
 
     def on_side(fn):
         side.wait_stream(main)
+        centred = torch.cuda.Event()
         with torch.cuda.stream(side):
-            out = fn()
-        ev = torch.cuda.Event()
-        ev.record(side)
+            out = fn(lambda: centred.record(side))
+        done = torch.cuda.Event()
+        done.record(side)
         for t in out if isinstance(out, tuple) else (out,):
             if isinstance(t, torch.Tensor):
                 t.record_stream(main)
-        return out, ev
+        return out, (centred, done)
 
     def sweep(mode, acc0, acc1, ref=None, info=None, xf_out=None, pending=None):
         work, k = None, 0
@@ -762,9 +767,11 @@ def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, 
                                           x)
                     else:
                         eng.frame_com_seq(b.ptr, b.fstride, b.n_frames, n_sel, b.sel, m_dev, mass_total, x)
-                        main.wait_event(pending)
+                        main.wait_event(pending[0])
+                        eng.inner_product_seq(b.ptr, b.fstride, b.n_frames, n_sel, b.sel, ref, x)
+                        main.wait_event(pending[1])
                         pending = None
-                        eng.superpose_seq_from_com(b.ptr, b.fstride, b.n_frames, n_sel, b.sel, ref, info, x)
+                        eng.superpose_seq_qcp(b.n_frames, n_sel, info, x)
                 if rmsd is not None:
                     rmsd[k:k + b.n_frames].copy_(x[:, 12])
                 if xf_out is not None:
@@ -780,8 +787,9 @@ def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, 
 
     ref = info = average = pending = None
     if aligned:   # RMSF.py:80-87
-        def ref_frame_setup():
-            return reference_from_frame(eng, source, ref_frame, n_sel, m_dev, ref_owner, mass_total=mass_total)
+        def ref_frame_setup(after_centre=None):
+            return reference_from_frame(eng, source, ref_frame, n_sel, m_dev, ref_owner, mass_total=mass_total,
+                                        after_centre=after_centre)
         if overlap:
             (ref, info), pending = on_side(ref_frame_setup)
         else:
@@ -791,12 +799,13 @@ def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, 
         if n_local:
             sweep(RMSF_MODE_SUM, total, None, ref, info, xf_first, pending)   # RMSF.py:91-103
         elif pending is not None:
-            main.wait_event(pending)
+            main.wait_event(pending[1])
         pending = None
         parallel.allreduce_sum_ordered_(eng, total)             # RMSF.py:110, rank order
 
-        def ref_avg_setup():                                    # RMSF.py:111 + 113-118
-            return eng.reference_setup_seq(n_sel, mass_total, total=total, n_frames=float(n_total), masses=m_dev)
+        def ref_avg_setup(after_centre=None):                   # RMSF.py:111 + 113-118
+            return eng.reference_setup_seq(n_sel, mass_total, total=total, n_frames=float(n_total), masses=m_dev,
+                                           after_centre=after_centre)
         if overlap:
             (average, ref, info), pending = on_side(ref_avg_setup)
         else:
@@ -805,7 +814,7 @@ def _run_exact(eng: Engine, source, frames: FrameList, max_batch, block, timer, 
     if n_local:
         sweep(RMSF_MODE_WELFORD, mean, ss, ref, info, xf_last, pending)  # RMSF.py:123-138
     elif pending is not None:
-        main.wait_event(pending)
+        main.wait_event(pending[1])
     if size > 1:                                                # RMSF.py:141-143, comm.reduce's order
         with _span(timer, "merge"):
             mean, ss = parallel.global_chan_exact(eng, mean, ss, [e - s for s, e in blocks], root, merge_order)

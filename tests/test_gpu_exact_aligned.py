@@ -240,6 +240,54 @@ def test_exact_aligned_graph_and_split_superpose(align, overlap, monkeypatch):
     _same(b.cpu().numpy(), a.cpu().numpy(), "split superposition")
 
 
+@pytest.mark.parametrize("n_atoms,step,masses", [(3000, 5, True), (20000, 1, False), (60000, 3, True)])
+def test_exact_split_entry_points(n_atoms, step, masses):
+    """The halves the side stream runs, against the whole calls, bit for bit:
+    rmsf_reference_centre_sequential + rmsf_reference_sums_sequential ==
+    rmsf_reference_setup_sequential (from a frame and from sweep-1 sums),
+    and rmsf_inner_product_sequential + rmsf_superpose_sequential_qcp ==
+    rmsf_superpose_sequential_from_com -- below and above the 16,384 atoms
+    from which the reference's fill and centring run grid-wide."""
+    from rmsf_amd._lib import RMSF_XFORM_DOUBLES
+    from rmsf_amd.engine import Engine
+    from rmsf_amd.synth import motion_table
+    nf = 6
+    traj = torch.tensor(SY.frames(81, n_atoms, 0, nf, motion_table(82, nf)), device="cuda")
+    sel = np.arange(1, n_atoms, step) if step > 1 else None
+    ns = n_atoms if sel is None else len(sel)
+    m = np.random.default_rng(83).uniform(1.0, 16.0, ns) if masses else None
+    md = torch.tensor(m, device="cuda") if masses else None
+    mt = float(m.sum()) if masses else float(ns)
+    eng = Engine()
+    st = eng.sel_tensor(sel) if sel is not None else None
+    marks = []  # (the record is info[:16]; the rest is the frame-parallel setup's scratch)
+    _, r1, i1 = eng.reference_setup_seq(ns, mt, frame_ptr=traj.data_ptr(), sel=st, masses=md)
+    _, r2, i2 = eng.reference_setup_seq(ns, mt, frame_ptr=traj.data_ptr(), sel=st, masses=md,
+                                        after_centre=lambda: marks.append(1))
+    total = (traj[:, torch.as_tensor(sel, device="cuda")] if sel is not None else traj).to(torch.float64).sum(0).reshape(-1).contiguous()
+    a1, r3, i3 = eng.reference_setup_seq(ns, mt, total=total, n_frames=float(nf), masses=md)
+    a2, r4, i4 = eng.reference_setup_seq(ns, mt, total=total, n_frames=float(nf), masses=md,
+                                         after_centre=lambda: marks.append(2))
+    x1 = eng.empty(nf, RMSF_XFORM_DOUBLES)
+    x2 = eng.empty(nf, RMSF_XFORM_DOUBLES)
+    fs = 3 * n_atoms
+    eng.frame_com_seq(traj.data_ptr(), fs, nf, ns, st, md, mt, x1)
+    x2.copy_(x1)
+    eng.superpose_seq_from_com(traj.data_ptr(), fs, nf, ns, st, r1, i1, x1)
+    eng.inner_product_seq(traj.data_ptr(), fs, nf, ns, st, r1, x2)
+    eng.superpose_seq_qcp(nf, ns, i1, x2)
+    torch.cuda.synchronize()
+    assert marks == [1, 2]
+    for got, want, what in ((r2, r1, "ref"), (i2[:16], i1[:16], "record"), (r4, r3, "ref, average"),
+                            (i4[:16], i3[:16], "record, average"), (a2, a1, "average"), (x2, x1, "records")):
+        _same(got.cpu().numpy(), want.cpu().numpy(), what)
+    # and the oracle's reference (RMSF.py:84-85): COM atom by atom, centred
+    xs = traj[0].cpu().numpy()[sel] if sel is not None else traj[0].cpu().numpy()
+    com, rc = O.centred_reference(xs, m)
+    _same(i1.cpu().numpy()[:3], np.asarray(com), "ref_com vs oracle")
+    _same(r1.cpu().numpy(), rc, "centred ref vs oracle")
+
+
 @pytest.mark.parametrize("align", ["frame0", "average"])
 def test_exact_transforms_and_rmsd(align):
     """The per-frame records of the last sweep: rotation, mobile COM and the

@@ -9,7 +9,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_exact_aligned.py tests/test
 tail -1 $O/tests.log
 timeout -k 10 400 python -u tools/probe_exact_aligned.py 2 > $O/cur.txt 2>&1 || { tail -5 $O/cur.txt; exit 1; }
 grep -v amdgpu $O/cur.txt
-if [ -n "$1" ]; then
+if [ -n "$1" ] && [ "$1" != "-" ]; then
   RMSF_AB_LIB=tools/_ab/librmsf_$1.so timeout -k 10 600 python -u tools/probe_exact_aligned.py 1 > $O/$1.txt 2>&1 || { tail -5 $O/$1.txt; exit 1; }
   grep -v amdgpu $O/$1.txt
 fi
