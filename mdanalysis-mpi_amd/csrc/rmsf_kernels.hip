@@ -705,6 +705,19 @@ __global__ __launch_bounds__(kBlock) void k_welford_seq_atoms(const float *__res
 // private to the wave.
 constexpr int kSeqK = 16;             // atoms per lane per block (4 / 8 / 16 measured: 16 ~7 % faster)
 constexpr int kSeqBlk = 64 * kSeqK;   // atoms per block
+// A chain is issue-bound: two chain waves on one SIMD run at half speed each
+// (ubench_chain2 V5: 2.05 -> 3.8 ns per add).  So the reference's workgroup
+// (four chains) holds nearly all of its CU's LDS, and a launch of at most
+// kSeqReserveMax chain waves reserves kSeqReserve bytes of LDS per wave
+// beside its 8 KB slice (40 KB in all), so at most four share a CU, one per
+// SIMD.  Above that the reservation cost more than it saved (the waves fill
+// the CUs unevenly and some wait a whole chain): 100k atoms x 100 frames'
+// 1,000 InnerProduct chains 0.96 ms unreserved against 1.2, 1M x 32's 320
+// 5.7 against 7.3 ms (profiles/r06_workloads/exact_chain_dpp.txt).
+constexpr int kRefSlice = 4 * kSeqBlk + kSeqBlk / 2;
+constexpr size_t kSeqReserve = 4 * kSeqBlk * sizeof(double);
+constexpr int64_t kSeqReserveMax = 768;
+inline size_t seq_reserve(int64_t waves) { return waves <= kSeqReserveMax ? kSeqReserve : 0; }
 // s += the group's 32 terms (lane 0's pair first), in order.  The opening
 // s_nop 1: a DPP read of a VGPR needs 2 wait states after a VALU write, and
 // hipcc pads nothing inside an asm string.  The adds follow each other with
@@ -860,7 +873,7 @@ __global__ __launch_bounds__(kBlock) void k_ref_seq(const float *__restrict__ fr
                                                     double *__restrict__ avg_out, double *__restrict__ ref,
                                                     double *__restrict__ info) {
   __shared__ double com[3];
-  __shared__ double slice[kBlock / 64][kSeqBlk];
+  __shared__ double slice[kBlock / 64][kRefSlice];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool lead = (threadIdx.x & 63) == 0;
   if (PART == kRefAll || PART == kRefCentre) {
@@ -3377,8 +3390,10 @@ RMSF_EXPORT int rmsf_frame_com_sequential(const float *d_xyz, int64_t fstride, i
   hipStream_t s = S(stream);
   const bool g = d_sel != nullptr, m = d_masses != nullptr;
   const dim3 gc((unsigned)n_frames, 3);
-#define SEQCOM(G, M) \
-  hipLaunchKernelGGL((k_seq_com<G, M>), gc, dim3(64), 0, s, d_xyz, fstride, n_sel, d_sel, d_masses, mass_total, d_xform)
+  const size_t lds = seq_reserve(3 * n_frames);
+#define SEQCOM(G, M)                                                                                              \
+  hipLaunchKernelGGL((k_seq_com<G, M>), gc, dim3(64), lds, s, d_xyz, fstride, n_sel, d_sel, d_masses, mass_total, \
+                     d_xform)
   if (g && m) SEQCOM(true, true);
   else if (g) SEQCOM(true, false);
   else if (m) SEQCOM(false, true);
@@ -3395,10 +3410,11 @@ RMSF_EXPORT int rmsf_inner_product_sequential(const float *d_xyz, int64_t fstrid
   if (n_frames == 0) return RMSF_OK;
   hipStream_t s = S(stream);
   const dim3 gi((unsigned)n_frames, 10);
+  const size_t lds = seq_reserve(10 * n_frames);
   if (d_sel)
-    hipLaunchKernelGGL((k_seq_ip<true>), gi, dim3(64), 0, s, d_xyz, fstride, n_sel, d_sel, d_ref, d_xform);
+    hipLaunchKernelGGL((k_seq_ip<true>), gi, dim3(64), lds, s, d_xyz, fstride, n_sel, d_sel, d_ref, d_xform);
   else
-    hipLaunchKernelGGL((k_seq_ip<false>), gi, dim3(64), 0, s, d_xyz, fstride, n_sel, d_sel, d_ref, d_xform);
+    hipLaunchKernelGGL((k_seq_ip<false>), gi, dim3(64), lds, s, d_xyz, fstride, n_sel, d_sel, d_ref, d_xform);
   return after_launch("k_seq_ip");
 }
 
