@@ -715,9 +715,21 @@ constexpr int kSeqBlk = 64 * kSeqK;   // atoms per block
 // 1,000 InnerProduct chains 0.96 ms unreserved against 1.2, 1M x 32's 320
 // 5.7 against 7.3 ms (profiles/r06_workloads/exact_chain_dpp.txt).
 constexpr int kRefSlice = 4 * kSeqBlk + kSeqBlk / 2;
+// At most kSeqPcMax chains a launch runs each chain as a two-wave workgroup
+// (pc_seq_sum: one wave forms the terms, one adds them) with 16 KB + 56 KB of
+// LDS, at most two per CU; up to kSeqReserveMax as one wave with 8 KB + 32 KB,
+// at most four per CU; above that one wave, unreserved.  (Two-wave chains
+// at 1M atoms x 32 frames: 5.54 against 5.91 ms; at 100k x 100's 1,000
+// InnerProduct chains, where the doubled wave count shares SIMDs, 1.16
+// against 1.10: profiles/r06_workloads/exact_pc_ab.txt.)
+constexpr int64_t kSeqPcMax = 512;
+constexpr size_t kSeqPcReserve = 7 * kSeqBlk * sizeof(double);
 constexpr size_t kSeqReserve = 4 * kSeqBlk * sizeof(double);
 constexpr int64_t kSeqReserveMax = 768;
-inline size_t seq_reserve(int64_t waves) { return waves <= kSeqReserveMax ? kSeqReserve : 0; }
+inline bool seq_pc(int64_t chains) { return chains <= kSeqPcMax; }
+inline size_t seq_reserve(int64_t chains) {
+  return seq_pc(chains) ? kSeqPcReserve : chains <= kSeqReserveMax ? kSeqReserve : 0;
+}
 // s += the group's 32 terms (lane 0's pair first), in order.  The opening
 // s_nop 1: a DPP read of a VGPR needs 2 wait states after a VALU write, and
 // hipcc pads nothing inside an asm string.  The adds follow each other with
@@ -736,13 +748,39 @@ __device__ __forceinline__ double row_add32(double s, const double2 &u, double o
   return s;
 }
 #undef RMSF_ROW_FMAC
+// The chain over one parked block: s += its cnt terms in order (whole
+// groups of 32; the caller pads the last group with +0.0).  Lane i of a row
+// reads the pair 2i, 2i + 1 of each group.
+__device__ __forceinline__ double chain_block(double s, const double *lds, int cnt) {
+  const double one = 1.0;
+  const double2 *pair = reinterpret_cast<const double2 *>(lds) + (threadIdx.x & 15);
+  constexpr int NG = kSeqBlk / 32;
+  if (cnt == kSeqBlk) {  // two groups' reads in flight while one is added
+    double2 u[3];
+    u[0] = pair[0];
+    u[1] = pair[16];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (g + 2 < NG) u[(g + 2) % 3] = pair[16 * (g + 2)];
+      __builtin_amdgcn_sched_barrier(0);
+      s = row_add32(s, u[g % 3], one);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {  // the ragged last block: its groups, the last one padded with +0.0
+    const int ng = (cnt + 31) / 32;
+    double2 u = pair[0];
+    for (int g = 0; g < ng; ++g) {
+      const double2 w = u;
+      if (g + 1 < ng) u = pair[16 * (g + 1)];
+      s = row_add32(s, w, one);
+    }
+  }
+  return s;
+}
 template <class Load, class Term>
 __device__ __forceinline__ double wave_seq_sum(int64_t n, double *lds, Load load, Term term) {
   using Raw = decltype(load(int64_t(0)));
   const int lane = threadIdx.x & 63;
-  const double one = 1.0;
-  // lane i of a row reads the pair 2i, 2i + 1 of each 32-term group
-  const double2 *pair = reinterpret_cast<const double2 *>(lds) + (lane & 15);
   Raw va[kSeqK], vb[kSeqK];
   double s = 0.0;
   // whole blocks: unclamped indices, so one base and constant offsets per
@@ -768,28 +806,7 @@ __device__ __forceinline__ double wave_seq_sum(int64_t n, double *lds, Load load
       for (int j = 0; j < kSeqK; ++j) lds[lane + 64 * j] = b + 64 * j < n ? term(v[j], b + 64 * j) : 0.0;
     }
     __builtin_amdgcn_wave_barrier();  // one wave: its LDS operations complete in order
-    const int cnt = (int)min((int64_t)kSeqBlk, n - a0);
-    constexpr int NG = kSeqBlk / 32;
-    if (cnt == kSeqBlk) {  // two groups' reads in flight while one is added
-      double2 u[3];
-      u[0] = pair[0];
-      u[1] = pair[16];
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        if (g + 2 < NG) u[(g + 2) % 3] = pair[16 * (g + 2)];
-        __builtin_amdgcn_sched_barrier(0);
-        s = row_add32(s, u[g % 3], one);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    } else {  // the ragged last block: its groups, the last one padded with +0.0
-      const int ng = (cnt + 31) / 32;
-      double2 u = pair[0];
-      for (int g = 0; g < ng; ++g) {
-        const double2 w = u;
-        if (g + 1 < ng) u = pair[16 * (g + 1)];
-        s = row_add32(s, w, one);
-      }
-    }
+    s = chain_block(s, lds, (int)min((int64_t)kSeqBlk, n - a0));
     __builtin_amdgcn_wave_barrier();  // the slice is rewritten by the next block
   };
   fill(va, 0);
@@ -803,6 +820,70 @@ __device__ __forceinline__ double wave_seq_sum(int64_t n, double *lds, Load load
   fill(vb, a0 + kSeqBlk);
   run(va, a0);
   if (a0 + kSeqBlk < n) run(vb, a0 + kSeqBlk);
+  return s;
+}
+
+// pc_seq_sum: wave_seq_sum split over a workgroup of two waves (round 6).
+// Wave 1 loads block b + 1 and parks its terms in one LDS buffer while wave
+// 0 adds block b's from the other, so the chain wave issues nothing but its
+// reads and adds; one barrier per block.  Same loads, terms and order, so
+// the same bits.  s is wave 0's.  buf: two kSeqBlk-double buffers.
+template <class Load, class Term>
+__device__ __forceinline__ double pc_seq_sum(int64_t n, double (*buf)[kSeqBlk], Load load, Term term) {
+  using Raw = decltype(load(int64_t(0)));
+  const bool chain = threadIdx.x < 64;  // wave-uniform
+  const int lane = threadIdx.x & 63;
+  const int64_t nb = (n + kSeqBlk - 1) / kSeqBlk;
+  Raw va[kSeqK], vb[kSeqK];
+  double s = 0.0;
+  auto fill = [&](Raw(&v)[kSeqK], int64_t blk) {
+    const int64_t a0 = blk * kSeqBlk, b = a0 + lane;
+    if (a0 + kSeqBlk <= n) {
+#pragma unroll
+      for (int j = 0; j < kSeqK; ++j) v[j] = load(b + 64 * j);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kSeqK; ++j) v[j] = load(min(b + 64 * j, n - 1));
+    }
+  };
+  auto park = [&](const Raw(&v)[kSeqK], int64_t blk) {
+    double *lds = buf[blk & 1];
+    const int64_t a0 = blk * kSeqBlk, b = a0 + lane;
+    if (a0 + kSeqBlk <= n) {
+#pragma unroll
+      for (int j = 0; j < kSeqK; ++j) lds[lane + 64 * j] = term(v[j], b + 64 * j);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kSeqK; ++j) lds[lane + 64 * j] = b + 64 * j < n ? term(v[j], b + 64 * j) : 0.0;
+    }
+  };
+  auto cnt = [&](int64_t blk) { return (int)min((int64_t)kSeqBlk, n - blk * kSeqBlk); };
+  if (!chain) {
+    fill(va, 0);
+    fill(vb, 1);
+    park(va, 0);
+    fill(va, 2);
+  }
+  __syncthreads();
+  // step b: the chain adds block b; wave 1 parks block b + 1 (loaded two
+  // steps ago) and issues block b + 3's loads into the same registers
+  for (int64_t b = 0; b < nb; b += 2) {
+    if (chain) {
+      s = chain_block(s, buf[b & 1], cnt(b));
+    } else if (b + 1 < nb) {
+      park(vb, b + 1);
+      fill(vb, b + 3);
+    }
+    __syncthreads();
+    if (b + 1 >= nb) break;
+    if (chain) {
+      s = chain_block(s, buf[(b + 1) & 1], cnt(b + 1));
+    } else if (b + 2 < nb) {
+      park(va, b + 2);
+      fill(va, b + 4);
+    }
+    __syncthreads();
+  }
   return s;
 }
 
@@ -928,26 +1009,38 @@ __global__ __launch_bounds__(kBlock) void k_ref_seq(const float *__restrict__ fr
 //     [0..8], G1 in [13];
 //   k_seq_qcp: E0 = (G1 + G2) * 0.5 and the QCP solve -> R in [0..8], rmsd in
 //     [12], [13..15] zero.
-template <bool GATHER, bool MASSES>
-__global__ __launch_bounds__(64) void k_seq_com(const float *__restrict__ xyz, int64_t fstride, int64_t n_sel,
-                                                const int32_t *__restrict__ sel, const double *__restrict__ masses,
-                                                double mass_total, double *__restrict__ xform) {
-  __shared__ double slice[kSeqBlk];
+// the frames' chains: seq_sum_in(slice, n, load, term), two waves (PC) or one
+template <class Load, class Term>
+__device__ __forceinline__ double seq_sum_in(double (*buf)[kSeqBlk], int64_t n, Load load, Term term) {
+  return pc_seq_sum(n, buf, load, term);
+}
+template <class Load, class Term>
+__device__ __forceinline__ double seq_sum_in(double *buf, int64_t n, Load load, Term term) {
+  return wave_seq_sum(n, buf, load, term);
+}
+#define RMSF_SEQ_SUM(...) seq_sum_in(slice, __VA_ARGS__)
+#define RMSF_SEQ_SLICE __shared__ std::conditional_t<PC, double[2][kSeqBlk], double[kSeqBlk]> slice
+
+template <bool GATHER, bool MASSES, bool PC>
+__global__ __launch_bounds__(PC ? 128 : 64) void k_seq_com(const float *__restrict__ xyz, int64_t fstride,
+                                                           int64_t n_sel, const int32_t *__restrict__ sel,
+                                                           const double *__restrict__ masses, double mass_total,
+                                                           double *__restrict__ xform) {
+  RMSF_SEQ_SLICE;
   const int64_t f = blockIdx.x;
   const int c = blockIdx.y;
   const float *__restrict__ fr = xyz + f * fstride + c;
-  const double s = wave_seq_sum(
-      n_sel, slice,
-      [&](int64_t a) { return SeqF1D{fr[3 * (GATHER ? (int64_t)sel[a] : a)], MASSES ? masses[a] : 1.0}; },
+  const double s = RMSF_SEQ_SUM(
+      n_sel, [&](int64_t a) { return SeqF1D{fr[3 * (GATHER ? (int64_t)sel[a] : a)], MASSES ? masses[a] : 1.0}; },
       [&](const SeqF1D &v, int64_t) { return (double)v.x * v.d; });
   if (threadIdx.x == 0) xform[f * kXform + 9 + c] = s / mass_total;
 }
 
-template <bool GATHER>
-__global__ __launch_bounds__(64) void k_seq_ip(const float *__restrict__ xyz, int64_t fstride, int64_t n_sel,
-                                               const int32_t *__restrict__ sel, const double *__restrict__ ref,
-                                               double *__restrict__ xform) {
-  __shared__ double slice[kSeqBlk];
+template <bool GATHER, bool PC>
+__global__ __launch_bounds__(PC ? 128 : 64) void k_seq_ip(const float *__restrict__ xyz, int64_t fstride,
+                                                          int64_t n_sel, const int32_t *__restrict__ sel,
+                                                          const double *__restrict__ ref, double *__restrict__ xform) {
+  RMSF_SEQ_SLICE;
   const int64_t f = blockIdx.x;
   const int j = blockIdx.y;
   const float *__restrict__ fr = xyz + f * fstride;
@@ -957,13 +1050,13 @@ __global__ __launch_bounds__(64) void k_seq_ip(const float *__restrict__ xyz, in
   if (j < 9) {
     const int ax = j / 3, rb = j % 3;
     const double cx = t[9 + ax];
-    s = wave_seq_sum(
-        n_sel, slice, [&](int64_t a) { return SeqF1D{fr[row(a) + ax], ref[3 * a + rb]}; },
+    s = RMSF_SEQ_SUM(
+        n_sel, [&](int64_t a) { return SeqF1D{fr[row(a) + ax], ref[3 * a + rb]}; },
         [&](const SeqF1D &v, int64_t) { return ((double)v.x - cx) * v.d; });
   } else {
     const double c0 = t[9], c1 = t[10], c2 = t[11];
-    s = wave_seq_sum(
-        n_sel, slice,
+    s = RMSF_SEQ_SUM(
+        n_sel,
         [&](int64_t a) {
           const float *p = fr + row(a);
           return SeqF3{p[0], p[1], p[2]};
@@ -975,6 +1068,8 @@ __global__ __launch_bounds__(64) void k_seq_ip(const float *__restrict__ xyz, in
   }
   if (threadIdx.x == 0) xform[f * kXform + (j < 9 ? j : 13)] = s;
 }
+#undef RMSF_SEQ_SUM
+#undef RMSF_SEQ_SLICE
 
 __global__ __launch_bounds__(64) void k_seq_qcp(int64_t n_frames, int64_t n_sel, const double *__restrict__ refinfo,
                                                 double *__restrict__ xform) {
@@ -3391,9 +3486,15 @@ RMSF_EXPORT int rmsf_frame_com_sequential(const float *d_xyz, int64_t fstride, i
   const bool g = d_sel != nullptr, m = d_masses != nullptr;
   const dim3 gc((unsigned)n_frames, 3);
   const size_t lds = seq_reserve(3 * n_frames);
-#define SEQCOM(G, M)                                                                                              \
-  hipLaunchKernelGGL((k_seq_com<G, M>), gc, dim3(64), lds, s, d_xyz, fstride, n_sel, d_sel, d_masses, mass_total, \
-                     d_xform)
+#define SEQCOM(G, M)                                                                                         \
+  do {                                                                                                       \
+    if (seq_pc(3 * n_frames))                                                                                \
+      hipLaunchKernelGGL((k_seq_com<G, M, true>), gc, dim3(128), lds, s, d_xyz, fstride, n_sel, d_sel, d_masses, \
+                         mass_total, d_xform);                                                               \
+    else                                                                                                     \
+      hipLaunchKernelGGL((k_seq_com<G, M, false>), gc, dim3(64), lds, s, d_xyz, fstride, n_sel, d_sel,       \
+                         d_masses, mass_total, d_xform);                                                     \
+  } while (0)
   if (g && m) SEQCOM(true, true);
   else if (g) SEQCOM(true, false);
   else if (m) SEQCOM(false, true);
@@ -3411,10 +3512,16 @@ RMSF_EXPORT int rmsf_inner_product_sequential(const float *d_xyz, int64_t fstrid
   hipStream_t s = S(stream);
   const dim3 gi((unsigned)n_frames, 10);
   const size_t lds = seq_reserve(10 * n_frames);
-  if (d_sel)
-    hipLaunchKernelGGL((k_seq_ip<true>), gi, dim3(64), lds, s, d_xyz, fstride, n_sel, d_sel, d_ref, d_xform);
-  else
-    hipLaunchKernelGGL((k_seq_ip<false>), gi, dim3(64), lds, s, d_xyz, fstride, n_sel, d_sel, d_ref, d_xform);
+#define SEQIP(G, PC) \
+  hipLaunchKernelGGL((k_seq_ip<G, PC>), gi, dim3(PC ? 128 : 64), lds, s, d_xyz, fstride, n_sel, d_sel, d_ref, d_xform)
+  if (seq_pc(10 * n_frames)) {
+    if (d_sel) SEQIP(true, true);
+    else SEQIP(false, true);
+  } else {
+    if (d_sel) SEQIP(true, false);
+    else SEQIP(false, false);
+  }
+#undef SEQIP
   return after_launch("k_seq_ip");
 }
 
