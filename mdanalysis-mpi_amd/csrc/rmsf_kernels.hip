@@ -827,11 +827,14 @@ __device__ __forceinline__ double wave_seq_sum(int64_t n, double *lds, Load load
 // Wave 1 loads block b + 1 and parks its terms in one LDS buffer while wave
 // 0 adds block b's from the other, so the chain wave issues nothing but its
 // reads and adds; one barrier per block.  Same loads, terms and order, so
-// the same bits.  s is wave 0's.  buf: two kSeqBlk-double buffers.
+// the same bits.  s is the chain wave's.  buf: two kSeqBlk-double buffers.
+// chain: whether this wave adds (wave-uniform); several pairs may share a
+// workgroup, each with its own buf, as long as every pair has the same n
+// (the barriers are the workgroup's).
 template <class Load, class Term>
-__device__ __forceinline__ double pc_seq_sum(int64_t n, double (*buf)[kSeqBlk], Load load, Term term) {
+__device__ __forceinline__ double pc_seq_sum(int64_t n, double (*buf)[kSeqBlk], Load load, Term term,
+                                             bool chain = threadIdx.x < 64) {
   using Raw = decltype(load(int64_t(0)));
-  const bool chain = threadIdx.x < 64;  // wave-uniform
   const int lane = threadIdx.x & 63;
   const int64_t nb = (n + kSeqBlk - 1) / kSeqBlk;
   Raw va[kSeqK], vb[kSeqK];
@@ -918,6 +921,7 @@ struct SeqD3 {
 // ~4 ms of a 1M-atom setup's 8.5 (profiles/r06_workloads/exact_chain_dpp.txt).
 constexpr int kRefAll = 0, kRefCentre = 1, kRefCom = 2, kRefSums = 3;
 constexpr int64_t kRefGridMin = 16384;
+constexpr size_t kRefPairsLds = 144 * 1024 - 3 * 2 * 1024 * sizeof(double);  // k_ref_com_pairs' dynamic LDS
 template <bool FROM_F32, bool GATHER>
 __device__ __forceinline__ void ref_fill_atom(int64_t a, const float *__restrict__ frame,
                                               const double *__restrict__ avg, double div,
@@ -947,6 +951,29 @@ __global__ __launch_bounds__(kBlock) void k_ref_centre_grid(int64_t n_coord, con
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i < n_coord) ref[i] = ref[i] - info[i % 3];
 }
+// k_ref_com_pairs: k_ref_seq's part 2 (the reference's three COM chains,
+// which the InnerProduct waits for) from kRefGridMin atoms, each chain a
+// pair of waves (pc_seq_sum: wave c adds, wave c + 3 forms the terms; the
+// adding waves must not share a SIMD, and a CU's waves are dealt to its
+// SIMDs in turn -- pairs as waves 2c / 2c + 1 put two chains on one SIMD
+// and ran 1.25x slower).
+// Launched with kRefPairsLds of LDS so its CU runs nothing else.  Same bits
+// as k_ref_seq's one-wave chains.  (The sums of r and G2 run beside the
+// InnerProduct, off the critical path, and keep one wave each.)
+template <bool MASSES>
+__global__ __launch_bounds__(384) void k_ref_com_pairs(int64_t n_sel, const double *__restrict__ masses,
+                                                       double mass_total, const double *__restrict__ ref,
+                                                       double *__restrict__ info) {
+  __shared__ double buf[3][2][kSeqBlk];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = w % 3;
+  const bool chain = w < 3;  // waves 0-2 add, on three SIMDs; 3-5 form the terms
+  const double s = pc_seq_sum(
+      n_sel, buf[c], [&](int64_t a) { return SeqD1D{ref[3 * a + c], MASSES ? masses[a] : 1.0}; },
+      [&](const SeqD1D &v, int64_t) { return v.x * v.d; }, chain);
+  if (chain && (threadIdx.x & 63) == 0) info[c] = s / mass_total;
+}
+
 template <bool FROM_F32, bool GATHER, bool MASSES, int PART>
 __global__ __launch_bounds__(kBlock) void k_ref_seq(const float *__restrict__ frame, const double *__restrict__ avg,
                                                     double div, int64_t n_sel, const int32_t *__restrict__ sel,
@@ -3431,8 +3458,13 @@ int ref_centre_seq(const float *d_frame, const double *d_avg, double div, int64_
     hipLaunchKernelGGL((k_ref_fill<false, false>), dim3(grid1(n_sel)), dim3(kBlock), 0, s, d_frame, d_avg, div,
                        n_sel, d_sel, d_avg_out, d_ref);
   if (int rc = after_launch("k_ref_fill")) return rc;
-  ref_seq_launch<kRefCom>(d_frame, d_avg, div, n_sel, d_sel, d_masses, mass_total, d_avg_out, d_ref, d_refinfo, s);
-  if (int rc = after_launch("k_ref_seq")) return rc;
+  if (d_masses)
+    hipLaunchKernelGGL((k_ref_com_pairs<true>), dim3(1), dim3(384), kRefPairsLds, s, n_sel, d_masses, mass_total,
+                       d_ref, d_refinfo);
+  else
+    hipLaunchKernelGGL((k_ref_com_pairs<false>), dim3(1), dim3(384), kRefPairsLds, s, n_sel, d_masses, mass_total,
+                       d_ref, d_refinfo);
+  if (int rc = after_launch("k_ref_com_pairs")) return rc;
   hipLaunchKernelGGL(k_ref_centre_grid, dim3(grid1(3 * n_sel)), dim3(kBlock), 0, s, 3 * n_sel, d_refinfo, d_ref);
   return after_launch("k_ref_centre_grid");
 }
