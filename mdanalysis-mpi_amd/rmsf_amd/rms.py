@@ -105,7 +105,7 @@ class RMSF:
         product atom by atom, the sweep-1 sum and Welford frame by frame
         (the rmsf_*_sequential kernels) -- each sum an in-order add chain
         over the atoms, so its cost grows with the selection, not the
-        frames: faster than the default at RMSF.py's 214 atoms, 1.0-1.9 ms
+        frames: about the default's cost at RMSF.py's 214 atoms, 1.0-1.9 ms
         against 0.16-0.29 ms at 100k atoms x 100 frames (DESIGN section 5,
         "Few frames").  The ranks are
         folded by second_order_moments in RMSF.py:143's reduce order
